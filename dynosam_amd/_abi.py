@@ -1,0 +1,123 @@
+"""ctypes mirror of include/dynohip.h and include/dynosynth.h.
+
+Plain struct layouts only; the product binding (dynosam_amd.optimizer) and
+the test-only oracle binding (tests/oracle_binding.py) both use them.
+"""
+import ctypes as C
+
+FACTOR_TYPES = (
+    "pose_to_point",
+    "landmark_motion_ternary",
+    "between",
+    "prior",
+    "landmark_motion_pose",
+    "landmark_pose_smoothing",
+)
+# keys per factor, residual dim, measurement dim, slot kinds (0 pose, 1 point)
+FACTOR_NKEYS = (2, 3, 2, 1, 4, 3)
+FACTOR_DIM = (3, 3, 6, 6, 3, 6)
+FACTOR_MEAS = (3, 0, 12, 12, 0, 0)
+FACTOR_SLOTS = ((0, 1), (1, 1, 0), (0, 0), (0,), (1, 1, 0, 0), (0, 0, 0))
+
+POSE3 = 0
+POINT3 = 1
+
+
+class FactorBlock(C.Structure):
+    _fields_ = [
+        ("n", C.c_size_t),
+        ("keys", C.POINTER(C.c_uint64)),
+        ("measured", C.POINTER(C.c_double)),
+        ("sigmas", C.POINTER(C.c_double)),
+        ("huber_k", C.POINTER(C.c_double)),
+    ]
+
+
+class GraphView(C.Structure):
+    _fields_ = [(name, FactorBlock) for name in FACTOR_TYPES]
+
+
+class LMParams(C.Structure):
+    _fields_ = [
+        ("lambda_initial", C.c_double),
+        ("lambda_factor", C.c_double),
+        ("lambda_upper_bound", C.c_double),
+        ("lambda_lower_bound", C.c_double),
+        ("min_model_fidelity", C.c_double),
+        ("relative_error_tol", C.c_double),
+        ("absolute_error_tol", C.c_double),
+        ("error_tol", C.c_double),
+        ("max_iterations", C.c_int),
+        ("diagonal_damping", C.c_int),
+        ("use_fixed_lambda_factor", C.c_int),
+        ("reserved", C.c_int),
+    ]
+
+    @classmethod
+    def gtsam_default(cls):
+        """gtsam::LevenbergMarquardtParams() defaults (GTSAM 4.2.0)."""
+        return cls(1e-5, 10.0, 1e5, 0.0, 1e-3, 1e-5, 1e-5, 0.0, 100, 0, 1, 0)
+
+
+class LMSummary(C.Structure):
+    _fields_ = [
+        ("iterations", C.c_int),
+        ("inner_iterations", C.c_int),
+        ("initial_error", C.c_double),
+        ("final_error", C.c_double),
+        ("final_lambda", C.c_double),
+        ("converged", C.c_int),
+        ("reserved", C.c_int),
+    ]
+
+
+class TraceEntry(C.Structure):
+    _fields_ = [
+        ("outer_iteration", C.c_int),
+        ("solved", C.c_int),
+        ("accepted", C.c_int),
+        ("stop", C.c_int),
+        ("lambda_", C.c_double),
+        ("current_error", C.c_double),
+        ("new_error", C.c_double),
+        ("old_linear_error", C.c_double),
+        ("new_linear_error", C.c_double),
+        ("model_fidelity", C.c_double),
+    ]
+
+
+class SynthConfig(C.Structure):
+    _fields_ = [
+        ("frames", C.c_int),
+        ("objects", C.c_int),
+        ("static_landmarks", C.c_int),
+        ("dyn_slots", C.c_int),
+        ("static_track_len", C.c_int),
+        ("dyn_track_len", C.c_int),
+        ("seed", C.c_uint64),
+        ("noise_code_defaults", C.c_int),
+        ("object_visible_frames", C.c_int),
+        ("formulation", C.c_int),
+        ("smoothing", C.c_int),
+        ("robust", C.c_int),
+    ]
+
+
+def trace_to_dicts(entries):
+    out = []
+    for e in entries:
+        out.append(
+            dict(
+                outer_iteration=e.outer_iteration,
+                solved=e.solved,
+                accepted=e.accepted,
+                stop=e.stop,
+                lam=e.lambda_,
+                current_error=e.current_error,
+                new_error=e.new_error,
+                old_linear_error=e.old_linear_error,
+                new_linear_error=e.new_linear_error,
+                model_fidelity=e.model_fidelity,
+            )
+        )
+    return out

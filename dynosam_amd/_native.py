@@ -1,0 +1,109 @@
+"""Locate and load the in-tree native libraries.
+
+libdynohip.so (HIP product path) and libdynosynth.so (host-only synthetic
+graph generator) are built in-tree by __graft_entry__.build() into
+dynosam_amd/lib/. There is no fallback: a missing library raises.
+"""
+import ctypes as C
+import os
+
+from . import _abi
+
+LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+_libs = {}
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def lib_path(name):
+    return os.path.join(LIB_DIR, name)
+
+
+def load(name):
+    if name in _libs:
+        return _libs[name]
+    path = lib_path(name)
+    if not os.path.exists(path):
+        raise NativeLibraryMissing(
+            f"{path} not built; run `python -c 'import __graft_entry__ as g; g.build()'`"
+        )
+    lib = C.CDLL(path)
+    _libs[name] = lib
+    _declare(name, lib)
+    return lib
+
+
+def _declare(name, lib):
+    P = C.POINTER
+    if name == "libdynosynth.so":
+        lib.dynosynth_config_default.argtypes = [P(_abi.SynthConfig)]
+        lib.dynosynth_generate.argtypes = [P(_abi.SynthConfig), P(C.c_void_p)]
+        lib.dynosynth_generate.restype = C.c_int
+        lib.dynosynth_destroy.argtypes = [C.c_void_p]
+        lib.dynosynth_graph.argtypes = [C.c_void_p, P(_abi.GraphView)]
+        lib.dynosynth_num_values.argtypes = [C.c_void_p]
+        lib.dynosynth_num_values.restype = C.c_size_t
+        lib.dynosynth_values_len.argtypes = [C.c_void_p]
+        lib.dynosynth_values_len.restype = C.c_size_t
+        lib.dynosynth_value_keys.argtypes = [C.c_void_p]
+        lib.dynosynth_value_keys.restype = P(C.c_uint64)
+        lib.dynosynth_value_kinds.argtypes = [C.c_void_p]
+        lib.dynosynth_value_kinds.restype = P(C.c_uint8)
+        lib.dynosynth_value_data.argtypes = [C.c_void_p]
+        lib.dynosynth_value_data.restype = P(C.c_double)
+        lib.dynosynth_ground_truth.argtypes = [C.c_void_p]
+        lib.dynosynth_ground_truth.restype = P(C.c_double)
+    elif name == "libdynohip.so":
+        vp = C.c_void_p
+        lib.dynohip_abi_version.restype = C.c_int
+        lib.dynohip_lm_params_default.argtypes = [P(_abi.LMParams)]
+        lib.dynohip_create.argtypes = [C.c_int, P(vp)]
+        lib.dynohip_create.restype = C.c_int
+        lib.dynohip_destroy.argtypes = [vp]
+        lib.dynohip_last_error.argtypes = [vp]
+        lib.dynohip_last_error.restype = C.c_char_p
+        lib.dynohip_set_graph.argtypes = [vp, P(_abi.GraphView)]
+        lib.dynohip_set_graph.restype = C.c_int
+        lib.dynohip_set_values.argtypes = [vp, P(C.c_uint64), P(C.c_uint8), P(C.c_double), C.c_size_t]
+        lib.dynohip_set_values.restype = C.c_int
+        lib.dynohip_get_values.argtypes = [vp, P(C.c_double), C.c_size_t]
+        lib.dynohip_get_values.restype = C.c_int
+        lib.dynohip_graph_error.argtypes = [vp, P(C.c_double)]
+        lib.dynohip_graph_error.restype = C.c_int
+        lib.dynohip_lm_reset.argtypes = [vp, P(_abi.LMParams)]
+        lib.dynohip_lm_reset.restype = C.c_int
+        lib.dynohip_iterate.argtypes = [vp, P(_abi.LMSummary)]
+        lib.dynohip_iterate.restype = C.c_int
+        lib.dynohip_optimize.argtypes = [vp, P(_abi.LMParams), P(_abi.LMSummary)]
+        lib.dynohip_optimize.restype = C.c_int
+        lib.dynohip_get_trace.argtypes = [vp, P(_abi.TraceEntry), C.c_size_t, P(C.c_size_t)]
+        lib.dynohip_get_trace.restype = C.c_int
+        lib.dynohip_linearize.argtypes = [vp, P(C.c_double), C.c_size_t]
+        lib.dynohip_linearize.restype = C.c_int
+        lib.dynohip_linearize_size.argtypes = [vp]
+        lib.dynohip_linearize_size.restype = C.c_size_t
+        lib.dynohip_get_phase_times.argtypes = [vp, P(C.c_double), C.c_size_t]
+        lib.dynohip_get_phase_times.restype = C.c_int
+        for fn, args, res in [
+            ("dynohip_symbol", [C.c_ubyte, C.c_uint64], C.c_uint64),
+            ("dynohip_labeled_symbol", [C.c_ubyte, C.c_ubyte, C.c_uint64], C.c_uint64),
+            ("dynohip_symbol_chr", [C.c_uint64], C.c_ubyte),
+            ("dynohip_symbol_index", [C.c_uint64], C.c_uint64),
+            ("dynohip_labeled_label", [C.c_uint64], C.c_ubyte),
+            ("dynohip_labeled_index", [C.c_uint64], C.c_uint64),
+            ("dynohip_cantor_pair", [C.c_uint64, C.c_uint64], C.c_uint64),
+            ("dynohip_cantor_depair", [C.c_uint64, P(C.c_uint64), P(C.c_uint64)], None),
+            ("dynohip_camera_pose_key", [C.c_uint64], C.c_uint64),
+            ("dynohip_static_landmark_key", [C.c_int64], C.c_uint64),
+            ("dynohip_dynamic_landmark_key", [C.c_uint64, C.c_int64, P(C.c_uint64)], C.c_int),
+            ("dynohip_object_motion_key", [C.c_int, C.c_uint64], C.c_uint64),
+            ("dynohip_object_pose_key", [C.c_int, C.c_uint64], C.c_uint64),
+            ("dynohip_reconstruct_motion_info", [C.c_uint64, P(C.c_int), P(C.c_uint64)], C.c_int),
+            ("dynohip_reconstruct_pose_info", [C.c_uint64, P(C.c_int), P(C.c_uint64)], C.c_int),
+            ("dynohip_chr_extract", [C.c_uint64], C.c_ubyte),
+        ]:
+            f = getattr(lib, fn)
+            f.argtypes = args
+            f.restype = res
