@@ -1,0 +1,82 @@
+// kernels.hpp — device data views and launchers for the HIP hot path.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "plan.hpp"
+
+namespace dynohip {
+
+struct TypeDev {
+  int n = 0;
+  uint64_t base = 0;
+  uint32_t stride = 0;
+  const int32_t* idx = nullptr;
+  const double* meas = nullptr;
+  const double* isig = nullptr;
+  const double* hk = nullptr;
+};
+
+struct GatherDev {
+  int n = 0;
+  const int64_t* start = nullptr;
+  const GEntry* ent = nullptr;
+};
+
+struct ChainDev {
+  int n_comp = 0;
+  int n_nb = 0;
+  const int32_t* comp_start = nullptr;
+  const int32_t* comp_nb_start = nullptr;
+  const int32_t* nb_comp = nullptr;
+  const int64_t* comp_y_base = nullptr;
+  const int32_t* nbedge_start = nullptr;
+  const int32_t* nbedge_pt = nullptr;
+  const uint32_t* nbedge_w = nullptr;
+  const int32_t* pt_edge_start = nullptr;
+  const int32_t* edge_pose = nullptr;
+  uint64_t off_D = 0, off_E = 0, off_gp = 0, off_W = 0, off_v = 0, off_L = 0, off_M = 0;
+};
+
+struct BandDev {
+  int NT = 0;
+  int n_red = 0;
+  double* band = nullptr;
+  const int64_t* off = nullptr;
+  const int32_t* D = nullptr;
+  const int32_t* cmin = nullptr;
+};
+
+// ---- launchers (all asynchronous on `s`) ----
+void launch_linearize(int type, const TypeDev& t, const double* pose, const double* pt, double* arena, hipStream_t s);
+// per-factor nonlinear error, block partial sums written at partials[0..]
+int error_blocks(int n);
+void launch_error(int type, const TypeDev& t, const double* pose, const double* pt, double* partials, hipStream_t s);
+// 0.5 || J delta - b ||^2 per factor (delta null -> 0.5||b||^2)
+void launch_linerr(int type, const TypeDev& t, const double* arena, const double* dpose, const double* dpt,
+                   double* partials, hipStream_t s);
+void launch_reduce(const double* partials, int n, double* out, hipStream_t s);
+
+// point-side gathers (thread per target), dst = arena + off
+void launch_gather_3x3(const GatherDev& g, const double* arena, double* dst, hipStream_t s);
+void launch_gather_3x1(const GatherDev& g, const double* arena, double* dst, hipStream_t s);
+void launch_gather_3x6(const GatherDev& g, const double* arena, double* dst, hipStream_t s);
+// reduced system (wave per target)
+void launch_gather_band(const GatherDev& g, const double* arena, const int32_t* tA, const int32_t* tB,
+                        const BandDev& b, double lambda, hipStream_t s);
+void launch_gather_grad(const GatherDev& g, const double* arena, double* gred, hipStream_t s);
+
+void launch_chain_factor(const ChainDev& c, double* arena, double lambda, int* fail, hipStream_t s);
+void launch_chain_solve_y(const ChainDev& c, double* arena, hipStream_t s);
+void launch_backsub(const ChainDev& c, const double* arena, const double* dpose, double* dpt, hipStream_t s);
+
+void launch_band_pad(const BandDev& b, hipStream_t s);
+void launch_band_cholesky(const BandDev& b, const int32_t* host_D, int* fail, hipStream_t s);
+void launch_band_solve(const BandDev& b, const double* g, double* y, double* x, hipStream_t s);
+
+void launch_retract(int n_pose, int n_pt, const double* pose, const double* pt, const double* dpose,
+                    const double* dpt, double* pose_out, double* pt_out, hipStream_t s);
+
+}  // namespace dynohip

@@ -1,0 +1,419 @@
+// plan.cpp — factor graph -> device layout / gather lists (see plan.hpp).
+#include "plan.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <unordered_map>
+
+namespace dynohip {
+
+namespace {
+
+struct PoseSortKey {
+  uint64_t frame;
+  unsigned chr, label;
+  uint64_t key;
+  int32_t user;
+};
+
+// frame order of a pose key: X(k) -> k; LabeledSymbol H/L(j,k) -> k
+// (BackendDefinitions.hpp:57-88)
+PoseSortKey pose_sort_key(uint64_t key, int32_t user) {
+  PoseSortKey s;
+  s.key = key;
+  s.user = user;
+  s.chr = static_cast<unsigned>(key >> 56);
+  const unsigned l = static_cast<unsigned>((key >> 48) & 0xff);
+  if (s.chr > 0 && l > 0) {
+    s.label = l;
+    s.frame = key & ((1ULL << 48) - 1);
+  } else {
+    s.label = 0;
+    s.frame = key & ((1ULL << 56) - 1);
+  }
+  return s;
+}
+
+uint32_t block_off(const TypePlan& tp, int type, int i, int slot) {
+  return static_cast<uint32_t>(tp.base + static_cast<uint64_t>(tp.stride) * i +
+                               static_cast<uint64_t>(kDim[type]) * kColStart[type][slot]);
+}
+uint32_t b_off(const TypePlan& tp, int type, int i) {
+  return static_cast<uint32_t>(tp.base + static_cast<uint64_t>(tp.stride) * i +
+                               static_cast<uint64_t>(kDim[type]) * kCols[type]);
+}
+
+// build a CSR gather list from (target, entry) pairs, stable in generation order
+void to_csr(size_t ntargets, std::vector<std::pair<int32_t, GEntry>>& pairs, GatherList& out) {
+  out.start.assign(ntargets + 1, 0);
+  for (auto& p : pairs) out.start[p.first + 1]++;
+  for (size_t t = 0; t < ntargets; ++t) out.start[t + 1] += out.start[t];
+  out.ent.resize(pairs.size());
+  std::vector<int64_t> cur(out.start.begin(), out.start.end() - 1);
+  for (auto& p : pairs) out.ent[cur[p.first]++] = p.second;
+  pairs.clear();
+  pairs.shrink_to_fit();
+}
+
+}  // namespace
+
+int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t* kind, size_t n, Plan& P,
+               std::string& err) {
+  P = Plan();
+  // ---- values: key lookup ----
+  std::unordered_map<uint64_t, int32_t> key_to_user;
+  key_to_user.reserve(n * 2 + 1);
+  for (size_t i = 0; i < n; ++i) {
+    if (kind[i] > 1) { err = "bad value kind"; return DYNOHIP_EINVAL; }
+    if (!key_to_user.emplace(keys[i], static_cast<int32_t>(i)).second) { err = "duplicate value key"; return DYNOHIP_EINVAL; }
+  }
+  P.user_kind.assign(kind, kind + n);
+  P.user_idx.assign(n, -1);
+
+  const dynohip_factor_block* blocks[kNTypes] = {&g.pose_to_point, &g.landmark_motion_ternary, &g.between,
+                                                 &g.prior, &g.landmark_motion_pose, &g.landmark_pose_smoothing};
+  // user index per factor slot
+  std::vector<int32_t> fuser[kNTypes];
+  for (int t = 0; t < kNTypes; ++t) {
+    const auto* b = blocks[t];
+    if (b->n == 0) continue;
+    if (!b->keys || !b->sigmas || (kMeasDim[t] > 0 && !b->measured)) {
+      err = "factor type " + std::to_string(t) + ": null keys/sigmas/measured";
+      return DYNOHIP_EINVAL;
+    }
+    fuser[t].resize(b->n * kNKeys[t]);
+    for (size_t i = 0; i < b->n; ++i)
+      for (int s = 0; s < kNKeys[t]; ++s) {
+        const uint64_t key = b->keys[i * kNKeys[t] + s];
+        auto it = key_to_user.find(key);
+        if (it == key_to_user.end()) {
+          err = "factor type " + std::to_string(t) + " #" + std::to_string(i) + ": key " + std::to_string(key) +
+                " does not exist in the values";
+          return DYNOHIP_EKEY;
+        }
+        const int want = kSlotKind[t][s] == 0 ? DYNOHIP_POSE3 : DYNOHIP_POINT3;
+        if (kind[it->second] != want) {
+          err = "factor type " + std::to_string(t) + " #" + std::to_string(i) + ": key has wrong value kind";
+          return DYNOHIP_EINVAL;
+        }
+        fuser[t][i * kNKeys[t] + s] = it->second;
+      }
+    for (size_t i = 0; i < b->n * kDim[t]; ++i)
+      if (!(b->sigmas[i] > 0.0) || !std::isfinite(b->sigmas[i])) { err = "non-positive sigma"; return DYNOHIP_EINVAL; }
+    for (size_t i = 0; i < b->n * kMeasDim[t]; ++i)
+      if (!std::isfinite(b->measured[i])) { err = "non-finite measurement"; return DYNOHIP_ENONFINITE; }
+  }
+
+  // ---- poses: frame order ----
+  {
+    std::vector<PoseSortKey> ps;
+    for (size_t i = 0; i < n; ++i)
+      if (kind[i] == DYNOHIP_POSE3) ps.push_back(pose_sort_key(keys[i], static_cast<int32_t>(i)));
+    std::sort(ps.begin(), ps.end(), [](const PoseSortKey& a, const PoseSortKey& b) {
+      if (a.frame != b.frame) return a.frame < b.frame;
+      if (a.chr != b.chr) return a.chr < b.chr;
+      if (a.label != b.label) return a.label < b.label;
+      return a.key < b.key;
+    });
+    P.n_pose = static_cast<int>(ps.size());
+    P.pose_key.resize(ps.size());
+    for (size_t r = 0; r < ps.size(); ++r) {
+      P.user_idx[ps[r].user] = static_cast<int32_t>(r);
+      P.pose_key[r] = ps[r].key;
+    }
+  }
+
+  // ---- point chains ----
+  // adjacency between points from factors with two point slots
+  std::vector<std::vector<int32_t>> adj(n);
+  for (int t = 0; t < kNTypes; ++t) {
+    const int nk = kNKeys[t];
+    int ps[4], np = 0;
+    for (int s = 0; s < nk; ++s)
+      if (kSlotKind[t][s] == 1) ps[np++] = s;
+    if (np < 2) continue;
+    if (np > 2) { err = "factor with >2 point slots unsupported"; return DYNOHIP_ESTRUCT; }
+    for (size_t i = 0; i < blocks[t]->n; ++i) {
+      const int32_t a = fuser[t][i * nk + ps[0]], b = fuser[t][i * nk + ps[1]];
+      if (a == b) { err = "factor links a point to itself"; return DYNOHIP_ESTRUCT; }
+      adj[a].push_back(b);
+      adj[b].push_back(a);
+    }
+  }
+  for (auto& a : adj) {
+    std::sort(a.begin(), a.end());
+    a.erase(std::unique(a.begin(), a.end()), a.end());
+  }
+  {
+    std::vector<char> seen(n, 0);
+    int32_t next_pt = 0;
+    P.comp_start.push_back(0);
+    for (size_t i = 0; i < n; ++i) {
+      if (kind[i] != DYNOHIP_POINT3 || seen[i]) continue;
+      // collect component
+      std::vector<int32_t> comp{static_cast<int32_t>(i)};
+      seen[i] = 1;
+      size_t nedges2 = 0;
+      for (size_t q = 0; q < comp.size(); ++q) {
+        const int32_t u = comp[q];
+        nedges2 += adj[u].size();
+        if (adj[u].size() > 2) { err = "point component is not a chain (degree > 2)"; return DYNOHIP_ESTRUCT; }
+        for (int32_t w : adj[u])
+          if (!seen[w]) { seen[w] = 1; comp.push_back(w); }
+      }
+      if (nedges2 / 2 != comp.size() - 1) { err = "point component is not a chain (cycle)"; return DYNOHIP_ESTRUCT; }
+      // endpoint with the smallest key
+      int32_t start = -1;
+      for (int32_t u : comp)
+        if (adj[u].size() <= 1 && (start < 0 || keys[u] < keys[start])) start = u;
+      int32_t prev = -1, cur = start;
+      for (size_t q = 0; q < comp.size(); ++q) {
+        P.user_idx[cur] = next_pt++;
+        P.pt_key.push_back(keys[cur]);
+        int32_t nxt = -1;
+        for (int32_t w : adj[cur])
+          if (w != prev) nxt = w;
+        prev = cur;
+        cur = nxt;
+      }
+      P.comp_start.push_back(next_pt);
+      P.max_chain = std::max(P.max_chain, static_cast<int>(comp.size()));
+    }
+    P.n_pt = next_pt;
+    P.n_comp = static_cast<int>(P.comp_start.size()) - 1;
+  }
+  std::vector<int32_t> comp_of(P.n_pt);
+  for (int c = 0; c < P.n_comp; ++c)
+    for (int32_t i = P.comp_start[c]; i < P.comp_start[c + 1]; ++i) comp_of[i] = c;
+
+  // ---- factor types: indices, measurements, arena records ----
+  uint64_t arena = 0;
+  for (int t = 0; t < kNTypes; ++t) {
+    TypePlan& tp = P.types[t];
+    const auto* b = blocks[t];
+    tp.n = static_cast<int>(b->n);
+    tp.stride = static_cast<uint32_t>((kDim[t] * (kCols[t] + 1) + 1) & ~1);
+    tp.base = arena;
+    arena += static_cast<uint64_t>(tp.stride) * tp.n;
+    tp.idx.resize(b->n * kNKeys[t]);
+    for (size_t i = 0; i < b->n * kNKeys[t]; ++i) tp.idx[i] = P.user_idx[fuser[t][i]];
+    tp.meas.assign(b->measured ? b->measured : nullptr, b->measured ? b->measured + b->n * kMeasDim[t] : nullptr);
+    tp.isig.resize(b->n * kDim[t]);
+    for (size_t i = 0; i < b->n * kDim[t]; ++i) tp.isig[i] = 1.0 / b->sigmas[i];
+    tp.hk.assign(b->n, 0.0);
+    if (b->huber_k)
+      for (size_t i = 0; i < b->n; ++i) tp.hk[i] = b->huber_k[i];
+  }
+
+  // ---- point-pose edges ----
+  {
+    std::vector<std::pair<int32_t, int32_t>> ep;
+    for (int t = 0; t < kNTypes; ++t) {
+      const TypePlan& tp = P.types[t];
+      const int nk = kNKeys[t];
+      for (int i = 0; i < tp.n; ++i)
+        for (int sa = 0; sa < nk; ++sa)
+          if (kSlotKind[t][sa] == 1)
+            for (int sb = 0; sb < nk; ++sb)
+              if (kSlotKind[t][sb] == 0) ep.emplace_back(tp.idx[i * nk + sa], tp.idx[i * nk + sb]);
+    }
+    std::sort(ep.begin(), ep.end());
+    ep.erase(std::unique(ep.begin(), ep.end()), ep.end());
+    P.n_edge = static_cast<int>(ep.size());
+    P.edge_pt.resize(ep.size());
+    P.edge_pose.resize(ep.size());
+    P.pt_edge_start.assign(P.n_pt + 1, 0);
+    for (size_t e = 0; e < ep.size(); ++e) {
+      P.edge_pt[e] = ep[e].first;
+      P.edge_pose[e] = ep[e].second;
+      P.pt_edge_start[ep[e].first + 1]++;
+    }
+    for (int i = 0; i < P.n_pt; ++i) P.pt_edge_start[i + 1] += P.pt_edge_start[i];
+  }
+  auto find_edge = [&](int32_t pt, int32_t pose) -> int32_t {
+    auto b = P.edge_pose.begin() + P.pt_edge_start[pt];
+    auto e = P.edge_pose.begin() + P.pt_edge_start[pt + 1];
+    auto it = std::lower_bound(b, e, pose);
+    return static_cast<int32_t>(it - P.edge_pose.begin());
+  };
+
+  // ---- arena layout ----
+  P.off_D = arena; arena += 9ull * P.n_pt;
+  P.off_E = arena; arena += 9ull * P.n_pt;
+  P.off_gp = arena; arena += 3ull * P.n_pt;
+  P.off_W = arena; arena += 18ull * P.n_edge;
+
+  // ---- component neighbour poses and Y layout ----
+  P.comp_nb_start.assign(1, 0);
+  P.comp_y_base.resize(P.n_comp);
+  P.off_Y = arena;
+  P.nbedge_start.assign(1, 0);
+  for (int c = 0; c < P.n_comp; ++c) {
+    std::vector<int32_t> nb;
+    for (int32_t i = P.comp_start[c]; i < P.comp_start[c + 1]; ++i)
+      for (int32_t e = P.pt_edge_start[i]; e < P.pt_edge_start[i + 1]; ++e) nb.push_back(P.edge_pose[e]);
+    std::sort(nb.begin(), nb.end());
+    nb.erase(std::unique(nb.begin(), nb.end()), nb.end());
+    const int nc = P.comp_start[c + 1] - P.comp_start[c];
+    const int m = static_cast<int>(nb.size());
+    P.comp_y_base[c] = static_cast<int64_t>(arena);
+    arena += 18ull * nc * m;
+    for (int b = 0; b < m; ++b) {
+      P.nb_pose.push_back(nb[b]);
+      P.nb_comp.push_back(c);
+      for (int32_t i = P.comp_start[c]; i < P.comp_start[c + 1]; ++i) {
+        const int32_t e = find_edge(i, nb[b]);
+        if (e < P.pt_edge_start[i + 1] && P.edge_pose[e] == nb[b]) {
+          P.nbedge_pt.push_back(i - P.comp_start[c]);
+          P.nbedge_w.push_back(static_cast<uint32_t>(P.off_W + 18ull * e));
+        }
+      }
+      P.nbedge_start.push_back(static_cast<int32_t>(P.nbedge_pt.size()));
+    }
+    P.comp_nb_start.push_back(static_cast<int32_t>(P.nb_pose.size()));
+  }
+  P.off_v = arena; arena += 3ull * P.n_pt;
+  P.off_L = arena; arena += 9ull * P.n_pt;
+  P.off_M = arena; arena += 9ull * P.n_pt;
+  P.arena_size = arena;
+  if (arena >= (1ull << 32)) { err = "graph too large for 32-bit arena offsets"; return DYNOHIP_ESTRUCT; }
+
+  // ---- point-side gathers ----
+  {
+    std::vector<std::pair<int32_t, GEntry>> pD, pE, pG, pW;
+    for (int t = 0; t < kNTypes; ++t) {
+      const TypePlan& tp = P.types[t];
+      const int nk = kNKeys[t], d = kDim[t];
+      for (int i = 0; i < tp.n; ++i) {
+        int pslot[2], np = 0;
+        for (int s = 0; s < nk; ++s) {
+          if (kSlotKind[t][s] != 1) continue;
+          pslot[np++] = s;
+          const int32_t pt = tp.idx[i * nk + s];
+          const uint32_t J = block_off(tp, t, i, s);
+          pD.push_back({pt, GEntry{J, J, d, 1}});
+          pG.push_back({pt, GEntry{J, b_off(tp, t, i), d, 1}});
+          for (int sb = 0; sb < nk; ++sb)
+            if (kSlotKind[t][sb] == 0)
+              pW.push_back({find_edge(pt, tp.idx[i * nk + sb]), GEntry{J, block_off(tp, t, i, sb), d, 1}});
+        }
+        if (np == 2) {
+          int sa = pslot[0], sb = pslot[1];
+          int32_t pa = tp.idx[i * nk + sa], pb = tp.idx[i * nk + sb];
+          if (pa > pb) { std::swap(pa, pb); std::swap(sa, sb); }
+          if (pb != pa + 1 || comp_of[pa] != comp_of[pb]) { err = "internal: chain link not adjacent"; return DYNOHIP_ESTRUCT; }
+          // E_pa = C_{pa+1, pa} = J_{pb}^T J_{pa}
+          pE.push_back({pa, GEntry{block_off(tp, t, i, sb), block_off(tp, t, i, sa), d, 1}});
+        }
+      }
+    }
+    to_csr(P.n_pt, pD, P.gD);
+    to_csr(P.n_pt, pE, P.gE);
+    to_csr(P.n_pt, pG, P.gGp);
+    to_csr(P.n_edge, pW, P.gW);
+  }
+
+  // ---- reduced system targets ----
+  {
+    std::unordered_map<uint64_t, int32_t> tmap;
+    std::vector<std::pair<int32_t, int32_t>> tgt;  // (A, B)
+    auto target = [&](int32_t A, int32_t B) -> int32_t {
+      const uint64_t k = (static_cast<uint64_t>(A) << 32) | static_cast<uint32_t>(B);
+      auto it = tmap.find(k);
+      if (it != tmap.end()) return it->second;
+      const int32_t id = static_cast<int32_t>(tgt.size());
+      tmap.emplace(k, id);
+      tgt.emplace_back(A, B);
+      return id;
+    };
+    for (int32_t A = 0; A < P.n_pose; ++A) target(A, A);  // every diagonal (damping)
+    std::vector<std::pair<int32_t, GEntry>> pr, pg;
+    for (int t = 0; t < kNTypes; ++t) {
+      const TypePlan& tp = P.types[t];
+      const int nk = kNKeys[t], d = kDim[t];
+      for (int i = 0; i < tp.n; ++i)
+        for (int sa = 0; sa < nk; ++sa) {
+          if (kSlotKind[t][sa] != 0) continue;
+          const int32_t A = tp.idx[i * nk + sa];
+          pg.push_back({A, GEntry{block_off(tp, t, i, sa), b_off(tp, t, i), d, 1}});
+          for (int sb = 0; sb < nk; ++sb) {
+            if (kSlotKind[t][sb] != 0) continue;
+            const int32_t B = tp.idx[i * nk + sb];
+            if (A < B) continue;
+            pr.push_back({target(A, B), GEntry{block_off(tp, t, i, sa), block_off(tp, t, i, sb), d, 1}});
+          }
+        }
+    }
+    for (int c = 0; c < P.n_comp; ++c) {
+      const int32_t nb0 = P.comp_nb_start[c], m = P.comp_nb_start[c + 1] - nb0;
+      for (int a = 0; a < m; ++a) {
+        const int32_t A = P.nb_pose[nb0 + a];
+        for (int32_t q = P.nbedge_start[nb0 + a]; q < P.nbedge_start[nb0 + a + 1]; ++q)
+          pg.push_back({A, GEntry{P.nbedge_w[q], static_cast<uint32_t>(P.off_v + 3ull * (P.comp_start[c] + P.nbedge_pt[q])), 3, -1}});
+        for (int b = 0; b <= a; ++b) {
+          const int32_t B = P.nb_pose[nb0 + b];
+          const int32_t tid = target(A, B);
+          for (int32_t q = P.nbedge_start[nb0 + a]; q < P.nbedge_start[nb0 + a + 1]; ++q) {
+            const int i = P.nbedge_pt[q];
+            const uint32_t y = static_cast<uint32_t>(P.comp_y_base[c] + 18ll * (static_cast<int64_t>(i) * m + b));
+            pr.push_back({tid, GEntry{P.nbedge_w[q], y, 3, -1}});
+          }
+        }
+      }
+    }
+    // renumber targets in (B, A) order (band column order)
+    std::vector<int32_t> order(tgt.size());
+    std::iota(order.begin(), order.end(), 0);
+    std::sort(order.begin(), order.end(), [&](int32_t x, int32_t y) {
+      if (tgt[x].second != tgt[y].second) return tgt[x].second < tgt[y].second;
+      return tgt[x].first < tgt[y].first;
+    });
+    std::vector<int32_t> rank(tgt.size());
+    for (size_t r = 0; r < order.size(); ++r) rank[order[r]] = static_cast<int32_t>(r);
+    for (auto& p : pr) p.first = rank[p.first];
+    P.red_A.resize(tgt.size());
+    P.red_B.resize(tgt.size());
+    for (size_t r = 0; r < order.size(); ++r) {
+      P.red_A[r] = tgt[order[r]].first;
+      P.red_B[r] = tgt[order[r]].second;
+    }
+    to_csr(tgt.size(), pr, P.gRed);
+    to_csr(P.n_pose, pg, P.gGred);
+  }
+
+  // ---- band layout ----
+  P.n_red = 6 * P.n_pose;
+  P.NT = (P.n_red + kTile - 1) / kTile;
+  std::vector<int32_t> rlow(P.NT);
+  for (int j = 0; j < P.NT; ++j) rlow[j] = j;
+  for (size_t t = 0; t < P.red_A.size(); ++t) {
+    const int r1 = (6 * P.red_A[t] + 5) / kTile;
+    const int c0 = (6 * P.red_B[t]) / kTile, c1 = (6 * P.red_B[t] + 5) / kTile;
+    for (int j = c0; j <= c1; ++j) rlow[j] = std::max(rlow[j], r1);
+  }
+  for (int j = 1; j < P.NT; ++j) rlow[j] = std::max(rlow[j], rlow[j - 1]);
+  P.band_D.resize(P.NT);
+  P.band_off.resize(P.NT);
+  int64_t off = 0;
+  P.max_D = 0;
+  for (int j = 0; j < P.NT; ++j) {
+    P.band_D[j] = rlow[j] - j;
+    P.max_D = std::max(P.max_D, P.band_D[j]);
+    P.band_off[j] = off;
+    off += static_cast<int64_t>(P.band_D[j] + 1) * kTile * kTile;
+  }
+  P.band_size = off;
+  P.band_cmin.resize(P.NT);
+  {
+    int c = 0;
+    for (int i = 0; i < P.NT; ++i) {
+      while (rlow[c] < i) ++c;
+      P.band_cmin[i] = c;
+    }
+  }
+  return DYNOHIP_OK;
+}
+
+}  // namespace dynohip

@@ -1,0 +1,110 @@
+// plan.hpp — host-side analysis of a factor graph into the device layout.
+//
+// Built once per dynohip_set_graph/set_values (the reference re-derives the
+// equivalent structure on every solve: COLAMD + symbolic elimination inside
+// GTSAM's NonlinearOptimizer::solve, called from RGBDBackendModule.cc:220,
+// 374). Everything here is integer index work and is deterministic.
+//
+// Device layout (all FP64 data lives in one "arena"; gather lists address
+// it with 32-bit double offsets):
+//   factor records   per type, per factor: [J_slot0 | J_slot1 | ... | b]
+//                    (each J block dim x slot_dim row-major, whitened and
+//                    Huber-reweighted; b = -whitened residual)
+//   D[n_pt]  (3x3)   point diagonal blocks      sum J_p^T J_p
+//   E[n_pt]  (3x3)   chain sub-diagonal blocks  C_{i+1,i} = sum J_{i+1}^T J_i
+//   gp[n_pt] (3)     point gradients            sum J_p^T b
+//   W[n_edge](3x6)   point-pose coupling        sum J_p^T J_X
+//   Y        (3x6)   C^-1 W per (component, point, neighbour pose)
+//   v[n_pt]  (3)     C^-1 gp
+//   L, M[n_pt](3x3)  block-Cholesky factors of each point chain
+// Reduced (Schur) pose system: lower block-band in 64x64 column tiles,
+// poses in frame order (X_k, then H/L_{j,k}).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/dynohip.h"
+
+namespace dynohip {
+
+constexpr int kNTypes = 6;
+constexpr int kNKeys[kNTypes] = {2, 3, 2, 1, 4, 3};
+constexpr int kDim[kNTypes] = {3, 3, 6, 6, 3, 6};
+constexpr int kMeasDim[kNTypes] = {3, 0, 12, 12, 0, 0};
+constexpr int kCols[kNTypes] = {9, 12, 12, 6, 18, 18};
+// 0 = pose slot, 1 = point slot, -1 unused
+constexpr int kSlotKind[kNTypes][4] = {{0, 1, -1, -1}, {1, 1, 0, -1}, {0, 0, -1, -1},
+                                       {0, -1, -1, -1}, {1, 1, 0, 0}, {0, 0, 0, -1}};
+constexpr int kColStart[kNTypes][4] = {{0, 6, 0, 0}, {0, 3, 6, 0}, {0, 6, 0, 0},
+                                       {0, 0, 0, 0}, {0, 3, 6, 12}, {0, 6, 12, 0}};
+constexpr int kTile = 64;
+
+// sum_e sign * A_e^T B_e, A_e: k x R, B_e: k x C (row-major blocks)
+struct GEntry {
+  uint32_t a;
+  uint32_t b;
+  int32_t k;
+  int32_t sign;
+};
+
+struct GatherList {
+  std::vector<int64_t> start;  // ntargets + 1
+  std::vector<GEntry> ent;
+  size_t ntargets() const { return start.empty() ? 0 : start.size() - 1; }
+};
+
+struct TypePlan {
+  int n = 0;
+  uint64_t base = 0;     // arena offset of the first record
+  uint32_t stride = 0;   // doubles per record
+  std::vector<int32_t> idx;   // n * nkeys (pose index or point index per slot)
+  std::vector<double> meas;   // n * meas_dim
+  std::vector<double> isig;   // n * dim (1/sigma)
+  std::vector<double> hk;     // n (Huber k, <= 0 Gaussian)
+};
+
+struct Plan {
+  // variables
+  int n_pose = 0, n_pt = 0;
+  std::vector<uint8_t> user_kind;   // per user value
+  std::vector<int32_t> user_idx;    // pose index or point index
+  std::vector<uint64_t> pose_key, pt_key;
+  // point components (chains), points contiguous in chain order
+  int n_comp = 0;
+  int max_chain = 0;
+  std::vector<int32_t> comp_start;      // n_comp + 1
+  std::vector<int32_t> comp_nb_start;   // n_comp + 1 (into nb arrays)
+  std::vector<int32_t> nb_pose;         // per nb entry
+  std::vector<int32_t> nb_comp;         // per nb entry
+  std::vector<int64_t> comp_y_base;     // arena offset of comp's Y
+  std::vector<int32_t> nbedge_start;    // per nb entry + 1
+  std::vector<int32_t> nbedge_pt;       // local point index in comp
+  std::vector<uint32_t> nbedge_w;       // arena offset of W block
+  // point-pose edges, sorted by (point, pose)
+  int n_edge = 0;
+  std::vector<int32_t> edge_pt, edge_pose;
+  std::vector<int32_t> pt_edge_start;   // n_pt + 1
+  TypePlan types[kNTypes];
+  // gathers
+  GatherList gD, gE, gGp, gW, gRed, gGred;
+  std::vector<int32_t> red_A, red_B;    // reduced target pose indices (A >= B)
+  // arena
+  uint64_t off_D = 0, off_E = 0, off_gp = 0, off_W = 0, off_Y = 0, off_v = 0, off_L = 0, off_M = 0;
+  uint64_t arena_size = 0;
+  // reduced band
+  int n_red = 0;                        // 6 * n_pose
+  int NT = 0;                           // column tiles
+  std::vector<int32_t> band_D;          // per column tile: #sub-diagonal tiles
+  std::vector<int64_t> band_off;        // per column tile: offset (doubles)
+  std::vector<int32_t> band_cmin;       // per row tile: first column tile present
+  int64_t band_size = 0;
+  int max_D = 0;
+};
+
+// returns DYNOHIP_OK or an error code with `err` filled
+int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t* kind, size_t n, Plan& plan,
+               std::string& err);
+
+}  // namespace dynohip

@@ -1,0 +1,646 @@
+// solver.cpp — dynohip C-ABI: handle, device buffers, GTSAM 4.2.0
+// Levenberg–Marquardt control loop driving the HIP kernels.
+//
+// Replaces `gtsam::LevenbergMarquardtOptimizer(graph, values,
+// LevenbergMarquardtParams()).optimize()` at RGBDBackendModule.cc:207-231
+// and :364-383. LM semantics: SURVEY.md Appendix A (GTSAM 4.2.0
+// LevenbergMarquardtOptimizer::tryLambda / iterate, NonlinearOptimizer::
+// defaultOptimize, checkConvergence). Only ~3 scalars cross to the host per
+// inner iteration.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/dynohip.h"
+#include "kernels.hpp"
+#include "plan.hpp"
+
+using namespace dynohip;
+
+namespace {
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  hipError_t alloc(size_t count) {
+    release();
+    n = count;
+    if (count == 0) return hipSuccess;
+    return hipMalloc(reinterpret_cast<void**>(&p), count * sizeof(T));
+  }
+  hipError_t upload(const std::vector<T>& v, hipStream_t s) {
+    hipError_t e = alloc(v.size());
+    if (e != hipSuccess || v.empty()) return e;
+    return hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s);
+  }
+};
+
+struct GraphCopy {
+  std::vector<uint64_t> keys[kNTypes];
+  std::vector<double> meas[kNTypes], sig[kNTypes], hub[kNTypes];
+  size_t n[kNTypes] = {};
+  dynohip_graph_view view() const {
+    dynohip_graph_view g;
+    dynohip_factor_block* b[kNTypes] = {&g.pose_to_point, &g.landmark_motion_ternary, &g.between,
+                                        &g.prior, &g.landmark_motion_pose, &g.landmark_pose_smoothing};
+    for (int t = 0; t < kNTypes; ++t) {
+      b[t]->n = n[t];
+      b[t]->keys = keys[t].data();
+      b[t]->measured = meas[t].empty() ? nullptr : meas[t].data();
+      b[t]->sigmas = sig[t].data();
+      b[t]->huber_k = hub[t].data();
+    }
+    return g;
+  }
+};
+
+struct TypeBufs {
+  DevBuf<int32_t> idx;
+  DevBuf<double> meas, isig, hk;
+};
+
+struct GatherBufs {
+  DevBuf<int64_t> start;
+  DevBuf<GEntry> ent;
+  GatherDev dev(size_t nt) const {
+    GatherDev g;
+    g.n = static_cast<int>(nt);
+    g.start = start.p;
+    g.ent = ent.p;
+    return g;
+  }
+};
+
+}  // namespace
+
+struct dynohip_solver {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  GraphCopy graph;
+  bool has_graph = false;
+  bool has_plan = false;
+  bool has_values = false;
+  std::vector<uint64_t> value_keys;
+  Plan plan;
+  // device state
+  DevBuf<double> pose, pt, pose_c, pt_c, arena;
+  TypeBufs tb[kNTypes];
+  TypeDev td[kNTypes];
+  GatherBufs gD, gE, gGp, gW, gRed, gGred;
+  DevBuf<int32_t> redA, redB;
+  DevBuf<int32_t> comp_start, comp_nb_start, nb_comp, nbedge_start, nbedge_pt, pt_edge_start, edge_pose;
+  DevBuf<int64_t> comp_y_base;
+  DevBuf<uint32_t> nbedge_w;
+  DevBuf<double> band, gred, xy, dpt;
+  DevBuf<int64_t> band_off;
+  DevBuf<int32_t> band_D, band_cmin;
+  DevBuf<double> partials, result;
+  DevBuf<int> fail;
+  int partial_slots = 0;
+  ChainDev cd;
+  BandDev bd;
+  // LM state
+  dynohip_lm_params prm{};
+  double lambda = 1e-5, error = 0.0;
+  int iterations = 0, inner = 0, converged = 0;
+  std::vector<dynohip_trace_entry> trace;
+  // phase timing
+  hipEvent_t ev[8] = {};
+  double phase_ms[7] = {};
+};
+
+namespace {
+
+int set_err(dynohip_solver* s, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  s->err = buf;
+  return code;
+}
+
+#define HIPCHK(s, expr)                                                                     \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess) return set_err(s, DYNOHIP_EHIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+int upload_gather(dynohip_solver* s, const GatherList& g, GatherBufs& b) {
+  HIPCHK(s, b.start.upload(g.start, s->stream));
+  HIPCHK(s, b.ent.upload(g.ent, s->stream));
+  return 0;
+}
+
+int upload_plan(dynohip_solver* s) {
+  Plan& P = s->plan;
+  hipStream_t st = s->stream;
+  HIPCHK(s, s->pose.alloc(12ull * P.n_pose));
+  HIPCHK(s, s->pt.alloc(3ull * P.n_pt));
+  HIPCHK(s, s->pose_c.alloc(12ull * P.n_pose));
+  HIPCHK(s, s->pt_c.alloc(3ull * P.n_pt));
+  HIPCHK(s, s->arena.alloc(P.arena_size));
+  int slots = 1;
+  for (int t = 0; t < kNTypes; ++t) {
+    TypePlan& tp = P.types[t];
+    HIPCHK(s, s->tb[t].idx.upload(tp.idx, st));
+    HIPCHK(s, s->tb[t].meas.upload(tp.meas, st));
+    HIPCHK(s, s->tb[t].isig.upload(tp.isig, st));
+    HIPCHK(s, s->tb[t].hk.upload(tp.hk, st));
+    TypeDev& d = s->td[t];
+    d.n = tp.n;
+    d.base = tp.base;
+    d.stride = tp.stride;
+    d.idx = s->tb[t].idx.p;
+    d.meas = s->tb[t].meas.p;
+    d.isig = s->tb[t].isig.p;
+    d.hk = s->tb[t].hk.p;
+    slots += error_blocks(tp.n);
+  }
+  s->partial_slots = slots;
+  HIPCHK(s, s->partials.alloc(2ull * slots));
+  HIPCHK(s, s->result.alloc(8));
+  HIPCHK(s, s->fail.alloc(1));
+  if (upload_gather(s, P.gD, s->gD) || upload_gather(s, P.gE, s->gE) || upload_gather(s, P.gGp, s->gGp) ||
+      upload_gather(s, P.gW, s->gW) || upload_gather(s, P.gRed, s->gRed) || upload_gather(s, P.gGred, s->gGred))
+    return DYNOHIP_EHIP;
+  HIPCHK(s, s->redA.upload(P.red_A, st));
+  HIPCHK(s, s->redB.upload(P.red_B, st));
+  HIPCHK(s, s->comp_start.upload(P.comp_start, st));
+  HIPCHK(s, s->comp_nb_start.upload(P.comp_nb_start, st));
+  HIPCHK(s, s->nb_comp.upload(P.nb_comp, st));
+  HIPCHK(s, s->comp_y_base.upload(P.comp_y_base, st));
+  HIPCHK(s, s->nbedge_start.upload(P.nbedge_start, st));
+  HIPCHK(s, s->nbedge_pt.upload(P.nbedge_pt, st));
+  HIPCHK(s, s->nbedge_w.upload(P.nbedge_w, st));
+  HIPCHK(s, s->pt_edge_start.upload(P.pt_edge_start, st));
+  HIPCHK(s, s->edge_pose.upload(P.edge_pose, st));
+  HIPCHK(s, s->band.alloc(P.band_size));
+  HIPCHK(s, s->band_off.upload(P.band_off, st));
+  HIPCHK(s, s->band_D.upload(P.band_D, st));
+  HIPCHK(s, s->band_cmin.upload(P.band_cmin, st));
+  const size_t nrp = static_cast<size_t>(P.NT) * kTile;
+  HIPCHK(s, s->gred.alloc(nrp > 0 ? nrp : 1));
+  HIPCHK(s, s->xy.alloc(2 * (nrp > 0 ? nrp : 1)));
+  HIPCHK(s, s->dpt.alloc(3ull * P.n_pt + 1));
+  ChainDev& c = s->cd;
+  c.n_comp = P.n_comp;
+  c.n_nb = static_cast<int>(P.nb_pose.size());
+  c.comp_start = s->comp_start.p;
+  c.comp_nb_start = s->comp_nb_start.p;
+  c.nb_comp = s->nb_comp.p;
+  c.comp_y_base = s->comp_y_base.p;
+  c.nbedge_start = s->nbedge_start.p;
+  c.nbedge_pt = s->nbedge_pt.p;
+  c.nbedge_w = s->nbedge_w.p;
+  c.pt_edge_start = s->pt_edge_start.p;
+  c.edge_pose = s->edge_pose.p;
+  c.off_D = P.off_D;
+  c.off_E = P.off_E;
+  c.off_gp = P.off_gp;
+  c.off_W = P.off_W;
+  c.off_v = P.off_v;
+  c.off_L = P.off_L;
+  c.off_M = P.off_M;
+  BandDev& b = s->bd;
+  b.NT = P.NT;
+  b.n_red = P.n_red;
+  b.band = s->band.p;
+  b.off = s->band_off.p;
+  b.D = s->band_D.p;
+  b.cmin = s->band_cmin.p;
+  HIPCHK(s, hipStreamSynchronize(st));
+  return 0;
+}
+
+// error at (pose, pt) into result[slot]
+void enqueue_error(dynohip_solver* s, const double* pose, const double* pt, double* partials, double* out) {
+  int off = 0;
+  for (int t = 0; t < kNTypes; ++t) {
+    launch_error(t, s->td[t], pose, pt, partials + off, s->stream);
+    off += error_blocks(s->td[t].n);
+  }
+  launch_reduce(partials, off, out, s->stream);
+}
+
+void enqueue_linerr(dynohip_solver* s, const double* dpose, const double* dpt, double* partials, double* out) {
+  int off = 0;
+  for (int t = 0; t < kNTypes; ++t) {
+    launch_linerr(t, s->td[t], s->arena.p, dpose, dpt, partials + off, s->stream);
+    off += error_blocks(s->td[t].n);
+  }
+  launch_reduce(partials, off, out, s->stream);
+}
+
+int compute_error(dynohip_solver* s, const double* pose, const double* pt, double* err_out) {
+  enqueue_error(s, pose, pt, s->partials.p, s->result.p);
+  HIPCHK(s, hipMemcpyAsync(err_out, s->result.p, sizeof(double), hipMemcpyDeviceToHost, s->stream));
+  HIPCHK(s, hipStreamSynchronize(s->stream));
+  return 0;
+}
+
+// linearisation + point-side blocks (once per outer iteration)
+void enqueue_linearize(dynohip_solver* s) {
+  Plan& P = s->plan;
+  double* A = s->arena.p;
+  for (int t = 0; t < kNTypes; ++t) launch_linearize(t, s->td[t], s->pose.p, s->pt.p, A, s->stream);
+  launch_gather_3x3(s->gD.dev(P.gD.ntargets()), A, A + P.off_D, s->stream);
+  launch_gather_3x3(s->gE.dev(P.gE.ntargets()), A, A + P.off_E, s->stream);
+  launch_gather_3x1(s->gGp.dev(P.gGp.ntargets()), A, A + P.off_gp, s->stream);
+  launch_gather_3x6(s->gW.dev(P.gW.ntargets()), A, A + P.off_W, s->stream);
+}
+
+// damped solve + linearised error + retract + error for one lambda.
+// result[0] = new linear error, result[1] = new nonlinear error; fail flag.
+void enqueue_try(dynohip_solver* s, double lambda, bool timed) {
+  Plan& P = s->plan;
+  hipStream_t st = s->stream;
+  double* A = s->arena.p;
+  const size_t nrp = static_cast<size_t>(P.NT) * kTile;
+  if (timed) (void)hipEventRecord(s->ev[1], st);
+  (void)hipMemsetAsync(s->fail.p, 0, sizeof(int), st);
+  (void)hipMemsetAsync(s->band.p, 0, P.band_size * sizeof(double), st);
+  (void)hipMemsetAsync(s->gred.p, 0, nrp * sizeof(double), st);
+  launch_chain_factor(s->cd, A, lambda, s->fail.p, st);
+  launch_chain_solve_y(s->cd, A, st);
+  if (timed) (void)hipEventRecord(s->ev[2], st);
+  launch_gather_band(s->gRed.dev(P.gRed.ntargets()), A, s->redA.p, s->redB.p, s->bd, lambda, st);
+  launch_band_pad(s->bd, st);
+  launch_gather_grad(s->gGred.dev(P.gGred.ntargets()), A, s->gred.p, st);
+  if (timed) (void)hipEventRecord(s->ev[3], st);
+  launch_band_cholesky(s->bd, P.band_D.data(), s->fail.p, st);
+  if (timed) (void)hipEventRecord(s->ev[4], st);
+  double* y = s->xy.p;
+  double* x = s->xy.p + nrp;
+  launch_band_solve(s->bd, s->gred.p, y, x, st);
+  if (timed) (void)hipEventRecord(s->ev[5], st);
+  // pose deltas are x[0 .. 6 n_pose) in pose-index order
+  launch_backsub(s->cd, A, x, s->dpt.p, st);
+  enqueue_linerr(s, x, s->dpt.p, s->partials.p, s->result.p);
+  if (timed) (void)hipEventRecord(s->ev[6], st);
+  launch_retract(P.n_pose, P.n_pt, s->pose.p, s->pt.p, x, s->dpt.p, s->pose_c.p, s->pt_c.p, st);
+  enqueue_error(s, s->pose_c.p, s->pt_c.p, s->partials.p + s->partial_slots, s->result.p + 1);
+  if (timed) (void)hipEventRecord(s->ev[7], st);
+}
+
+void push_trace(dynohip_solver* s, const dynohip_trace_entry& e) { s->trace.push_back(e); }
+
+// LevenbergMarquardtOptimizer::iterate()
+int lm_iterate(dynohip_solver* s) {
+  hipStream_t st = s->stream;
+  (void)hipEventRecord(s->ev[0], st);
+  enqueue_linearize(s);
+  enqueue_linerr(s, nullptr, nullptr, s->partials.p, s->result.p + 2);
+  double oldLin = 0.0;
+  HIPCHK(s, hipMemcpyAsync(&oldLin, s->result.p + 2, sizeof(double), hipMemcpyDeviceToHost, st));
+  HIPCHK(s, hipStreamSynchronize(st));
+  bool first = true;
+  for (;;) {
+    dynohip_trace_entry te{};
+    te.outer_iteration = s->iterations;
+    te.lambda = s->lambda;
+    te.current_error = s->error;
+    te.new_error = INFINITY;
+    te.old_linear_error = oldLin;
+    enqueue_try(s, s->lambda, first);
+    double res[2];
+    int fail = 0;
+    HIPCHK(s, hipMemcpyAsync(res, s->result.p, 2 * sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPCHK(s, hipMemcpyAsync(&fail, s->fail.p, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPCHK(s, hipStreamSynchronize(st));
+    if (first) {
+      float ms = 0.f;
+      for (int k = 0; k < 7; ++k) {
+        (void)hipEventElapsedTime(&ms, s->ev[k], s->ev[k + 1]);
+        s->phase_ms[k] = ms;
+      }
+      first = false;
+    }
+    const int solved = fail == 0 && std::isfinite(res[0]);
+    te.solved = solved;
+    bool step_ok = false, stop = false;
+    double modelFidelity = 0.0, newError = INFINITY;
+    if (solved) {
+      const double newLin = res[0];
+      te.new_linear_error = newLin;
+      const double linChange = oldLin - newLin;
+      if (linChange >= 0) {
+        newError = res[1];
+        te.new_error = newError;
+        const double costChange = s->error - newError;
+        if (linChange > DBL_EPSILON * oldLin) {
+          modelFidelity = costChange / linChange;
+          step_ok = modelFidelity > s->prm.min_model_fidelity;
+        }
+        if (std::fabs(costChange) < s->prm.relative_error_tol * s->error) stop = true;
+      }
+    }
+    te.model_fidelity = modelFidelity;
+    te.accepted = step_ok;
+    te.stop = stop;
+    push_trace(s, te);
+    if (step_ok) {
+      std::swap(s->pose.p, s->pose_c.p);
+      std::swap(s->pt.p, s->pt_c.p);
+      s->error = newError;
+      s->lambda /= s->prm.lambda_factor;
+      if (s->lambda < s->prm.lambda_lower_bound) s->lambda = s->prm.lambda_lower_bound;
+      s->iterations++;
+      s->inner++;
+      break;
+    } else if (!stop) {
+      s->lambda *= s->prm.lambda_factor;
+      s->inner++;
+      if (s->lambda >= s->prm.lambda_upper_bound) break;
+    } else {
+      break;
+    }
+  }
+  return 0;
+}
+
+void fill_summary(const dynohip_solver* s, double initial, dynohip_lm_summary* out) {
+  if (!out) return;
+  out->iterations = s->iterations;
+  out->inner_iterations = s->inner;
+  out->initial_error = initial;
+  out->final_error = s->error;
+  out->final_lambda = s->lambda;
+  out->converged = s->converged;
+  out->reserved = 0;
+}
+
+int ready(dynohip_solver* s) {
+  if (!s) return DYNOHIP_EINVAL;
+  if (!s->has_graph || !s->has_plan || !s->has_values) return set_err(s, DYNOHIP_ESTATE, "graph and values must be set");
+  return 0;
+}
+
+}  // namespace
+
+// ======================================================================
+extern "C" {
+
+int dynohip_abi_version(void) { return DYNOHIP_ABI_VERSION; }
+
+void dynohip_lm_params_default(dynohip_lm_params* p) {
+  if (!p) return;
+  std::memset(p, 0, sizeof(*p));
+  p->lambda_initial = 1e-5;
+  p->lambda_factor = 10.0;
+  p->lambda_upper_bound = 1e5;
+  p->lambda_lower_bound = 0.0;
+  p->min_model_fidelity = 1e-3;
+  p->relative_error_tol = 1e-5;
+  p->absolute_error_tol = 1e-5;
+  p->error_tol = 0.0;
+  p->max_iterations = 100;
+  p->diagonal_damping = 0;
+  p->use_fixed_lambda_factor = 1;
+}
+
+int dynohip_create(int device_id, dynohip_solver** out) {
+  if (!out) return DYNOHIP_EINVAL;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return DYNOHIP_EHIP;
+  if (device_id < 0 || device_id >= ndev) return DYNOHIP_EINVAL;
+  if (hipSetDevice(device_id) != hipSuccess) return DYNOHIP_EHIP;
+  dynohip_solver* s = new dynohip_solver();
+  s->device = device_id;
+  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete s;
+    return DYNOHIP_EHIP;
+  }
+  for (auto& e : s->ev) (void)hipEventCreate(&e);
+  dynohip_lm_params_default(&s->prm);
+  *out = s;
+  return DYNOHIP_OK;
+}
+
+void dynohip_destroy(dynohip_solver* s) {
+  if (!s) return;
+  (void)hipSetDevice(s->device);
+  if (s->stream) (void)hipStreamSynchronize(s->stream);
+  for (auto& e : s->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (s->stream) (void)hipStreamDestroy(s->stream);
+  delete s;
+}
+
+const char* dynohip_last_error(const dynohip_solver* s) { return s ? s->err.c_str() : "null handle"; }
+
+int dynohip_set_graph(dynohip_solver* s, const dynohip_graph_view* g) {
+  if (!s || !g) return DYNOHIP_EINVAL;
+  const dynohip_factor_block* b[kNTypes] = {&g->pose_to_point, &g->landmark_motion_ternary, &g->between,
+                                            &g->prior, &g->landmark_motion_pose, &g->landmark_pose_smoothing};
+  GraphCopy gc;
+  for (int t = 0; t < kNTypes; ++t) {
+    const size_t n = b[t]->n;
+    gc.n[t] = n;
+    if (n == 0) continue;
+    if (!b[t]->keys || !b[t]->sigmas || (kMeasDim[t] && !b[t]->measured))
+      return set_err(s, DYNOHIP_EINVAL, "factor type %d: null keys/sigmas/measured", t);
+    gc.keys[t].assign(b[t]->keys, b[t]->keys + n * kNKeys[t]);
+    if (kMeasDim[t]) gc.meas[t].assign(b[t]->measured, b[t]->measured + n * kMeasDim[t]);
+    gc.sig[t].assign(b[t]->sigmas, b[t]->sigmas + n * kDim[t]);
+    if (b[t]->huber_k) gc.hub[t].assign(b[t]->huber_k, b[t]->huber_k + n);
+    else gc.hub[t].assign(n, 0.0);
+  }
+  s->graph = std::move(gc);
+  s->has_graph = true;
+  s->has_plan = false;
+  s->has_values = false;
+  return DYNOHIP_OK;
+}
+
+int dynohip_set_values(dynohip_solver* s, const uint64_t* keys, const uint8_t* kind, const double* data, size_t n) {
+  if (!s || (n && (!keys || !kind || !data))) return DYNOHIP_EINVAL;
+  if (!s->has_graph) return set_err(s, DYNOHIP_ESTATE, "set_graph first");
+  (void)hipSetDevice(s->device);
+  const bool same = s->has_plan && s->value_keys.size() == n &&
+                    std::equal(s->value_keys.begin(), s->value_keys.end(), keys);
+  if (!same) {
+    s->has_plan = false;
+    dynohip_graph_view g = s->graph.view();
+    int rc = build_plan(g, keys, kind, n, s->plan, s->err);
+    if (rc) return rc;
+    rc = upload_plan(s);
+    if (rc) return rc;
+    s->value_keys.assign(keys, keys + n);
+    s->has_plan = true;
+  }
+  Plan& P = s->plan;
+  std::vector<double> hp(12ull * P.n_pose), hq(3ull * P.n_pt);
+  size_t off = 0;
+  for (size_t i = 0; i < n; ++i) {
+    if (kind[i] != P.user_kind[i]) return set_err(s, DYNOHIP_EINVAL, "value kind changed for key %zu", i);
+    const int sz = kind[i] == DYNOHIP_POSE3 ? 12 : 3;
+    for (int k = 0; k < sz; ++k)
+      if (!std::isfinite(data[off + k])) return set_err(s, DYNOHIP_ENONFINITE, "non-finite value");
+    double* dst = kind[i] == DYNOHIP_POSE3 ? &hp[12ull * P.user_idx[i]] : &hq[3ull * P.user_idx[i]];
+    std::memcpy(dst, data + off, sz * sizeof(double));
+    off += sz;
+  }
+  if (!hp.empty()) HIPCHK(s, hipMemcpyAsync(s->pose.p, hp.data(), hp.size() * sizeof(double), hipMemcpyHostToDevice, s->stream));
+  if (!hq.empty()) HIPCHK(s, hipMemcpyAsync(s->pt.p, hq.data(), hq.size() * sizeof(double), hipMemcpyHostToDevice, s->stream));
+  HIPCHK(s, hipStreamSynchronize(s->stream));
+  s->has_values = true;
+  return dynohip_lm_reset(s, &s->prm);
+}
+
+int dynohip_get_values(dynohip_solver* s, double* out, size_t n_doubles) {
+  int rc = ready(s);
+  if (rc) return rc;
+  (void)hipSetDevice(s->device);
+  Plan& P = s->plan;
+  std::vector<double> hp(12ull * P.n_pose), hq(3ull * P.n_pt);
+  if (!hp.empty()) HIPCHK(s, hipMemcpyAsync(hp.data(), s->pose.p, hp.size() * sizeof(double), hipMemcpyDeviceToHost, s->stream));
+  if (!hq.empty()) HIPCHK(s, hipMemcpyAsync(hq.data(), s->pt.p, hq.size() * sizeof(double), hipMemcpyDeviceToHost, s->stream));
+  HIPCHK(s, hipStreamSynchronize(s->stream));
+  size_t need = 12ull * P.n_pose + 3ull * P.n_pt;
+  if (n_doubles < need) return set_err(s, DYNOHIP_EINVAL, "output buffer too small (%zu < %zu)", n_doubles, need);
+  size_t off = 0;
+  for (size_t i = 0; i < P.user_kind.size(); ++i) {
+    const int sz = P.user_kind[i] == DYNOHIP_POSE3 ? 12 : 3;
+    const double* src = P.user_kind[i] == DYNOHIP_POSE3 ? &hp[12ull * P.user_idx[i]] : &hq[3ull * P.user_idx[i]];
+    std::memcpy(out + off, src, sz * sizeof(double));
+    off += sz;
+  }
+  return DYNOHIP_OK;
+}
+
+int dynohip_graph_error(dynohip_solver* s, double* error_out) {
+  int rc = ready(s);
+  if (rc) return rc;
+  if (!error_out) return DYNOHIP_EINVAL;
+  (void)hipSetDevice(s->device);
+  return compute_error(s, s->pose.p, s->pt.p, error_out);
+}
+
+int dynohip_lm_reset(dynohip_solver* s, const dynohip_lm_params* p) {
+  int rc = ready(s);
+  if (rc) return rc;
+  if (!p) return DYNOHIP_EINVAL;
+  if (p->diagonal_damping || !p->use_fixed_lambda_factor)
+    return set_err(s, DYNOHIP_EINVAL, "only diagonalDamping=false, useFixedLambdaFactor=true are supported");
+  (void)hipSetDevice(s->device);
+  s->prm = *p;
+  s->lambda = p->lambda_initial;
+  s->iterations = 0;
+  s->inner = 0;
+  s->converged = 0;
+  s->trace.clear();
+  return compute_error(s, s->pose.p, s->pt.p, &s->error);
+}
+
+int dynohip_iterate(dynohip_solver* s, dynohip_lm_summary* out) {
+  int rc = ready(s);
+  if (rc) return rc;
+  (void)hipSetDevice(s->device);
+  const double e0 = s->error;
+  rc = lm_iterate(s);
+  if (rc) return rc;
+  fill_summary(s, e0, out);
+  return DYNOHIP_OK;
+}
+
+// NonlinearOptimizer::defaultOptimize + checkConvergence
+int dynohip_optimize(dynohip_solver* s, const dynohip_lm_params* p, dynohip_lm_summary* out) {
+  int rc = dynohip_lm_reset(s, p);
+  if (rc) return rc;
+  const double initial = s->error;
+  double currentError = s->error;
+  if (currentError <= p->error_tol || s->iterations >= p->max_iterations) {
+    s->converged = currentError <= p->error_tol;
+    fill_summary(s, initial, out);
+    return DYNOHIP_OK;
+  }
+  double newError = currentError;
+  do {
+    currentError = newError;
+    rc = lm_iterate(s);
+    if (rc) return rc;
+    newError = s->error;
+    bool conv;
+    if (newError <= p->error_tol) {
+      conv = true;
+    } else {
+      const double absd = currentError - newError;
+      const double reld = absd / currentError;
+      conv = (reld <= p->relative_error_tol) || (absd <= p->absolute_error_tol);
+    }
+    s->converged = conv;
+  } while (s->iterations < p->max_iterations && !s->converged && std::isfinite(currentError));
+  fill_summary(s, initial, out);
+  return DYNOHIP_OK;
+}
+
+int dynohip_get_trace(dynohip_solver* s, dynohip_trace_entry* out, size_t capacity, size_t* n_out) {
+  if (!s) return DYNOHIP_EINVAL;
+  const size_t n = std::min(capacity, s->trace.size());
+  if (out && n) std::memcpy(out, s->trace.data(), n * sizeof(dynohip_trace_entry));
+  if (n_out) *n_out = s->trace.size();
+  return DYNOHIP_OK;
+}
+
+size_t dynohip_linearize_size(const dynohip_solver* s) {
+  if (!s || !s->has_plan) return 0;
+  size_t n = 0;
+  for (int t = 0; t < kNTypes; ++t) n += static_cast<size_t>(s->plan.types[t].n) * kDim[t] * (kCols[t] + 1);
+  return n;
+}
+
+int dynohip_linearize(dynohip_solver* s, double* out, size_t n_doubles) {
+  int rc = ready(s);
+  if (rc) return rc;
+  if (n_doubles < dynohip_linearize_size(s)) return set_err(s, DYNOHIP_EINVAL, "output buffer too small");
+  (void)hipSetDevice(s->device);
+  enqueue_linearize(s);
+  const Plan& P = s->plan;
+  std::vector<double> rec;
+  size_t o = 0;
+  for (int t = 0; t < kNTypes; ++t) {
+    const TypePlan& tp = P.types[t];
+    if (tp.n == 0) continue;
+    rec.resize(static_cast<size_t>(tp.stride) * tp.n);
+    HIPCHK(s, hipMemcpyAsync(rec.data(), s->arena.p + tp.base, rec.size() * sizeof(double), hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(s, hipStreamSynchronize(s->stream));
+    const int d = kDim[t];
+    for (int i = 0; i < tp.n; ++i) {
+      const double* r = rec.data() + static_cast<size_t>(tp.stride) * i;
+      for (int k = 0; k < d; ++k) {
+        for (int sl = 0; sl < kNKeys[t]; ++sl) {
+          const int ds = kSlotKind[t][sl] == 0 ? 6 : 3;
+          const double* blk = r + d * kColStart[t][sl];
+          for (int c = 0; c < ds; ++c) out[o++] = blk[k * ds + c];
+        }
+        out[o++] = r[d * kCols[t] + k];
+      }
+    }
+  }
+  return DYNOHIP_OK;
+}
+
+int dynohip_get_phase_times(dynohip_solver* s, double* ms_out, size_t n) {
+  if (!s || !ms_out) return DYNOHIP_EINVAL;
+  for (size_t k = 0; k < n && k < 7; ++k) ms_out[k] = s->phase_ms[k];
+  return DYNOHIP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,143 @@
+"""LevenbergMarquardtOptimizer over the dynohip C-ABI (HIP on MI355X).
+
+Python mirror of the reference call sites
+    gtsam::LevenbergMarquardtOptimizer problem(graph, theta, opt_params);
+    gtsam::Values optimised = problem.optimize();
+    problem.iterations(); problem.getInnerIterations();
+(RGBDBackendModule.cc:207-231, :364-383). The work runs in libdynohip.so;
+there is no CPU fallback: a missing library or device raises.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _abi, _native
+from .graph import Values
+
+
+class DynohipError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"dynohip error {code}: {msg}")
+        self.code = code
+
+
+def _check(lib, h, rc):
+    if rc != 0:
+        msg = lib.dynohip_last_error(h).decode() if h else ""
+        raise DynohipError(rc, msg)
+
+
+class Solver:
+    """One dynohip_solver handle bound to a HIP device."""
+
+    def __init__(self, device=0):
+        self.lib = _native.load("libdynohip.so")
+        self.h = C.c_void_p()
+        rc = self.lib.dynohip_create(int(device), C.byref(self.h))
+        if rc != 0:
+            raise DynohipError(rc, "dynohip_create failed (no HIP device?)")
+        self._graph = None
+        self._values = None
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.dynohip_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def set_graph(self, graph):
+        self._graph = graph
+        gv = graph.view()
+        _check(self.lib, self.h, self.lib.dynohip_set_graph(self.h, C.byref(gv)))
+
+    def set_values(self, values):
+        self._values = values
+        keys = np.ascontiguousarray(values.keys, dtype=np.uint64)
+        kinds = np.ascontiguousarray(values.kinds, dtype=np.uint8)
+        data = np.ascontiguousarray(values.data, dtype=np.float64)
+        _check(self.lib, self.h, self.lib.dynohip_set_values(
+            self.h, keys.ctypes.data_as(C.POINTER(C.c_uint64)), kinds.ctypes.data_as(C.POINTER(C.c_uint8)),
+            data.ctypes.data_as(C.POINTER(C.c_double)), keys.shape[0]))
+
+    def values_data(self):
+        n = self._values.data.shape[0]
+        out = np.zeros(n)
+        _check(self.lib, self.h, self.lib.dynohip_get_values(self.h, out.ctypes.data_as(C.POINTER(C.c_double)), n))
+        return out
+
+    def values(self):
+        return self._values.with_data(self.values_data())
+
+    def error(self):
+        e = C.c_double()
+        _check(self.lib, self.h, self.lib.dynohip_graph_error(self.h, C.byref(e)))
+        return e.value
+
+    def reset(self, params=None):
+        params = params or _abi.LMParams.gtsam_default()
+        _check(self.lib, self.h, self.lib.dynohip_lm_reset(self.h, C.byref(params)))
+
+    def iterate(self):
+        s = _abi.LMSummary()
+        _check(self.lib, self.h, self.lib.dynohip_iterate(self.h, C.byref(s)))
+        return s
+
+    def optimize(self, params=None):
+        params = params or _abi.LMParams.gtsam_default()
+        s = _abi.LMSummary()
+        _check(self.lib, self.h, self.lib.dynohip_optimize(self.h, C.byref(params), C.byref(s)))
+        return s
+
+    def trace(self):
+        n = C.c_size_t()
+        self.lib.dynohip_get_trace(self.h, None, 0, C.byref(n))
+        arr = (_abi.TraceEntry * max(1, n.value))()
+        self.lib.dynohip_get_trace(self.h, arr, n.value, C.byref(n))
+        return _abi.trace_to_dicts(arr[: n.value])
+
+    def linearize(self):
+        n = self.lib.dynohip_linearize_size(self.h)
+        out = np.zeros(n)
+        _check(self.lib, self.h, self.lib.dynohip_linearize(self.h, out.ctypes.data_as(C.POINTER(C.c_double)), n))
+        return out
+
+    def phase_times(self):
+        out = np.zeros(7)
+        self.lib.dynohip_get_phase_times(self.h, out.ctypes.data_as(C.POINTER(C.c_double)), 7)
+        return out
+
+
+class LevenbergMarquardtOptimizer:
+    """gtsam::LevenbergMarquardtOptimizer(graph, values, params) on the GPU."""
+
+    def __init__(self, graph, values, params=None, device=0, solver=None):
+        self.params = params or _abi.LMParams.gtsam_default()
+        self.solver = solver or Solver(device)
+        self.solver.set_graph(graph)
+        self.solver.set_values(values)
+        self._summary = None
+
+    def optimize(self):
+        self._summary = self.solver.optimize(self.params)
+        return self.solver.values()
+
+    def iterate(self):
+        self._summary = self.solver.iterate()
+        return self._summary
+
+    def iterations(self):
+        return self._summary.iterations if self._summary else 0
+
+    def getInnerIterations(self):  # noqa: N802 (reference API name)
+        return self._summary.inner_iterations if self._summary else 0
+
+    def error(self):
+        return self.solver.error()
+
+    def summary(self):
+        return self._summary
+
+    def trace(self):
+        return self.solver.trace()
