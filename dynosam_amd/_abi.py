@@ -86,6 +86,44 @@ class TraceEntry(C.Structure):
     ]
 
 
+class Stats(C.Structure):
+    _fields_ = [
+        ("n_pose", C.c_int64),
+        ("n_point", C.c_int64),
+        ("n_factor", C.c_int64),
+        ("n_chain", C.c_int64),
+        ("n_edge", C.c_int64),
+        ("reduced_dim", C.c_int64),
+        ("band_tiles", C.c_int64),
+        ("band_max_tiles", C.c_int64),
+        ("lin_bytes", C.c_double),
+        ("assembly_bytes", C.c_double),
+        ("chol_flops", C.c_double),
+        ("chol_tile_flops", C.c_double),
+        ("ms_linearize", C.c_double),
+        ("ms_schur", C.c_double),
+        ("ms_assembly", C.c_double),
+        ("ms_cholesky", C.c_double),
+        ("ms_solve", C.c_double),
+        ("ms_backsub", C.c_double),
+        ("ms_retract_error", C.c_double),
+        ("n_linearize", C.c_int64),
+        ("n_solves", C.c_int64),
+    ]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+class SlidingWindowState(C.Structure):
+    _fields_ = [
+        ("sliding_window", C.c_int),
+        ("overlap_size", C.c_int),
+        ("previous_trigger_frame", C.c_int),
+        ("first_frame", C.c_int),
+    ]
+
+
 class SynthConfig(C.Structure):
     _fields_ = [
         ("frames", C.c_int),

@@ -84,8 +84,20 @@ def _declare(name, lib):
         lib.dynohip_linearize.restype = C.c_int
         lib.dynohip_linearize_size.argtypes = [vp]
         lib.dynohip_linearize_size.restype = C.c_size_t
-        lib.dynohip_get_phase_times.argtypes = [vp, P(C.c_double), C.c_size_t]
-        lib.dynohip_get_phase_times.restype = C.c_int
+        lib.dynohip_values_snapshot.argtypes = [vp]
+        lib.dynohip_values_snapshot.restype = C.c_int
+        lib.dynohip_values_restore.argtypes = [vp]
+        lib.dynohip_values_restore.restype = C.c_int
+        lib.dynohip_get_stats.argtypes = [vp, P(_abi.Stats)]
+        lib.dynohip_get_stats.restype = C.c_int
+        lib.dynohip_set_timing.argtypes = [vp, C.c_int]
+        lib.dynohip_set_timing.restype = C.c_int
+        lib.dynohip_sliding_window_init.argtypes = [P(_abi.SlidingWindowState), C.c_int, C.c_int]
+        lib.dynohip_sliding_window_init.restype = None
+        lib.dynohip_sliding_window_check.argtypes = [P(_abi.SlidingWindowState), C.c_uint64, P(C.c_uint64), P(C.c_uint64)]
+        lib.dynohip_sliding_window_check.restype = C.c_int
+        lib.dynohip_full_batch_trigger.argtypes = [C.c_int64, C.c_uint64]
+        lib.dynohip_full_batch_trigger.restype = C.c_int
         for fn, args, res in [
             ("dynohip_symbol", [C.c_ubyte, C.c_uint64], C.c_uint64),
             ("dynohip_labeled_symbol", [C.c_ubyte, C.c_ubyte, C.c_uint64], C.c_uint64),

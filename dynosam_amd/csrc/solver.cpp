@@ -13,6 +13,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -118,9 +119,14 @@ struct dynohip_solver {
   double lambda = 1e-5, error = 0.0;
   int iterations = 0, inner = 0, converged = 0;
   std::vector<dynohip_trace_entry> trace;
-  // phase timing
-  hipEvent_t ev[8] = {};
-  double phase_ms[7] = {};
+  // values snapshot (bench hook)
+  DevBuf<double> pose_snap, pt_snap;
+  // phase timing (HIP events, optional)
+  bool timing = false;
+  hipEvent_t ev[9] = {};
+  double phase_ms[7] = {};   // accumulated: lin, schur, assembly, chol, solve, backsub+linerr, retract+error
+  int64_t n_lin = 0, n_solves = 0;
+  dynohip_stats base_stats{};
 };
 
 namespace {
@@ -267,49 +273,111 @@ void enqueue_linearize(dynohip_solver* s) {
 
 // damped solve + linearised error + retract + error for one lambda.
 // result[0] = new linear error, result[1] = new nonlinear error; fail flag.
-void enqueue_try(dynohip_solver* s, double lambda, bool timed) {
+void enqueue_try(dynohip_solver* s, double lambda) {
+  const bool timed = s->timing;
   Plan& P = s->plan;
   hipStream_t st = s->stream;
   double* A = s->arena.p;
   const size_t nrp = static_cast<size_t>(P.NT) * kTile;
-  if (timed) (void)hipEventRecord(s->ev[1], st);
+  if (timed) (void)hipEventRecord(s->ev[2], st);
   (void)hipMemsetAsync(s->fail.p, 0, sizeof(int), st);
   (void)hipMemsetAsync(s->band.p, 0, P.band_size * sizeof(double), st);
   (void)hipMemsetAsync(s->gred.p, 0, nrp * sizeof(double), st);
   launch_chain_factor(s->cd, A, lambda, s->fail.p, st);
   launch_chain_solve_y(s->cd, A, st);
-  if (timed) (void)hipEventRecord(s->ev[2], st);
+  if (timed) (void)hipEventRecord(s->ev[3], st);
   launch_gather_band(s->gRed.dev(P.gRed.ntargets()), A, s->redA.p, s->redB.p, s->bd, lambda, st);
   launch_band_pad(s->bd, st);
   launch_gather_grad(s->gGred.dev(P.gGred.ntargets()), A, s->gred.p, st);
-  if (timed) (void)hipEventRecord(s->ev[3], st);
-  launch_band_cholesky(s->bd, P.band_D.data(), s->fail.p, st);
   if (timed) (void)hipEventRecord(s->ev[4], st);
+  launch_band_cholesky(s->bd, P.band_D.data(), s->fail.p, st);
+  if (timed) (void)hipEventRecord(s->ev[5], st);
   double* y = s->xy.p;
   double* x = s->xy.p + nrp;
   launch_band_solve(s->bd, s->gred.p, y, x, st);
-  if (timed) (void)hipEventRecord(s->ev[5], st);
+  if (timed) (void)hipEventRecord(s->ev[6], st);
   // pose deltas are x[0 .. 6 n_pose) in pose-index order
   launch_backsub(s->cd, A, x, s->dpt.p, st);
   enqueue_linerr(s, x, s->dpt.p, s->partials.p, s->result.p);
-  if (timed) (void)hipEventRecord(s->ev[6], st);
+  if (timed) (void)hipEventRecord(s->ev[7], st);
   launch_retract(P.n_pose, P.n_pt, s->pose.p, s->pt.p, x, s->dpt.p, s->pose_c.p, s->pt_c.p, st);
   enqueue_error(s, s->pose_c.p, s->pt_c.p, s->partials.p + s->partial_slots, s->result.p + 1);
-  if (timed) (void)hipEventRecord(s->ev[7], st);
+  if (timed) (void)hipEventRecord(s->ev[8], st);
 }
 
 void push_trace(dynohip_solver* s, const dynohip_trace_entry& e) { s->trace.push_back(e); }
 
+// algorithmic work per linearisation / assembly / factorisation
+void compute_base_stats(dynohip_solver* s) {
+  const Plan& P = s->plan;
+  dynohip_stats& st = s->base_stats;
+  std::memset(&st, 0, sizeof(st));
+  st.n_pose = P.n_pose;
+  st.n_point = P.n_pt;
+  st.n_chain = P.n_comp;
+  st.n_edge = P.n_edge;
+  st.reduced_dim = P.n_red;
+  int64_t tiles = 0;
+  for (int j = 0; j < P.NT; ++j) tiles += P.band_D[j] + 1;
+  st.band_tiles = tiles;
+  st.band_max_tiles = P.max_D;
+  double lin = 0.0;
+  for (int t = 0; t < kNTypes; ++t) {
+    const TypePlan& tp = P.types[t];
+    st.n_factor += tp.n;
+    double per = 4.0 * kNKeys[t] + 8.0 * kMeasDim[t] + 8.0 * kDim[t] + 8.0 + 8.0 * tp.stride;
+    for (int sl = 0; sl < kNKeys[t]; ++sl) per += kSlotKind[t][sl] == 0 ? 96.0 : 24.0;
+    lin += per * tp.n;
+  }
+  st.lin_bytes = lin;
+  double asmb = 0.0;
+  for (const GEntry& e : P.gRed.ent) asmb += 16.0 + 8.0 * e.k * 12.0;
+  for (const GEntry& e : P.gGred.ent) asmb += 16.0 + 8.0 * e.k * 7.0;
+  asmb += 36.0 * 8.0 * P.gRed.ntargets() + 6.0 * 8.0 * P.n_pose;
+  st.assembly_bytes = asmb;
+  // envelope Cholesky flop count of the reduced system
+  std::vector<int32_t> firstpose(P.n_pose);
+  for (int a = 0; a < P.n_pose; ++a) firstpose[a] = a;
+  for (size_t t = 0; t < P.red_A.size(); ++t)
+    firstpose[P.red_A[t]] = std::min(firstpose[P.red_A[t]], P.red_B[t]);
+  // rows of a pose share f_i; flops(i, j) = 2 * (j - max(f_i, f_j)) (+ 1)
+  double fl = 0.0;
+  for (int a = 0; a < P.n_pose; ++a) {
+    const int64_t fi = 6ll * firstpose[a];
+    for (int r = 0; r < 6; ++r) {
+      const int64_t i = 6ll * a + r;
+      for (int64_t j = fi; j <= i; ++j) {
+        const int64_t fj = 6ll * firstpose[j / 6];
+        fl += 2.0 * static_cast<double>(j - std::max(fi, fj)) + 1.0;
+      }
+    }
+  }
+  st.chol_flops = fl;
+  const double T3 = static_cast<double>(kTile) * kTile * kTile;
+  double tf = 0.0;
+  for (int j = 0; j < P.NT; ++j) {
+    const double D = P.band_D[j];
+    tf += T3 / 3.0 + D * T3 + D * (D + 1) / 2.0 * 2.0 * T3;
+  }
+  st.chol_tile_flops = tf;
+}
+
 // LevenbergMarquardtOptimizer::iterate()
 int lm_iterate(dynohip_solver* s) {
   hipStream_t st = s->stream;
-  (void)hipEventRecord(s->ev[0], st);
+  if (s->timing) (void)hipEventRecord(s->ev[0], st);
   enqueue_linearize(s);
+  if (s->timing) (void)hipEventRecord(s->ev[1], st);
   enqueue_linerr(s, nullptr, nullptr, s->partials.p, s->result.p + 2);
   double oldLin = 0.0;
   HIPCHK(s, hipMemcpyAsync(&oldLin, s->result.p + 2, sizeof(double), hipMemcpyDeviceToHost, st));
   HIPCHK(s, hipStreamSynchronize(st));
-  bool first = true;
+  s->n_lin++;
+  if (s->timing) {
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, s->ev[0], s->ev[1]);
+    s->phase_ms[0] += ms;
+  }
   for (;;) {
     dynohip_trace_entry te{};
     te.outer_iteration = s->iterations;
@@ -317,19 +385,19 @@ int lm_iterate(dynohip_solver* s) {
     te.current_error = s->error;
     te.new_error = INFINITY;
     te.old_linear_error = oldLin;
-    enqueue_try(s, s->lambda, first);
+    enqueue_try(s, s->lambda);
     double res[2];
     int fail = 0;
     HIPCHK(s, hipMemcpyAsync(res, s->result.p, 2 * sizeof(double), hipMemcpyDeviceToHost, st));
     HIPCHK(s, hipMemcpyAsync(&fail, s->fail.p, sizeof(int), hipMemcpyDeviceToHost, st));
     HIPCHK(s, hipStreamSynchronize(st));
-    if (first) {
+    s->n_solves++;
+    if (s->timing) {
       float ms = 0.f;
-      for (int k = 0; k < 7; ++k) {
+      for (int k = 2; k < 8; ++k) {
         (void)hipEventElapsedTime(&ms, s->ev[k], s->ev[k + 1]);
-        s->phase_ms[k] = ms;
+        s->phase_ms[k - 1] += ms;
       }
-      first = false;
     }
     const int solved = fail == 0 && std::isfinite(res[0]);
     te.solved = solved;
@@ -484,6 +552,7 @@ int dynohip_set_values(dynohip_solver* s, const uint64_t* keys, const uint8_t* k
     if (rc) return rc;
     s->value_keys.assign(keys, keys + n);
     s->has_plan = true;
+    compute_base_stats(s);
   }
   Plan& P = s->plan;
   std::vector<double> hp(12ull * P.n_pose), hq(3ull * P.n_pt);
@@ -546,6 +615,9 @@ int dynohip_lm_reset(dynohip_solver* s, const dynohip_lm_params* p) {
   s->inner = 0;
   s->converged = 0;
   s->trace.clear();
+  s->n_lin = 0;
+  s->n_solves = 0;
+  for (double& v : s->phase_ms) v = 0.0;
   return compute_error(s, s->pose.p, s->pt.p, &s->error);
 }
 
@@ -637,9 +709,49 @@ int dynohip_linearize(dynohip_solver* s, double* out, size_t n_doubles) {
   return DYNOHIP_OK;
 }
 
-int dynohip_get_phase_times(dynohip_solver* s, double* ms_out, size_t n) {
-  if (!s || !ms_out) return DYNOHIP_EINVAL;
-  for (size_t k = 0; k < n && k < 7; ++k) ms_out[k] = s->phase_ms[k];
+int dynohip_values_snapshot(dynohip_solver* s) {
+  int rc = ready(s);
+  if (rc) return rc;
+  (void)hipSetDevice(s->device);
+  const Plan& P = s->plan;
+  if (!s->pose_snap.p && P.n_pose) HIPCHK(s, s->pose_snap.alloc(12ull * P.n_pose));
+  if (!s->pt_snap.p && P.n_pt) HIPCHK(s, s->pt_snap.alloc(3ull * P.n_pt));
+  if (P.n_pose) HIPCHK(s, hipMemcpyAsync(s->pose_snap.p, s->pose.p, 12ull * P.n_pose * sizeof(double), hipMemcpyDeviceToDevice, s->stream));
+  if (P.n_pt) HIPCHK(s, hipMemcpyAsync(s->pt_snap.p, s->pt.p, 3ull * P.n_pt * sizeof(double), hipMemcpyDeviceToDevice, s->stream));
+  HIPCHK(s, hipStreamSynchronize(s->stream));
+  return DYNOHIP_OK;
+}
+
+int dynohip_values_restore(dynohip_solver* s) {
+  int rc = ready(s);
+  if (rc) return rc;
+  const Plan& P = s->plan;
+  if ((P.n_pose && !s->pose_snap.p) || (P.n_pt && !s->pt_snap.p)) return set_err(s, DYNOHIP_ESTATE, "no snapshot");
+  (void)hipSetDevice(s->device);
+  if (P.n_pose) HIPCHK(s, hipMemcpyAsync(s->pose.p, s->pose_snap.p, 12ull * P.n_pose * sizeof(double), hipMemcpyDeviceToDevice, s->stream));
+  if (P.n_pt) HIPCHK(s, hipMemcpyAsync(s->pt.p, s->pt_snap.p, 3ull * P.n_pt * sizeof(double), hipMemcpyDeviceToDevice, s->stream));
+  HIPCHK(s, hipStreamSynchronize(s->stream));
+  return DYNOHIP_OK;
+}
+
+int dynohip_get_stats(dynohip_solver* s, dynohip_stats* out) {
+  if (!s || !out) return DYNOHIP_EINVAL;
+  *out = s->base_stats;
+  out->ms_linearize = s->phase_ms[0];
+  out->ms_schur = s->phase_ms[1];
+  out->ms_assembly = s->phase_ms[2];
+  out->ms_cholesky = s->phase_ms[3];
+  out->ms_solve = s->phase_ms[4];
+  out->ms_backsub = s->phase_ms[5];
+  out->ms_retract_error = s->phase_ms[6];
+  out->n_linearize = s->n_lin;
+  out->n_solves = s->n_solves;
+  return DYNOHIP_OK;
+}
+
+int dynohip_set_timing(dynohip_solver* s, int enabled) {
+  if (!s) return DYNOHIP_EINVAL;
+  s->timing = enabled != 0;
   return DYNOHIP_OK;
 }
 

@@ -103,10 +103,19 @@ class Solver:
         _check(self.lib, self.h, self.lib.dynohip_linearize(self.h, out.ctypes.data_as(C.POINTER(C.c_double)), n))
         return out
 
-    def phase_times(self):
-        out = np.zeros(7)
-        self.lib.dynohip_get_phase_times(self.h, out.ctypes.data_as(C.POINTER(C.c_double)), 7)
-        return out
+    def stats(self):
+        st = _abi.Stats()
+        _check(self.lib, self.h, self.lib.dynohip_get_stats(self.h, C.byref(st)))
+        return st.as_dict()
+
+    def set_timing(self, enabled=True):
+        _check(self.lib, self.h, self.lib.dynohip_set_timing(self.h, 1 if enabled else 0))
+
+    def snapshot(self):
+        _check(self.lib, self.h, self.lib.dynohip_values_snapshot(self.h))
+
+    def restore(self):
+        _check(self.lib, self.h, self.lib.dynohip_values_restore(self.h))
 
 
 class LevenbergMarquardtOptimizer:

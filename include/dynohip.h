@@ -193,10 +193,53 @@ int dynohip_get_trace(dynohip_solver* s, dynohip_trace_entry* out,
 int dynohip_linearize(dynohip_solver* s, double* out, size_t n_doubles);
 size_t dynohip_linearize_size(const dynohip_solver* s);
 
-/* Device time (ms, HIP events) of the last iterate/optimize split into
-   phases; for the bench: [linearize, schur, reduced_assembly, factor,
-   solve, backsub+lin_error, retract+error]. */
-int dynohip_get_phase_times(dynohip_solver* s, double* ms_out, size_t n);
+/* Bench hooks: device-side snapshot / restore of the current values (no
+   PCIe traffic), and problem / work statistics. */
+int dynohip_values_snapshot(dynohip_solver* s);
+int dynohip_values_restore(dynohip_solver* s);
+
+typedef struct {
+  int64_t n_pose, n_point, n_factor, n_chain, n_edge;
+  int64_t reduced_dim;       /* 6 * n_pose                                  */
+  int64_t band_tiles;        /* 64x64 tiles stored for the reduced band     */
+  int64_t band_max_tiles;    /* max sub-diagonal tiles in a column          */
+  double lin_bytes;          /* algorithmic HBM bytes of one linearisation
+                                (factor records + values read, J|b written) */
+  double assembly_bytes;     /* algorithmic bytes of one reduced assembly
+                                (gather lists + blocks read, band written)  */
+  double chol_flops;         /* algorithmic flops of one envelope Cholesky  */
+  double chol_tile_flops;    /* flops actually issued by the tile algorithm */
+  /* accumulated device time (ms, HIP events) and counts since lm_reset */
+  double ms_linearize, ms_schur, ms_assembly, ms_cholesky, ms_solve,
+         ms_backsub, ms_retract_error;
+  int64_t n_linearize, n_solves;
+} dynohip_stats;
+
+int dynohip_get_stats(dynohip_solver* s, dynohip_stats* out);
+/* 1: record HIP events around every phase (default 0: none) */
+int dynohip_set_timing(dynohip_solver* s, int enabled);
+
+/* ------------------------------------------------------------------ */
+/* Window / batch drivers (integer, bit-exact)                          */
+/* ------------------------------------------------------------------ */
+/* RGBDBackendModule::SlidingWindow (RGBDBackendModule.hpp:87-145) */
+typedef struct {
+  int sliding_window;
+  int overlap_size;
+  int previous_trigger_frame;  /* starts at overlap_size                    */
+  int first_frame;             /* -1 until the first check                  */
+} dynohip_sliding_window;
+
+void dynohip_sliding_window_init(dynohip_sliding_window* w, int window,
+                                 int overlap);
+/* SlidingWindow::check(frame_k): returns the condition (1/0) and writes the
+   window [frame_k - window, frame_k] bounds. */
+int dynohip_sliding_window_check(dynohip_sliding_window* w, uint64_t frame_k,
+                                 uint64_t* starting_frame,
+                                 uint64_t* ending_frame);
+/* RGBDBackendModule.cc:201-202: full batch runs when
+   full_batch_frame - 1 == frame_k */
+int dynohip_full_batch_trigger(int64_t full_batch_frame, uint64_t frame_k);
 
 /* ------------------------------------------------------------------ */
 /* Keys (integer, bit-exact with gtsam::Symbol / LabeledSymbol and      */

@@ -11,7 +11,7 @@ names = sys.argv[1:] or ["T1", "T2", "C1"]
 for name in names:
     g, v, gt = synth.generate(name)
     s = Solver(0)
-    s.set_graph(g); s.set_values(v)
+    s.set_graph(g); s.set_values(v); s.set_timing(True)
     o = Oracle(g, v)
     print(f"== {name}: values {len(v)} factors {g.size()}", flush=True)
     e_gpu, e_orc = s.error(), o.error()
@@ -31,5 +31,5 @@ for name in names:
     rel = np.linalg.norm(s.values_data() - o2.values_data()) / np.linalg.norm(o2.values_data())
     print(f"optimize gpu it={sg.iterations} inner={sg.inner_iterations} err={sg.final_error:.6e} {tg*1e3:.1f} ms | "
           f"oracle it={so.iterations} inner={so.inner_iterations} err={so.final_error:.6e} {to*1e3:.1f} ms | rel {rel:.3e}", flush=True)
-    print("phase ms", s.phase_times(), flush=True)
+    print("stats", s.stats(), flush=True)
     s.close()
