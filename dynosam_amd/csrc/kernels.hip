@@ -19,7 +19,6 @@ namespace dynohip {
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kLdp = kTile + 1;  // padded LDS row stride (doubles)
 
 inline int nblocks(int64_t n, int b = kBlock) { return static_cast<int>((n + b - 1) / b); }
 
@@ -730,156 +729,6 @@ __global__ void k_band_pad(BandDev b) {
   b.band[band_index(b, row, row)] = 1.0;
 }
 
-// factor diagonal tile j (every block, redundantly, in LDS), block 0 stores
-// it, block d >= 1 solves X L^T = A for tile (j+d, j)
-__global__ __launch_bounds__(kBlock) void k_potrf_trsm(BandDev b, int j, int* fail) {
-  __shared__ double Lt[kTile * kLdp];
-  __shared__ double At[kTile * kLdp];
-  const int tid = threadIdx.x;
-  const int d = blockIdx.x;
-  double* diag = b.band + b.off[j];
-  for (int e = tid; e < kTile * kTile; e += kBlock) Lt[(e / kTile) * kLdp + e % kTile] = diag[e];
-  if (d > 0) {
-    const double* src = diag + static_cast<int64_t>(d) * kTile * kTile;
-    for (int e = tid; e < kTile * kTile; e += kBlock) At[(e / kTile) * kLdp + e % kTile] = src[e];
-  }
-  __syncthreads();
-  const int row = tid & 63, q = tid >> 6;
-  for (int k = 0; k < kTile; ++k) {
-    double akk = Lt[k * kLdp + k];
-    if (!(akk > 0.0)) {
-      if (tid == 0) *fail = 1;
-      akk = 1.0;
-    }
-    const double lkk = sqrt(akk);
-    __syncthreads();
-    if (q == 0 && row > k) Lt[row * kLdp + k] /= lkk;
-    if (tid == 0) Lt[k * kLdp + k] = lkk;
-    __syncthreads();
-    if (row > k) {
-      const double lik = Lt[row * kLdp + k];
-      for (int jj = k + 1 + q; jj <= row; jj += 4) Lt[row * kLdp + jj] -= lik * Lt[jj * kLdp + k];
-    }
-    __syncthreads();
-  }
-  if (d == 0) {
-    for (int e = tid; e < kTile * kTile; e += kBlock) {
-      const int r = e / kTile, c = e % kTile;
-      diag[e] = c <= r ? Lt[r * kLdp + c] : 0.0;
-    }
-    return;
-  }
-  // X L^T = A: 4 lanes per row within a wave (row = tid >> 2, part = tid & 3)
-  const int r = tid >> 2, p = tid & 3;
-  for (int k = 0; k < kTile; ++k) {
-    double s = 0.0;
-    for (int m = p; m < k; m += 4) s += At[r * kLdp + m] * Lt[k * kLdp + m];
-    s += __shfl_xor(s, 1);
-    s += __shfl_xor(s, 2);
-    const double x = (At[r * kLdp + k] - s) / Lt[k * kLdp + k];
-    __builtin_amdgcn_wave_barrier();
-    At[r * kLdp + k] = x;
-    __builtin_amdgcn_wave_barrier();
-  }
-  __syncthreads();
-  double* dst = diag + static_cast<int64_t>(d) * kTile * kTile;
-  for (int e = tid; e < kTile * kTile; e += kBlock) dst[e] = At[(e / kTile) * kLdp + e % kTile];
-}
-
-// trailing update of column j: tile(j+d1, j+d2) -= L(j+d1,j) L(j+d2,j)^T
-__global__ __launch_bounds__(kBlock) void k_update(BandDev b, int j) {
-  __shared__ double As[kTile * kLdp];
-  __shared__ double Bs[kTile * kLdp];
-  // blockIdx -> (d1, d2), 1 <= d2 <= d1
-  int t = blockIdx.x, d1 = 1;
-  while (t >= d1) { t -= d1; ++d1; }
-  const int d2 = t + 1;
-  const double* A = b.band + b.off[j] + static_cast<int64_t>(d1) * kTile * kTile;
-  const double* B = b.band + b.off[j] + static_cast<int64_t>(d2) * kTile * kTile;
-  double* C = b.band + b.off[j + d2] + static_cast<int64_t>(d1 - d2) * kTile * kTile;
-  const int tid = threadIdx.x;
-  for (int e = tid; e < kTile * kTile; e += kBlock) {
-    As[(e / kTile) * kLdp + e % kTile] = A[e];
-    Bs[(e / kTile) * kLdp + e % kTile] = B[e];
-  }
-  __syncthreads();
-  const int r0 = (tid >> 4) * 4, c0 = (tid & 15) * 4;
-  double acc[4][4] = {};
-  for (int k = 0; k < kTile; ++k) {
-    double a[4], bb[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) { a[u] = As[(r0 + u) * kLdp + k]; bb[u] = Bs[(c0 + u) * kLdp + k]; }
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int w = 0; w < 4; ++w) acc[u][w] += a[u] * bb[w];
-  }
-#pragma unroll
-  for (int u = 0; u < 4; ++u)
-#pragma unroll
-    for (int w = 0; w < 4; ++w) C[(r0 + u) * kTile + c0 + w] -= acc[u][w];
-}
-
-// forward L y = g, backward L^T x = y over the tile band (one workgroup)
-__global__ __launch_bounds__(kBlock) void k_band_solve(BandDev b, const double* __restrict__ g,
-                                                       double* __restrict__ y, double* __restrict__ x) {
-  __shared__ double Ld[kTile * kLdp];
-  __shared__ double part[4][kTile];
-  __shared__ double rv[kTile];
-  const int tid = threadIdx.x, row = tid & 63, q = tid >> 6;
-  for (int i = 0; i < b.NT; ++i) {
-    double s = 0.0;
-    for (int c = b.cmin[i]; c < i; ++c) {
-      const double* T = b.band + b.off[c] + static_cast<int64_t>(i - c) * kTile * kTile;
-      const double* yc = y + static_cast<int64_t>(c) * kTile;
-      for (int m = q; m < kTile; m += 4) s += T[row * kTile + m] * yc[m];
-    }
-    part[q][row] = s;
-    const double* D = b.band + b.off[i];
-    for (int e = tid; e < kTile * kTile; e += kBlock) Ld[(e / kTile) * kLdp + e % kTile] = D[e];
-    __syncthreads();
-    if (tid < 64) {
-      rv[row] = g[static_cast<int64_t>(i) * kTile + row] - ((part[0][row] + part[1][row]) + (part[2][row] + part[3][row]));
-      __builtin_amdgcn_wave_barrier();
-      for (int k = 0; k < kTile; ++k) {
-        const double yk = rv[k] / Ld[k * kLdp + k];
-        __builtin_amdgcn_wave_barrier();
-        if (row > k) rv[row] -= Ld[row * kLdp + k] * yk;
-        if (row == k) rv[row] = yk;
-        __builtin_amdgcn_wave_barrier();
-      }
-      y[static_cast<int64_t>(i) * kTile + row] = rv[row];
-    }
-    __syncthreads();
-  }
-  for (int i = b.NT - 1; i >= 0; --i) {
-    double s = 0.0;
-    const int D = b.D[i];
-    for (int dd = 1; dd <= D; ++dd) {
-      const double* T = b.band + b.off[i] + static_cast<int64_t>(dd) * kTile * kTile;
-      const double* xc = x + static_cast<int64_t>(i + dd) * kTile;
-      for (int m = q; m < kTile; m += 4) s += T[m * kTile + row] * xc[m];
-    }
-    part[q][row] = s;
-    const double* Dg = b.band + b.off[i];
-    for (int e = tid; e < kTile * kTile; e += kBlock) Ld[(e / kTile) * kLdp + e % kTile] = Dg[e];
-    __syncthreads();
-    if (tid < 64) {
-      rv[row] = y[static_cast<int64_t>(i) * kTile + row] - ((part[0][row] + part[1][row]) + (part[2][row] + part[3][row]));
-      __builtin_amdgcn_wave_barrier();
-      for (int k = kTile - 1; k >= 0; --k) {
-        const double xk = rv[k] / Ld[k * kLdp + k];
-        __builtin_amdgcn_wave_barrier();
-        if (row < k) rv[row] -= Ld[k * kLdp + row] * xk;
-        if (row == k) rv[row] = xk;
-        __builtin_amdgcn_wave_barrier();
-      }
-      x[static_cast<int64_t>(i) * kTile + row] = rv[row];
-    }
-    __syncthreads();
-  }
-}
-
 // ---------------------------------------------------------------- retract
 __global__ __launch_bounds__(kBlock) void k_retract(int n_pose, int n_pt, const double* __restrict__ pose,
                                                     const double* __restrict__ pt, const double* __restrict__ dpose,
@@ -975,19 +824,6 @@ void launch_band_pad(const BandDev& b, hipStream_t s) {
   const int npad = b.NT * kTile - b.n_red;
   if (npad <= 0) return;
   k_band_pad<<<1, kTile, 0, s>>>(b);
-}
-
-void launch_band_cholesky(const BandDev& b, const int32_t* host_D, int* fail, hipStream_t s) {
-  for (int j = 0; j < b.NT; ++j) {
-    const int D = host_D[j];
-    k_potrf_trsm<<<D + 1, kBlock, 0, s>>>(b, j, fail);
-    if (D > 0) k_update<<<D * (D + 1) / 2, kBlock, 0, s>>>(b, j);
-  }
-}
-
-void launch_band_solve(const BandDev& b, const double* g, double* y, double* x, hipStream_t s) {
-  if (b.NT == 0) return;
-  k_band_solve<<<1, kBlock, 0, s>>>(b, g, y, x);
 }
 
 void launch_retract(int n_pose, int n_pt, const double* pose, const double* pt, const double* dpose,

@@ -73,8 +73,11 @@ void launch_chain_solve_y(const ChainDev& c, double* arena, hipStream_t s);
 void launch_backsub(const ChainDev& c, const double* arena, const double* dpose, double* dpt, hipStream_t s);
 
 void launch_band_pad(const BandDev& b, hipStream_t s);
-void launch_band_cholesky(const BandDev& b, const int32_t* host_D, int* fail, hipStream_t s);
-void launch_band_solve(const BandDev& b, const double* g, double* y, double* x, hipStream_t s);
+// factor the band and solve (L L^T) x = r; r is overwritten (forward
+// substitution is fused into the factorisation), Linv holds NT diagonal
+// inverse tiles, y the forward result
+void launch_band_cholesky_solve(const BandDev& b, const int32_t* host_D, double* Linv, double* r, double* y,
+                                double* x, int* fail, hipStream_t s);
 
 void launch_retract(int n_pose, int n_pt, const double* pose, const double* pt, const double* dpose,
                     const double* dpt, double* pose_out, double* pt_out, hipStream_t s);

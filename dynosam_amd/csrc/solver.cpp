@@ -106,7 +106,7 @@ struct dynohip_solver {
   DevBuf<int32_t> comp_start, comp_nb_start, nb_comp, nbedge_start, nbedge_pt, pt_edge_start, edge_pose;
   DevBuf<int64_t> comp_y_base;
   DevBuf<uint32_t> nbedge_w;
-  DevBuf<double> band, gred, xy, dpt;
+  DevBuf<double> band, gred, xy, dpt, linv;
   DevBuf<int64_t> band_off;
   DevBuf<int32_t> band_D, band_cmin;
   DevBuf<double> partials, result;
@@ -203,6 +203,7 @@ int upload_plan(dynohip_solver* s) {
   const size_t nrp = static_cast<size_t>(P.NT) * kTile;
   HIPCHK(s, s->gred.alloc(nrp > 0 ? nrp : 1));
   HIPCHK(s, s->xy.alloc(2 * (nrp > 0 ? nrp : 1)));
+  HIPCHK(s, s->linv.alloc(static_cast<size_t>(P.NT) * kTile * kTile + 1));
   HIPCHK(s, s->dpt.alloc(3ull * P.n_pt + 1));
   ChainDev& c = s->cd;
   c.n_comp = P.n_comp;
@@ -290,11 +291,10 @@ void enqueue_try(dynohip_solver* s, double lambda) {
   launch_band_pad(s->bd, st);
   launch_gather_grad(s->gGred.dev(P.gGred.ntargets()), A, s->gred.p, st);
   if (timed) (void)hipEventRecord(s->ev[4], st);
-  launch_band_cholesky(s->bd, P.band_D.data(), s->fail.p, st);
-  if (timed) (void)hipEventRecord(s->ev[5], st);
   double* y = s->xy.p;
   double* x = s->xy.p + nrp;
-  launch_band_solve(s->bd, s->gred.p, y, x, st);
+  launch_band_cholesky_solve(s->bd, P.band_D.data(), s->linv.p, s->gred.p, y, x, s->fail.p, st);
+  if (timed) (void)hipEventRecord(s->ev[5], st);
   if (timed) (void)hipEventRecord(s->ev[6], st);
   // pose deltas are x[0 .. 6 n_pose) in pose-index order
   launch_backsub(s->cd, A, x, s->dpt.p, st);
