@@ -1,17 +1,25 @@
 // band.hip — block-banded Cholesky of the reduced (Schur) pose system and
-// its triangular solves, 64x64 FP64 tiles, lower band stored by column tile.
+// its triangular solves: 64x64 FP64 tiles, lower band stored by column tile
+// (tile (j+d, j) at off[j] + d*4096, row-major), D_j sub-diagonal tiles.
 //
-// Per column tile j (stream-ordered launches, no inter-workgroup sync):
-//   k_panel(j)   grid D_j+1: every workgroup factors the diagonal tile in
-//                registers (right-looking, 4x4 sub-block per thread, one
-//                barrier per pivot) and builds L_jj^-1 alongside; block 0
-//                stores L_jj^-1 and y_j = L_jj^-1 r_j (forward substitution
-//                fused into the factorisation); block d >= 1 turns tile
-//                (j+d, j) into L(j+d, j) = A L_jj^-T (a GEMM with the
-//                explicit inverse) and applies r_{j+d} -= L(j+d, j) y_j.
-//   k_update(j)  grid D_j(D_j+1)/2: trailing tiles -= L(j+d1,j) L(j+d2,j)^T.
-//   k_band_back  one workgroup: x_j = L_jj^-T (y_j - sum_d L(j+d,j)^T x_{j+d}).
-// A non-positive pivot sets *fail (the LM treats the step as failed,
+// One launch per column tile j, k_step(j), with two kinds of workgroups:
+//   panel blocks d = 0..D_j   apply column j-1's contribution to their own
+//       tile (j+d, j) and to the diagonal tile (j, j) (right-looking update,
+//       so no other launch is needed for column j), factor the diagonal
+//       tile in registers (4x4-blocked: one thread factors and inverts each
+//       4x4 diagonal sub-block, two barriers per 4 pivots) together with
+//       L_jj^-1, and then
+//         d == 0: store L_jj^-1 and y_j = L_jj^-1 r_j (forward substitution
+//                 fused into the factorisation),
+//         d >= 1: L(j+d, j) = A L_jj^-T (FP64 MFMA GEMM with the explicit
+//                 inverse), r_{j+d} -= L(j+d, j) y_j;
+//   update blocks             the rest of column j-1's trailing update:
+//       tile (j-1+d1, j-1+d2) -= L(j-1+d1, j-1) L(j-1+d2, j-1)^T, d2 >= 2.
+// Every tile receives each column's contribution exactly once and no
+// workgroup writes what another workgroup of the same launch reads, so the
+// result is deterministic. k_band_back then runs
+// x_j = L_jj^-T (y_j - sum_d L(j+d,j)^T x_{j+d}) in one workgroup.
+// A non-positive pivot sets *fail (the LM treats the step as failed:
 // GTSAM's IndeterminantLinearSystemException path).
 #include <hip/hip_runtime.h>
 
@@ -22,41 +30,9 @@ namespace dynohip {
 namespace {
 
 constexpr int T = kTile;
-constexpr int LD = T + 1;            // padded LDS row stride
-constexpr int kPanelThreads = 320;  // 5 waves: 272 sub-block owners
-constexpr int kSub = 16;             // 4x4 sub-blocks per tile side
-constexpr int kLowerSub = kSub * (kSub + 1) / 2;  // 136
+constexpr int LD = T + 4;            // padded LDS row stride (doubles)
 
-__device__ __forceinline__ void sub_index(int s, int& bi, int& bj) {
-  int i = static_cast<int>((sqrtf(8.0f * s + 1.0f) - 1.0f) * 0.5f);
-  while (i * (i + 1) / 2 > s) --i;
-  while ((i + 1) * (i + 2) / 2 <= s) ++i;
-  bi = i;
-  bj = s - i * (i + 1) / 2;
-}
-
-// 64x64x64 GEMM on LDS operands: C[r][c] = sum_m A[r][m] * B[c][m]
-// (B^T product), 4x4 outputs per thread for threads 0..255.
-__device__ __forceinline__ void gemm_abt_4x4(const double* As, const double* Bs, int tid, double acc[4][4],
-                                             int mmax = T) {
-  const int r0 = (tid >> 4) * 4, c0 = (tid & 15) * 4;
-#pragma unroll
-  for (int u = 0; u < 4; ++u)
-#pragma unroll
-    for (int w = 0; w < 4; ++w) acc[u][w] = 0.0;
-  for (int m = 0; m < mmax; ++m) {
-    double a[4], b[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      a[u] = As[(r0 + u) * LD + m];
-      b[u] = Bs[(c0 + u) * LD + m];
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int w = 0; w < 4; ++w) acc[u][w] += a[u] * b[w];
-  }
-}
+typedef double v4d __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void load_tile_lds(const double* __restrict__ src, double* dst, int tid, int nthreads) {
   const double2* s2 = reinterpret_cast<const double2*>(src);
@@ -68,187 +44,279 @@ __device__ __forceinline__ void load_tile_lds(const double* __restrict__ src, do
   }
 }
 
-__global__ __launch_bounds__(kPanelThreads) void k_panel(BandDev b, int j, double* __restrict__ Linv,
-                                                         double* __restrict__ r, double* __restrict__ y,
-                                                         int* fail) {
-  __shared__ double As[T * LD];
-  __shared__ double Xs[T * LD];
-  __shared__ double colbuf[2][T];
-  __shared__ double rowbuf[2][T];
-  __shared__ double akkbuf[2];
-  __shared__ double yv[T];
-  const int tid = threadIdx.x;
-  const int d = blockIdx.x;
-  const double* diag = b.band + b.off[j];
-  if (d > 0) load_tile_lds(diag + static_cast<int64_t>(d) * T * T, As, tid, kPanelThreads);
-  // ---- roles: 136 threads own 4x4 sub-blocks of A (lower), 136 of the inverse
-  const bool isA = tid < kLowerSub;
-  const bool isX = tid >= kLowerSub && tid < 2 * kLowerSub;
-  int bi = 0, bj = 0;
-  if (isA) sub_index(tid, bi, bj);
-  if (isX) sub_index(tid - kLowerSub, bi, bj);
-  double v[4][4];
-  if (isA) {
+// 64x64x64 C = A B^T on LDS operands with v_mfma_f64_16x16x4f64; waves 0..3
+// each own a 32x32 quadrant (2x2 MFMA tiles). Lane l feeds A[i0+(l&15)][k0+(l>>4)]
+// and B[j0+(l&15)][k0+(l>>4)]; result acc[ti][tj][r] = C[i0+16ti+(l>>4)+4r][j0+16tj+(l&15)].
+__device__ __forceinline__ void mfma_abt(const double* As, const double* Bs, int wave, int lane, v4d acc[2][2]) {
+  const int i0 = 32 * (wave >> 1), j0 = 32 * (wave & 1);
+  const int li = lane & 15, lk = lane >> 4;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const double4 q = *reinterpret_cast<const double4*>(diag + (4 * bi + u) * T + 4 * bj);
-      v[u][0] = q.x; v[u][1] = q.y; v[u][2] = q.z; v[u][3] = q.w;
-    }
-  } else {
+  for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int w = 0; w < 4; ++w) v[u][w] = (isX && bi == bj && u == w) ? 1.0 : 0.0;
-  }
-  // Right-looking elimination of A and forward elimination of [A | I]:
-  // at pivot k, with c_i = a_ik (i > k, else 0), r_c = acc_kc (row k of the
-  // running inverse, exactly 0 for c > k):
-  //   a_ij  -= c_i c_j / a_kk        (i, j > k; lower part kept)
-  //   acc_ic -= c_i r_c / a_kk       (i > k)
-  //   acc_kc *= 1 / sqrt(a_kk)       (row k of L^-1 is final)
-  // Publishers write exact zeros where a row / column is inactive, so every
-  // update below is unconditional (no per-element branches).
-  bool bad = false;
-#ifndef DH_NO_PIVOT
-  for (int kb = 0; kb < kSub; ++kb) {
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const int k = 4 * kb + kk, p = kk & 1;
-      if (isA && bj == kb) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int i = 4 * bi + u;
-          colbuf[p][i] = i > k ? v[u][kk] : 0.0;
-          if (i == k) akkbuf[p] = v[u][kk];
-        }
-      }
-      if (isX && bi == kb) {
-#pragma unroll
-        for (int w = 0; w < 4; ++w) rowbuf[p][4 * bj + w] = v[kk][w];
-      }
-      __syncthreads();
-      double akk = akkbuf[p];
-      if (!(akk > 0.0) || !isfinite(akk)) {
-        bad = true;
-        akk = 1.0;
-      }
-#ifdef DH_FAST_RCP
-      double rinv = __builtin_amdgcn_rcp(akk);
-      rinv = rinv * (2.0 - akk * rinv);
-      rinv = rinv * (2.0 - akk * rinv);
-#else
-      const double rinv = 1.0 / akk;
-#endif
-      if (isA && bj >= kb) {
-        double ci[4], cj[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          ci[u] = colbuf[p][4 * bi + u] * rinv;
-          cj[u] = colbuf[p][4 * bj + u];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-          for (int w = 0; w < 4; ++w) v[u][w] -= ci[u] * cj[w];
-      }
-      if (isX && bi >= kb && bj <= kb) {
-        double ci[4], rc[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          ci[u] = colbuf[p][4 * bi + u] * rinv;
-          rc[u] = rowbuf[p][4 * bj + u];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-          for (int w = 0; w < 4; ++w) v[u][w] -= ci[u] * rc[w];
-        if (bi == kb) {
-          const double isq = sqrt(rinv);
-#pragma unroll
-          for (int w = 0; w < 4; ++w) v[kk][w] *= isq;
-        }
-      }
-    }
-  }
-#endif
-  if (bad && tid == 0 && d == 0) *fail = 1;
-  __syncthreads();
-  // inverse -> LDS (full square, upper zero) ; block 0 also -> global
-  if (isX) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        Xs[(4 * bi + u) * LD + 4 * bj + w] = v[u][w];
-        if (bi != bj) Xs[(4 * bj + w) * LD + 4 * bi + u] = 0.0;
-      }
-  }
-  __syncthreads();
-  if (d == 0) {
-    double* dst = Linv + static_cast<int64_t>(j) * T * T;
-    for (int e = tid; e < T * T; e += kPanelThreads) dst[e] = Xs[(e / T) * LD + e % T];
-  }
-  // y_j = L_jj^-1 r_j (every block; block 0 stores it)
-  const double* rj = r + static_cast<int64_t>(j) * T;
-  if (tid < T) {
-    double s = 0.0;
-    for (int m = 0; m <= tid; ++m) s += Xs[tid * LD + m] * rj[m];
-    yv[tid] = s;
-    if (d == 0) y[static_cast<int64_t>(j) * T + tid] = s;
-  }
-  if (d == 0) return;
-  __syncthreads();
-  // L(j+d, j) = A L^-T  (Xs holds L^-1: C[r][c] = sum_m A[r][m] Linv[c][m])
-  double acc[4][4];
-  if (tid < 256) {
-    gemm_abt_4x4(As, Xs, tid, acc);
-    const int r0 = (tid >> 4) * 4, c0 = (tid & 15) * 4;
-    double* dst = b.band + b.off[j] + static_cast<int64_t>(d) * T * T;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      *reinterpret_cast<double4*>(dst + (r0 + u) * T + c0) = make_double4(acc[u][0], acc[u][1], acc[u][2], acc[u][3]);
-    }
-  }
-  __syncthreads();  // all reads of As done before reuse
-  if (tid < 256) {
-    const int r0 = (tid >> 4) * 4, c0 = (tid & 15) * 4;
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int w = 0; w < 4; ++w) As[(r0 + u) * LD + c0 + w] = acc[u][w];
-  }
-  __syncthreads();
-  // r_{j+d} -= L(j+d, j) y_j
-  if (tid < T) {
-    double s = 0.0;
-    for (int m = 0; m < T; ++m) s += As[tid * LD + m] * yv[m];
-    r[static_cast<int64_t>(j + d) * T + tid] -= s;
+    for (int b = 0; b < 2; ++b) acc[a][b] = v4d{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+  for (int k0 = 0; k0 < T; k0 += 4) {
+    const int k = k0 + lk;
+    const double a0 = As[(i0 + li) * LD + k], a1 = As[(i0 + 16 + li) * LD + k];
+    const double b0 = Bs[(j0 + li) * LD + k], b1 = Bs[(j0 + 16 + li) * LD + k];
+    acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+    acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+    acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+    acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
   }
 }
 
-// trailing update of column j: tile(j+d1, j+d2) -= L(j+d1,j) L(j+d2,j)^T
-__global__ __launch_bounds__(256) void k_update(BandDev b, int j) {
-  __shared__ double As[T * LD];
-  __shared__ double Bs[T * LD];
-  int t = blockIdx.x, d1 = 1;
-  while (t >= d1) { t -= d1; ++d1; }
-  const int d2 = t + 1;
-  const double* A = b.band + b.off[j] + static_cast<int64_t>(d1) * T * T;
-  const double* B = b.band + b.off[j] + static_cast<int64_t>(d2) * T * T;
-  double* C = b.band + b.off[j + d2] + static_cast<int64_t>(d1 - d2) * T * T;
-  const int tid = threadIdx.x;
-  load_tile_lds(A, As, tid, 256);
-  load_tile_lds(B, Bs, tid, 256);
-  __syncthreads();
-  double acc[4][4];
-  gemm_abt_4x4(As, Bs, tid, acc);
-  const int r0 = (tid >> 4) * 4, c0 = (tid & 15) * 4;
+// element (row, col) of the quadrant result held by this lane
+#define MFMA_ROW(wave, lane, ti, r) (32 * ((wave) >> 1) + 16 * (ti) + ((lane) >> 4) + 4 * (r))
+#define MFMA_COL(wave, lane, tj) (32 * ((wave) & 1) + 16 * (tj) + ((lane) & 15))
+
+__device__ __forceinline__ double pivot_ok(double x, bool& ok) {
+  if (!(x > 0.0) || !isfinite(x)) {
+    ok = false;
+    return 1.0;
+  }
+  return x;
+}
+
+// 1/sqrt(x): hardware estimate + two Newton steps (full FP64 accuracy)
+__device__ __forceinline__ double rsqrt_nr(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  y = y * (1.5 - 0.5 * x * y * y);
+  y = y * (1.5 - 0.5 * x * y * y);
+  return y;
+}
+
+// 4x4 Cholesky + inverse of a lower 4x4 (row-major a[4][4]); m receives
+// L^-1 (lower). Only the reciprocal pivots r_i = 1/l_ii are formed.
+// ok is cleared on a non-positive pivot.
+__device__ __forceinline__ void chol_inv4(const double (&a)[4][4], double (&m)[4][4], bool& ok) {
+  const double r0 = rsqrt_nr(pivot_ok(a[0][0], ok));
+  const double l10 = a[1][0] * r0, l20 = a[2][0] * r0, l30 = a[3][0] * r0;
+  const double r1 = rsqrt_nr(pivot_ok(a[1][1] - l10 * l10, ok));
+  const double l21 = (a[2][1] - l20 * l10) * r1, l31 = (a[3][1] - l30 * l10) * r1;
+  const double r2 = rsqrt_nr(pivot_ok(a[2][2] - l20 * l20 - l21 * l21, ok));
+  const double l32 = (a[3][2] - l30 * l20 - l31 * l21) * r2;
+  const double r3 = rsqrt_nr(pivot_ok(a[3][3] - l30 * l30 - l31 * l31 - l32 * l32, ok));
+  m[0][0] = r0; m[1][1] = r1; m[2][2] = r2; m[3][3] = r3;
+  m[1][0] = -r1 * (l10 * r0);
+  m[2][1] = -r2 * (l21 * r1);
+  m[3][2] = -r3 * (l32 * r2);
+  m[2][0] = -r2 * (l20 * r0 + l21 * m[1][0]);
+  m[3][1] = -r3 * (l31 * r1 + l32 * m[2][1]);
+  m[3][0] = -r3 * (l30 * r0 + l31 * m[1][0] + l32 * m[2][0]);
+  m[0][1] = m[0][2] = m[0][3] = m[1][2] = m[1][3] = m[2][3] = 0.0;
+}
+
+__device__ __forceinline__ double* tile_ptr(const BandDev& b, int i, int j) {
+  return b.band + b.off[j] + static_cast<int64_t>(i - j) * T * T;
+}
+
+// MFMA accumulator layout of a 64x64 tile over 4 waves: wave w holds the 16
+// rows 16w.. as four 16x16 tiles TJ; lane l, reg r of tile TJ is element
+// (16w + (l>>4) + 4r, 16TJ + (l&15)).
+#define ACC_ROW(w, l, r) (16 * (w) + ((l) >> 4) + 4 * (r))
+#define ACC_COL(TJ, l) (16 * (TJ) + ((l) & 15))
+
+// Factor the diagonal tile held in accumulator layout (accA) and build its
+// inverse (accX, starting from I). Right-looking, 4 pivots per step:
+//   publish column block kb of A and row block kb of the running inverse
+//   to LDS (double-buffered), one barrier; every lane forms M = L_kk^-1
+//   (4x4) redundantly, the panel entries it feeds to the MFMAs
+//   (L = A_panel M^T, zero for rows <= 4kb+3) and the finalised inverse
+//   rows Xf = M X_kb; then accA -= L L^T and accX -= L Xf (4+4
+//   v_mfma_f64_16x16x4 per wave) and X rows 4kb.. are replaced by Xf.
+__device__ bool factor_tile_mfma(v4d (&accA)[4], v4d (&accX)[4], int w, int l, double* Pcol, double* Xrow) {
+  bool ok = true;
+  const int li = l & 15, lk = l >> 4;
+  for (int KB = 0; KB < 4; ++KB) {
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    double4* pc = reinterpret_cast<double4*>(C + (r0 + u) * T + c0);
-    double4 q = *pc;
-    q.x -= acc[u][0]; q.y -= acc[u][1]; q.z -= acc[u][2]; q.w -= acc[u][3];
-    *pc = q;
+    for (int kk = 0; kk < 4; ++kk) {
+      const int kb = 4 * KB + kk, p = kk & 1;
+      double* P = Pcol + p * (T * 4);
+      double* X = Xrow + p * (4 * T);
+      // publish A[:, 4kb..4kb+3] (tile column KB, in-tile cols 4kk..4kk+3)
+      if (li >= 4 * kk && li < 4 * kk + 4) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) P[ACC_ROW(w, l, r) * 4 + (li - 4 * kk)] = accA[KB][r];
+      }
+      // publish X[4kb..4kb+3, :] (wave KB, register kk)
+      if (w == KB) {
+#pragma unroll
+        for (int TJ = 0; TJ < 4; ++TJ) X[lk * T + ACC_COL(TJ, l)] = accX[TJ][kk];
+      }
+      __syncthreads();
+      // M = L_kk^-1 of the 4x4 pivot block (every lane, redundantly)
+      double a4[4][4], M[4][4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a4[u][q] = P[(4 * kb + u) * 4 + q];
+      chol_inv4(a4, M, ok);
+      // panel entries fed to the MFMAs: L[i][k] = sum_{m<=k} A[i][m] M[k][m]
+      auto panel = [&](int i) {
+        double s = 0.0;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) s += P[i * 4 + m] * M[lk][m];
+        return i > 4 * kb + 3 ? s : 0.0;
+      };
+      const double aL = -panel(16 * w + li);
+      double bL[4], xf[4];
+#pragma unroll
+      for (int TJ = 0; TJ < 4; ++TJ) {
+        bL[TJ] = panel(16 * TJ + li);
+        double s = 0.0;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) s += M[lk][m] * X[m * T + ACC_COL(TJ, l)];
+        xf[TJ] = s;
+      }
+      // only active 16x16 tiles: rows > 4kb+3 (w >= KB); A lower (KB <= TJ <= w),
+      // inverse columns <= 4kb+3 (TJ <= KB)
+      if (w >= KB) {
+#pragma unroll
+        for (int TJ = 0; TJ < 4; ++TJ) {
+          if (TJ >= KB && TJ <= w) accA[TJ] = __builtin_amdgcn_mfma_f64_16x16x4f64(aL, bL[TJ], accA[TJ], 0, 0, 0);
+          if (TJ <= KB) accX[TJ] = __builtin_amdgcn_mfma_f64_16x16x4f64(aL, xf[TJ], accX[TJ], 0, 0, 0);
+        }
+      }
+      if (w == KB) {
+#pragma unroll
+        for (int TJ = 0; TJ < 4; ++TJ) accX[TJ][kk] = xf[TJ];
+      }
+    }
+  }
+  return ok;
+}
+
+// y = L^-1 v (64, L^-1 in LDS with stride LD, lower): 4 lanes per row
+__device__ __forceinline__ double lower_gemv4(const double* Li, const double* v, int tid) {
+  const int row = tid >> 2, part = tid & 3;
+  double s = 0.0;
+  for (int m = part; m <= row; m += 4) s += Li[row * LD + m] * v[m];
+  s += __shfl_xor(s, 1);
+  s += __shfl_xor(s, 2);
+  return s;
+}
+
+__global__ __launch_bounds__(256) void k_step(BandDev b, int j, int npanel, double* __restrict__ Linv,
+                                              double* __restrict__ r, double* __restrict__ y, int* fail) {
+  __shared__ double Ps[T * LD];   // L(j, j-1)  -> later L_jj^-1
+  __shared__ double Qs[T * LD];   // L(j+d, j-1) / update operand
+  __shared__ double As[T * LD];   // tile (j+d, j)
+  __shared__ double Pcol[2 * T * 4];
+  __shared__ double Xrow[2 * 4 * T];
+  __shared__ double vv[T];
+  const int tid = threadIdx.x;
+  const int w = tid >> 6, l = tid & 63;
+  const int Dprev = j > 0 ? b.D[j - 1] : 0;
+  if (static_cast<int>(blockIdx.x) >= npanel) {
+    // ---- update block: tile (j-1+d1, j-1+d2) -= L(j-1+d1, j-1) L(j-1+d2, j-1)^T, d2 >= 2
+    int t = blockIdx.x - npanel, d1 = 2;
+    while (t >= d1 - 1) { t -= d1 - 1; ++d1; }
+    const int d2 = t + 2;
+    load_tile_lds(tile_ptr(b, j - 1 + d1, j - 1), Qs, tid, 256);
+    load_tile_lds(tile_ptr(b, j - 1 + d2, j - 1), Ps, tid, 256);
+    __syncthreads();
+    v4d acc[2][2];
+    mfma_abt(Qs, Ps, w, l, acc);
+    double* dst = tile_ptr(b, j - 1 + d1, j - 1 + d2);
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) dst[MFMA_ROW(w, l, ti, rr) * T + MFMA_COL(w, l, tj)] -= acc[ti][tj][rr];
+    return;
+  }
+  // ---- panel block d
+  const int d = blockIdx.x;
+  const bool has_prev = Dprev >= 1;             // tile (j, j-1) exists
+  const bool prev_d = d > 0 && Dprev >= d + 1;  // tile (j+d, j-1) exists
+  if (has_prev) load_tile_lds(tile_ptr(b, j, j - 1), Ps, tid, 256);
+  if (d > 0) load_tile_lds(tile_ptr(b, j + d, j), As, tid, 256);
+  if (prev_d) load_tile_lds(tile_ptr(b, j + d, j - 1), Qs, tid, 256);
+  v4d accA[4], accX[4];
+  const double* diag = tile_ptr(b, j, j);
+#pragma unroll
+  for (int TJ = 0; TJ < 4; ++TJ)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int row = ACC_ROW(w, l, rr), col = ACC_COL(TJ, l);
+      accA[TJ][rr] = diag[row * T + col];
+      accX[TJ][rr] = row == col ? 1.0 : 0.0;
+    }
+  __syncthreads();
+  const int li = l & 15, lk = l >> 4;
+  if (has_prev) {
+    // A_jj -= L(j,j-1) L(j,j-1)^T into the accumulators (K = 64)
+#pragma unroll 4
+    for (int k0 = 0; k0 < T; k0 += 4) {
+      const double a = -Ps[(16 * w + li) * LD + k0 + lk];
+#pragma unroll
+      for (int TJ = 0; TJ < 4; ++TJ)
+        accA[TJ] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Ps[(16 * TJ + li) * LD + k0 + lk], accA[TJ], 0, 0, 0);
+    }
+  }
+  if (prev_d) {
+    // A_dj -= L(j+d,j-1) L(j,j-1)^T
+    v4d acc[2][2];
+    mfma_abt(Qs, Ps, w, l, acc);
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) As[MFMA_ROW(w, l, ti, rr) * LD + MFMA_COL(w, l, tj)] -= acc[ti][tj][rr];
+  }
+  __syncthreads();
+  const bool ok = factor_tile_mfma(accA, accX, w, l, Pcol, Xrow);
+  if (!ok && d == 0 && tid == 0) *fail = 1;
+  // L_jj^-1 -> Ps (full square; upper part is exactly zero)
+#pragma unroll
+  for (int TJ = 0; TJ < 4; ++TJ)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) Ps[ACC_ROW(w, l, rr) * LD + ACC_COL(TJ, l)] = accX[TJ][rr];
+  if (d == 0) {
+    double* dst = Linv + static_cast<int64_t>(j) * T * T;
+#pragma unroll
+    for (int TJ = 0; TJ < 4; ++TJ)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) dst[ACC_ROW(w, l, rr) * T + ACC_COL(TJ, l)] = accX[TJ][rr];
+  }
+  const double* rj = r + static_cast<int64_t>(j) * T;
+  if (tid < T) vv[tid] = rj[tid];
+  __syncthreads();
+  // y_j = L_jj^-1 r_j
+  const double yrow = lower_gemv4(Ps, vv, tid);
+  __syncthreads();
+  if ((tid & 3) == 0) {
+    vv[tid >> 2] = yrow;
+    if (d == 0) y[static_cast<int64_t>(j) * T + (tid >> 2)] = yrow;
+  }
+  if (d == 0) return;
+  // L(j+d, j) = A L^-T
+  v4d acc[2][2];
+  mfma_abt(As, Ps, w, l, acc);
+  __syncthreads();
+  double* dst = tile_ptr(b, j + d, j);
+#pragma unroll
+  for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int row = MFMA_ROW(w, l, ti, rr), col = MFMA_COL(w, l, tj);
+        dst[row * T + col] = acc[ti][tj][rr];
+        As[row * LD + col] = acc[ti][tj][rr];
+      }
+  __syncthreads();
+  // r_{j+d} -= L(j+d, j) y_j (4 lanes per row)
+  {
+    const int row = tid >> 2, part = tid & 3;
+    double s = 0.0;
+    for (int m = part; m < T; m += 4) s += As[row * LD + m] * vv[m];
+    s += __shfl_xor(s, 1);
+    s += __shfl_xor(s, 2);
+    if (part == 0) r[static_cast<int64_t>(j + d) * T + row] -= s;
   }
 }
 
@@ -256,10 +324,10 @@ __global__ __launch_bounds__(256) void k_update(BandDev b, int j) {
 constexpr int kBackThreads = 1024;
 __global__ __launch_bounds__(kBackThreads) void k_band_back(BandDev b, const double* __restrict__ Linv,
                                                             const double* __restrict__ y, double* __restrict__ x) {
-  __shared__ double part[kBackThreads / T][T];
+  constexpr int NP = kBackThreads / T;  // 16 parts
+  __shared__ double part[NP][T];
   __shared__ double rv[T];
-  const int tid = threadIdx.x, c = tid & (T - 1), q = tid >> 6;  // 16 parts
-  constexpr int NP = kBackThreads / T;
+  const int tid = threadIdx.x, c = tid & (T - 1), q = tid >> 6;
   for (int i = b.NT - 1; i >= 0; --i) {
     const int D = b.D[i];
     // sum_d sum_m L(i+d, i)[m][c] x_{i+d}[m]; the D*64 (d, m) rows are split
@@ -310,12 +378,12 @@ __global__ __launch_bounds__(kBackThreads) void k_band_back(BandDev b, const dou
 void launch_band_cholesky_solve(const BandDev& b, const int32_t* host_D, double* Linv, double* r, double* y,
                                 double* x, int* fail, hipStream_t s) {
   for (int j = 0; j < b.NT; ++j) {
-    const int D = host_D[j];
-    k_panel<<<D + 1, kPanelThreads, 0, s>>>(b, j, Linv, r, y, fail);
-#ifndef DH_NO_UPDATE
-    if (D > 0) k_update<<<D * (D + 1) / 2, 256, 0, s>>>(b, j);
-#endif
+    const int npanel = host_D[j] + 1;
+    const int Dp = j > 0 ? host_D[j - 1] : 0;
+    const int nupd = Dp >= 2 ? (Dp - 1) * Dp / 2 : 0;
+    k_step<<<npanel + nupd, 256, 0, s>>>(b, j, npanel, Linv, r, y, fail);
   }
+  // column NT-1 has no sub-diagonal tiles, so no trailing update is left over
   if (b.NT > 0) k_band_back<<<1, kBackThreads, 0, s>>>(b, Linv, y, x);
 }
 
