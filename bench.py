@@ -150,10 +150,13 @@ def main():
     if dominant == "cholesky":
         per = st["ms_cholesky"] / nsolve
         achieved = st["chol_flops"] / (per * 1e-3) / 1e12
-        roof = {"kernel": "band_cholesky (k_potrf_trsm + k_update per column tile)", "bound": "mfma",
+        roof = {"kernel": f"tile_cholesky (one factorisation + solve = {st['chol_levels']} k_tasks levels + "
+                          f"{st['back_levels']} k_back levels; nested-dissection leaf {st['nd_leaf']} tiles)",
+                "bound": "mfma",
                 "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
-                "algorithmic": f"{st['chol_flops']:.3e} envelope-Cholesky flops per factorisation",
+                "algorithmic": f"{st['chol_flops']:.3e} envelope-Cholesky flops per factorisation "
+                               f"(tile schedule issues {st['chol_tile_flops']:.3e} incl. fill)",
                 "ms_per_launch": per}
     elif dominant == "linearize":
         per = st["ms_linearize"] / nlin

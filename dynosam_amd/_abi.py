@@ -94,8 +94,11 @@ class Stats(C.Structure):
         ("n_chain", C.c_int64),
         ("n_edge", C.c_int64),
         ("reduced_dim", C.c_int64),
-        ("band_tiles", C.c_int64),
+        ("tiles_stored", C.c_int64),
         ("band_max_tiles", C.c_int64),
+        ("chol_levels", C.c_int64),
+        ("back_levels", C.c_int64),
+        ("nd_leaf", C.c_int64),
         ("lin_bytes", C.c_double),
         ("assembly_bytes", C.c_double),
         ("chol_flops", C.c_double),
@@ -159,3 +162,8 @@ def trace_to_dicts(entries):
             )
         )
     return out
+
+
+class ScheduleInfo(C.Structure):
+    _fields_ = [(n, C.c_int64) for n in ("n_pose", "n_tiles", "n_slots", "n_ftask", "n_pairs", "n_flevel", "n_btask",
+                                          "n_blevel", "n_bent", "n_red_blocks", "nd_leaf")]

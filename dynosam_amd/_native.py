@@ -96,6 +96,12 @@ def _declare(name, lib):
         lib.dynohip_sliding_window_init.restype = None
         lib.dynohip_sliding_window_check.argtypes = [P(_abi.SlidingWindowState), C.c_uint64, P(C.c_uint64), P(C.c_uint64)]
         lib.dynohip_sliding_window_check.restype = C.c_int
+        lib.dynohip_set_tile_ordering.argtypes = [C.c_int]
+        lib.dynohip_set_tile_ordering.restype = None
+        I32 = P(C.c_int32)
+        lib.dynohip_plan_schedule.argtypes = [P(_abi.GraphView), P(C.c_uint64), P(C.c_uint8), C.c_size_t,
+                                              P(_abi.ScheduleInfo)] + [I32] * 12
+        lib.dynohip_plan_schedule.restype = C.c_int
         lib.dynohip_full_batch_trigger.argtypes = [C.c_int64, C.c_uint64]
         lib.dynohip_full_batch_trigger.restype = C.c_int
         for fn, args, res in [

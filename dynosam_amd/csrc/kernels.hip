@@ -479,16 +479,27 @@ __device__ __forceinline__ void wave_gather(const int64_t* __restrict__ start, c
   }
 }
 
-__device__ __forceinline__ int64_t band_index(const BandDev& b, int row, int col) {
-  const int i = row / kTile, j = col / kTile;
-  return b.off[j] + static_cast<int64_t>(i - j) * kTile * kTile + (row % kTile) * kTile + (col % kTile);
+// element (row, col), row >= col, of the reduced matrix -> its stored tile
+// element (the tile is transposed when col's tile is eliminated later)
+__device__ __forceinline__ int64_t tile_index(const TileDev& b, int row, int col) {
+  int i = row / kTile, j = col / kTile, ri = row % kTile, cj = col % kTile;
+  if (b.pos[i] < b.pos[j]) {
+    const int t = i; i = j; j = t;
+    const int u = ri; ri = cj; cj = u;
+  }
+  int lo = b.row_start[i], hi = b.row_start[i + 1] - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (b.row_col[mid] < j) lo = mid + 1; else hi = mid;
+  }
+  return static_cast<int64_t>(b.row_slot[lo]) * kTile * kTile + ri * kTile + cj;
 }
 
 __global__ __launch_bounds__(kBlock) void k_gather_band(const int64_t* __restrict__ start,
                                                         const GEntry* __restrict__ ent, int nt,
                                                         const double* __restrict__ arena,
                                                         const int32_t* __restrict__ tA,
-                                                        const int32_t* __restrict__ tB, BandDev b, double lambda) {
+                                                        const int32_t* __restrict__ tB, TileDev b, double lambda) {
   const int t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (t >= nt) return;
   double acc[36];
@@ -503,7 +514,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_band(const int64_t* __restric
   const int r = lane / 6, c = lane % 6;
   if (A == B && r < c) return;
   if (A == B && r == c) v += lambda;
-  b.band[band_index(b, 6 * A + r, 6 * B + c)] = v;
+  b.slots[tile_index(b, 6 * A + r, 6 * B + c)] = v;
 }
 
 __global__ __launch_bounds__(kBlock) void k_gather_grad(const int64_t* __restrict__ start,
@@ -723,10 +734,10 @@ __global__ __launch_bounds__(kBlock) void k_backsub(ChainDev cd, const double* _
 }
 
 // ---------------------------------------------------------------- band
-__global__ void k_band_pad(BandDev b) {
+__global__ void k_tile_pad(TileDev b) {
   const int row = b.n_red + blockIdx.x * blockDim.x + threadIdx.x;
   if (row >= b.NT * kTile) return;
-  b.band[band_index(b, row, row)] = 1.0;
+  b.slots[tile_index(b, row, row)] = 1.0;
 }
 
 // ---------------------------------------------------------------- retract
@@ -797,7 +808,7 @@ void launch_gather_3x6(const GatherDev& g, const double* arena, double* dst, hip
   k_gather_thread<3, 6><<<nblocks(g.n), kBlock, 0, s>>>(g.start, g.ent, g.n, arena, dst);
 }
 void launch_gather_band(const GatherDev& g, const double* arena, const int32_t* tA, const int32_t* tB,
-                        const BandDev& b, double lambda, hipStream_t s) {
+                        const TileDev& b, double lambda, hipStream_t s) {
   if (g.n == 0) return;
   k_gather_band<<<nblocks(static_cast<int64_t>(g.n) * 64), kBlock, 0, s>>>(g.start, g.ent, g.n, arena, tA, tB, b,
                                                                             lambda);
@@ -820,10 +831,10 @@ void launch_backsub(const ChainDev& c, const double* arena, const double* dpose,
   k_backsub<<<nblocks(c.n_comp), kBlock, 0, s>>>(c, arena, dpose, dpt);
 }
 
-void launch_band_pad(const BandDev& b, hipStream_t s) {
+void launch_tile_pad(const TileDev& b, hipStream_t s) {
   const int npad = b.NT * kTile - b.n_red;
   if (npad <= 0) return;
-  k_band_pad<<<1, kTile, 0, s>>>(b);
+  k_tile_pad<<<1, kTile, 0, s>>>(b);
 }
 
 void launch_retract(int n_pose, int n_pt, const double* pose, const double* pt, const double* dpose,

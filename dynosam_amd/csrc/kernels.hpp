@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <vector>
 
 #include "plan.hpp"
 
@@ -40,13 +41,23 @@ struct ChainDev {
   uint64_t off_D = 0, off_E = 0, off_gp = 0, off_W = 0, off_v = 0, off_L = 0, off_M = 0;
 };
 
-struct BandDev {
+// reduced system in 64x64 tiles; tile (row tile i, column tile j) with
+// pos[i] >= pos[j] lives at slots + slot * 4096 (row-major)
+struct TileDev {
   int NT = 0;
   int n_red = 0;
-  double* band = nullptr;
-  const int64_t* off = nullptr;
-  const int32_t* D = nullptr;
-  const int32_t* cmin = nullptr;
+  double* slots = nullptr;
+  const int32_t* pos = nullptr;
+  const int32_t* row_start = nullptr;
+  const int32_t* row_col = nullptr;
+  const int32_t* row_slot = nullptr;
+};
+
+struct TileSchedDev {
+  const TileTask* ftask = nullptr;
+  const int32_t* pairs = nullptr;
+  const BackTask* btask = nullptr;
+  const int32_t* bent = nullptr;
 };
 
 // ---- launchers (all asynchronous on `s`) ----
@@ -65,19 +76,21 @@ void launch_gather_3x1(const GatherDev& g, const double* arena, double* dst, hip
 void launch_gather_3x6(const GatherDev& g, const double* arena, double* dst, hipStream_t s);
 // reduced system (wave per target)
 void launch_gather_band(const GatherDev& g, const double* arena, const int32_t* tA, const int32_t* tB,
-                        const BandDev& b, double lambda, hipStream_t s);
+                        const TileDev& b, double lambda, hipStream_t s);
 void launch_gather_grad(const GatherDev& g, const double* arena, double* gred, hipStream_t s);
 
 void launch_chain_factor(const ChainDev& c, double* arena, double lambda, int* fail, hipStream_t s);
 void launch_chain_solve_y(const ChainDev& c, double* arena, hipStream_t s);
 void launch_backsub(const ChainDev& c, const double* arena, const double* dpose, double* dpt, hipStream_t s);
 
-void launch_band_pad(const BandDev& b, hipStream_t s);
-// factor the band and solve (L L^T) x = r; r is overwritten (forward
-// substitution is fused into the factorisation), Linv holds NT diagonal
-// inverse tiles, y the forward result
-void launch_band_cholesky_solve(const BandDev& b, const int32_t* host_D, double* Linv, double* r, double* y,
-                                double* x, int* fail, hipStream_t s);
+void launch_tile_pad(const TileDev& b, hipStream_t s);
+// factor the tiles and solve (L L^T) x = r (forward substitution fused
+// into the factorisation: contrib holds L(i,k) y_k per stored tile). Linv
+// receives the NT diagonal inverse tiles, y the forward result. One launch
+// per level of the host schedule (flevel / blevel).
+void launch_tile_cholesky_solve(const TileDev& b, const TileSchedDev& sd, const std::vector<int32_t>& flevel,
+                                const std::vector<int32_t>& blevel, double* Linv, const double* r,
+                                double* contrib, double* y, double* x, int* fail, hipStream_t s);
 
 void launch_retract(int n_pose, int n_pt, const double* pose, const double* pt, const double* dpose,
                     const double* dpt, double* pose_out, double* pt_out, hipStream_t s);

@@ -395,24 +395,12 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
   }
   for (int j = 1; j < P.NT; ++j) rlow[j] = std::max(rlow[j], rlow[j - 1]);
   P.band_D.resize(P.NT);
-  P.band_off.resize(P.NT);
-  int64_t off = 0;
   P.max_D = 0;
   for (int j = 0; j < P.NT; ++j) {
     P.band_D[j] = rlow[j] - j;
     P.max_D = std::max(P.max_D, P.band_D[j]);
-    P.band_off[j] = off;
-    off += static_cast<int64_t>(P.band_D[j] + 1) * kTile * kTile;
   }
-  P.band_size = off;
-  P.band_cmin.resize(P.NT);
-  {
-    int c = 0;
-    for (int i = 0; i < P.NT; ++i) {
-      while (rlow[c] < i) ++c;
-      P.band_cmin[i] = c;
-    }
-  }
+  build_tile_schedule(P);
   return DYNOHIP_OK;
 }
 

@@ -17,8 +17,9 @@
 //   Y        (3x6)   C^-1 W per (component, point, neighbour pose)
 //   v[n_pt]  (3)     C^-1 gp
 //   L, M[n_pt](3x3)  block-Cholesky factors of each point chain
-// Reduced (Schur) pose system: lower block-band in 64x64 column tiles,
-// poses in frame order (X_k, then H/L_{j,k}).
+// Reduced (Schur) pose system: 64x64 tiles (tile t = reduced rows
+// 64t..64t+63, poses in frame order: X_k, then H/L_{j,k}), stored sparsely
+// by slot (see tiles.cpp) and factored by a level-scheduled tile DAG.
 #pragma once
 
 #include <cstdint>
@@ -47,6 +48,28 @@ struct GEntry {
   uint32_t b;
   int32_t k;
   int32_t sign;
+};
+
+// one workgroup task of the tile Cholesky (see tiles.cpp / tilechol.hip).
+// Operand pairs (A, B) index Plan::pairs; a pair stands for A B^T.
+struct TileTask {
+  int32_t kind;    // 0 = panel, 1 = update
+  int32_t k;       // panel: column tile
+  int32_t i;       // panel: row tile (== k for the diagonal task)
+  int32_t dst;     // slot written: L(i,k) (panel) / updated tile (update)
+  int32_t diag;    // panel: slot of A(k,k)
+  int32_t pd_beg;  // panel: pending updates of A(k,k), pairs [pd_beg, pd_end)
+  int32_t pd_end;
+  int32_t po_beg;  // panel: pending updates of A(i,k) / update: its pairs
+  int32_t po_end;
+  int32_t pad;
+};
+
+// backward-substitution task: x_k = L_kk^-T (y_k - sum L(i,k)^T x_i)
+struct BackTask {
+  int32_t k;
+  int32_t beg, end;  // entries [beg, end) of the (slot, row tile) list
+  int32_t pad;
 };
 
 struct GatherList {
@@ -93,15 +116,30 @@ struct Plan {
   // arena
   uint64_t off_D = 0, off_E = 0, off_gp = 0, off_W = 0, off_Y = 0, off_v = 0, off_L = 0, off_M = 0;
   uint64_t arena_size = 0;
-  // reduced band
+  // reduced system
   int n_red = 0;                        // 6 * n_pose
-  int NT = 0;                           // column tiles
-  std::vector<int32_t> band_D;          // per column tile: #sub-diagonal tiles
-  std::vector<int64_t> band_off;        // per column tile: offset (doubles)
-  std::vector<int32_t> band_cmin;       // per row tile: first column tile present
-  int64_t band_size = 0;
+  int NT = 0;                           // tiles
+  std::vector<int32_t> band_D;          // natural-order skyline: sub-diagonal tiles per column tile
   int max_D = 0;
+  // tile Cholesky (tiles.cpp)
+  int nd_leaf = 0;                      // chosen nested-dissection leaf size (0 = natural order)
+  std::vector<int32_t> tile_pos;        // elimination position of tile t
+  int32_t n_slots = 0;                  // stored tiles (lower factor incl. fill)
+  std::vector<int32_t> row_start;       // per tile t: stored tiles whose row tile is t
+  std::vector<int32_t> row_col;         //   their column tiles (sorted)
+  std::vector<int32_t> row_slot;        //   and slots
+  std::vector<TileTask> ftask;          // forward tasks, grouped by level
+  std::vector<int32_t> pairs;           // operand pairs (A slot, B slot) of the tasks
+  std::vector<int32_t> flevel;          // level l = tasks [flevel[l], flevel[l+1])
+  std::vector<BackTask> btask;
+  std::vector<int32_t> blevel;
+  std::vector<int32_t> bent;            // pairs (slot, row tile)
+  double tile_flops = 0.0;              // tile-level factorisation flops (incl. fill)
 };
+
+// Orders the tiles (nested dissection over frame order), computes the
+// tile-level fill and the task DAG with its level schedule.
+void build_tile_schedule(Plan& P);
 
 // returns DYNOHIP_OK or an error code with `err` filled
 int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t* kind, size_t n, Plan& plan,

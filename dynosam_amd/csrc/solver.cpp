@@ -106,14 +106,16 @@ struct dynohip_solver {
   DevBuf<int32_t> comp_start, comp_nb_start, nb_comp, nbedge_start, nbedge_pt, pt_edge_start, edge_pose;
   DevBuf<int64_t> comp_y_base;
   DevBuf<uint32_t> nbedge_w;
-  DevBuf<double> band, gred, xy, dpt, linv;
-  DevBuf<int64_t> band_off;
-  DevBuf<int32_t> band_D, band_cmin;
+  DevBuf<double> slots, gred, xy, dpt, linv, contrib;
+  DevBuf<int32_t> tile_pos, row_start, row_col, row_slot, bent, pairs;
+  DevBuf<TileTask> ftask;
+  DevBuf<BackTask> btask;
   DevBuf<double> partials, result;
   DevBuf<int> fail;
   int partial_slots = 0;
   ChainDev cd;
-  BandDev bd;
+  TileDev bd;
+  TileSchedDev sd;
   // LM state
   dynohip_lm_params prm{};
   double lambda = 1e-5, error = 0.0;
@@ -196,10 +198,16 @@ int upload_plan(dynohip_solver* s) {
   HIPCHK(s, s->nbedge_w.upload(P.nbedge_w, st));
   HIPCHK(s, s->pt_edge_start.upload(P.pt_edge_start, st));
   HIPCHK(s, s->edge_pose.upload(P.edge_pose, st));
-  HIPCHK(s, s->band.alloc(P.band_size));
-  HIPCHK(s, s->band_off.upload(P.band_off, st));
-  HIPCHK(s, s->band_D.upload(P.band_D, st));
-  HIPCHK(s, s->band_cmin.upload(P.band_cmin, st));
+  HIPCHK(s, s->slots.alloc(static_cast<size_t>(P.n_slots) * kTile * kTile));
+  HIPCHK(s, s->tile_pos.upload(P.tile_pos, st));
+  HIPCHK(s, s->row_start.upload(P.row_start, st));
+  HIPCHK(s, s->row_col.upload(P.row_col, st));
+  HIPCHK(s, s->row_slot.upload(P.row_slot, st));
+  HIPCHK(s, s->bent.upload(P.bent, st));
+  HIPCHK(s, s->ftask.upload(P.ftask, st));
+  HIPCHK(s, s->pairs.upload(P.pairs, st));
+  HIPCHK(s, s->contrib.alloc(static_cast<size_t>(P.n_slots) * kTile));
+  HIPCHK(s, s->btask.upload(P.btask, st));
   const size_t nrp = static_cast<size_t>(P.NT) * kTile;
   HIPCHK(s, s->gred.alloc(nrp > 0 ? nrp : 1));
   HIPCHK(s, s->xy.alloc(2 * (nrp > 0 ? nrp : 1)));
@@ -224,13 +232,18 @@ int upload_plan(dynohip_solver* s) {
   c.off_v = P.off_v;
   c.off_L = P.off_L;
   c.off_M = P.off_M;
-  BandDev& b = s->bd;
+  TileDev& b = s->bd;
   b.NT = P.NT;
   b.n_red = P.n_red;
-  b.band = s->band.p;
-  b.off = s->band_off.p;
-  b.D = s->band_D.p;
-  b.cmin = s->band_cmin.p;
+  b.slots = s->slots.p;
+  b.pos = s->tile_pos.p;
+  b.row_start = s->row_start.p;
+  b.row_col = s->row_col.p;
+  b.row_slot = s->row_slot.p;
+  s->sd.ftask = s->ftask.p;
+  s->sd.pairs = s->pairs.p;
+  s->sd.btask = s->btask.p;
+  s->sd.bent = s->bent.p;
   HIPCHK(s, hipStreamSynchronize(st));
   return 0;
 }
@@ -282,18 +295,19 @@ void enqueue_try(dynohip_solver* s, double lambda) {
   const size_t nrp = static_cast<size_t>(P.NT) * kTile;
   if (timed) (void)hipEventRecord(s->ev[2], st);
   (void)hipMemsetAsync(s->fail.p, 0, sizeof(int), st);
-  (void)hipMemsetAsync(s->band.p, 0, P.band_size * sizeof(double), st);
+  (void)hipMemsetAsync(s->slots.p, 0, static_cast<size_t>(P.n_slots) * kTile * kTile * sizeof(double), st);
   (void)hipMemsetAsync(s->gred.p, 0, nrp * sizeof(double), st);
   launch_chain_factor(s->cd, A, lambda, s->fail.p, st);
   launch_chain_solve_y(s->cd, A, st);
   if (timed) (void)hipEventRecord(s->ev[3], st);
   launch_gather_band(s->gRed.dev(P.gRed.ntargets()), A, s->redA.p, s->redB.p, s->bd, lambda, st);
-  launch_band_pad(s->bd, st);
+  launch_tile_pad(s->bd, st);
   launch_gather_grad(s->gGred.dev(P.gGred.ntargets()), A, s->gred.p, st);
   if (timed) (void)hipEventRecord(s->ev[4], st);
   double* y = s->xy.p;
   double* x = s->xy.p + nrp;
-  launch_band_cholesky_solve(s->bd, P.band_D.data(), s->linv.p, s->gred.p, y, x, s->fail.p, st);
+  launch_tile_cholesky_solve(s->bd, s->sd, P.flevel, P.blevel, s->linv.p, s->gred.p, s->contrib.p, y, x,
+                             s->fail.p, st);
   if (timed) (void)hipEventRecord(s->ev[5], st);
   if (timed) (void)hipEventRecord(s->ev[6], st);
   // pose deltas are x[0 .. 6 n_pose) in pose-index order
@@ -317,10 +331,11 @@ void compute_base_stats(dynohip_solver* s) {
   st.n_chain = P.n_comp;
   st.n_edge = P.n_edge;
   st.reduced_dim = P.n_red;
-  int64_t tiles = 0;
-  for (int j = 0; j < P.NT; ++j) tiles += P.band_D[j] + 1;
-  st.band_tiles = tiles;
+  st.tiles_stored = P.n_slots;
   st.band_max_tiles = P.max_D;
+  st.chol_levels = P.flevel.empty() ? 0 : static_cast<int64_t>(P.flevel.size()) - 1;
+  st.back_levels = P.blevel.empty() ? 0 : static_cast<int64_t>(P.blevel.size()) - 1;
+  st.nd_leaf = P.nd_leaf;
   double lin = 0.0;
   for (int t = 0; t < kNTypes; ++t) {
     const TypePlan& tp = P.types[t];
@@ -353,13 +368,7 @@ void compute_base_stats(dynohip_solver* s) {
     }
   }
   st.chol_flops = fl;
-  const double T3 = static_cast<double>(kTile) * kTile * kTile;
-  double tf = 0.0;
-  for (int j = 0; j < P.NT; ++j) {
-    const double D = P.band_D[j];
-    tf += T3 / 3.0 + D * T3 + D * (D + 1) / 2.0 * 2.0 * T3;
-  }
-  st.chol_tile_flops = tf;
+  st.chol_tile_flops = P.tile_flops;
 }
 
 // LevenbergMarquardtOptimizer::iterate()

@@ -1,26 +1,23 @@
-// band.hip — block-banded Cholesky of the reduced (Schur) pose system and
-// its triangular solves: 64x64 FP64 tiles, lower band stored by column tile
-// (tile (j+d, j) at off[j] + d*4096, row-major), D_j sub-diagonal tiles.
+// tilechol.hip — Cholesky of the reduced (Schur) pose system as a DAG of
+// 64x64 FP64 tile tasks (schedule built on the host, tiles.cpp), with the
+// forward substitution fused in and a level-scheduled backward substitution.
 //
-// One launch per column tile j, k_step(j), with two kinds of workgroups:
-//   panel blocks d = 0..D_j   apply column j-1's contribution to their own
-//       tile (j+d, j) and to the diagonal tile (j, j) (right-looking update,
-//       so no other launch is needed for column j), factor the diagonal
-//       tile in registers (4x4-blocked: one thread factors and inverts each
-//       4x4 diagonal sub-block, two barriers per 4 pivots) together with
-//       L_jj^-1, and then
-//         d == 0: store L_jj^-1 and y_j = L_jj^-1 r_j (forward substitution
-//                 fused into the factorisation),
-//         d >= 1: L(j+d, j) = A L_jj^-T (FP64 MFMA GEMM with the explicit
-//                 inverse), r_{j+d} -= L(j+d, j) y_j;
-//   update blocks             the rest of column j-1's trailing update:
-//       tile (j-1+d1, j-1+d2) -= L(j-1+d1, j-1) L(j-1+d2, j-1)^T, d2 >= 2.
-// Every tile receives each column's contribution exactly once and no
-// workgroup writes what another workgroup of the same launch reads, so the
-// result is deterministic. k_band_back then runs
-// x_j = L_jj^-T (y_j - sum_d L(j+d,j)^T x_{j+d}) in one workgroup.
-// A non-positive pivot sets *fail (the LM treats the step as failed:
-// GTSAM's IndeterminantLinearSystemException path).
+// k_tasks runs one level of the schedule: every workgroup executes one task.
+//   panel(k, i)   applies the last outstanding update of A(k,k) (L(k,c)
+//       L(k,c)^T, into the accumulators) and of its own tile A(i,k). It then
+//       factors the diagonal tile in registers (4x4-blocked right-looking
+//       Cholesky on v_mfma_f64_16x16x4f64, one barrier per 4 pivots)
+//       together with L_kk^-1, and computes y_k = L_kk^-1 r_k. Then
+//         i == k: store L_kk^-1 and y_k;
+//         i != k: L(i,k) = A(i,k) L_kk^-T (MFMA GEMM with the explicit
+//                 inverse), r_i -= L(i,k) y_k.
+//   update        A(i,j) -= L(i,c) L(j,c)^T (MFMA GEMM).
+// The host schedule guarantees that no workgroup of a level writes what
+// another workgroup of the same level reads or writes. Every tile receives
+// its updates in a fixed order, so results are deterministic. k_back runs
+// one level of x_k = L_kk^-T (y_k - sum_i L(i,k)^T x_i).
+// A non-positive pivot sets *fail. The LM then treats the step as failed,
+// like GTSAM's IndeterminantLinearSystemException path.
 #include <hip/hip_runtime.h>
 
 #include "kernels.hpp"
@@ -47,13 +44,17 @@ __device__ __forceinline__ void load_tile_lds(const double* __restrict__ src, do
 // 64x64x64 C = A B^T on LDS operands with v_mfma_f64_16x16x4f64; waves 0..3
 // each own a 32x32 quadrant (2x2 MFMA tiles). Lane l feeds A[i0+(l&15)][k0+(l>>4)]
 // and B[j0+(l&15)][k0+(l>>4)]; result acc[ti][tj][r] = C[i0+16ti+(l>>4)+4r][j0+16tj+(l&15)].
-__device__ __forceinline__ void mfma_abt(const double* As, const double* Bs, int wave, int lane, v4d acc[2][2]) {
-  const int i0 = 32 * (wave >> 1), j0 = 32 * (wave & 1);
-  const int li = lane & 15, lk = lane >> 4;
+__device__ __forceinline__ void zero_acc(v4d acc[2][2]) {
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = v4d{0.0, 0.0, 0.0, 0.0};
+}
+
+// acc += A B^T
+__device__ __forceinline__ void mfma_abt_acc(const double* As, const double* Bs, int wave, int lane, v4d acc[2][2]) {
+  const int i0 = 32 * (wave >> 1), j0 = 32 * (wave & 1);
+  const int li = lane & 15, lk = lane >> 4;
 #pragma unroll 4
   for (int k0 = 0; k0 < T; k0 += 4) {
     const int k = k0 + lk;
@@ -64,6 +65,11 @@ __device__ __forceinline__ void mfma_abt(const double* As, const double* Bs, int
     acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
     acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
   }
+}
+
+__device__ __forceinline__ void mfma_abt(const double* As, const double* Bs, int wave, int lane, v4d acc[2][2]) {
+  zero_acc(acc);
+  mfma_abt_acc(As, Bs, wave, lane, acc);
 }
 
 // element (row, col) of the quadrant result held by this lane
@@ -107,8 +113,8 @@ __device__ __forceinline__ void chol_inv4(const double (&a)[4][4], double (&m)[4
   m[0][1] = m[0][2] = m[0][3] = m[1][2] = m[1][3] = m[2][3] = 0.0;
 }
 
-__device__ __forceinline__ double* tile_ptr(const BandDev& b, int i, int j) {
-  return b.band + b.off[j] + static_cast<int64_t>(i - j) * T * T;
+__device__ __forceinline__ double* slot_ptr(const TileDev& b, int32_t slot) {
+  return b.slots + static_cast<int64_t>(slot) * T * T;
 }
 
 // MFMA accumulator layout of a 64x64 tile over 4 waves: wave w holds the 16
@@ -197,28 +203,40 @@ __device__ __forceinline__ double lower_gemv4(const double* Li, const double* v,
   return s;
 }
 
-__global__ __launch_bounds__(256) void k_step(BandDev b, int j, int npanel, double* __restrict__ Linv,
-                                              double* __restrict__ r, double* __restrict__ y, int* fail) {
-  __shared__ double Ps[T * LD];   // L(j, j-1)  -> later L_jj^-1
-  __shared__ double Qs[T * LD];   // L(j+d, j-1) / update operand
-  __shared__ double As[T * LD];   // tile (j+d, j)
+// sum over operand pairs [beg, end) of A B^T into acc (operands staged in
+// Qs / Rs; a pair with A == B is loaded once)
+__device__ __forceinline__ void sum_pairs(const TileDev& b, const int32_t* __restrict__ pairs, int beg, int end,
+                                          double* Qs, double* Rs, int tid, int w, int l, v4d acc[2][2]) {
+  zero_acc(acc);
+  for (int e = beg; e < end; ++e) {
+    const int32_t pa = pairs[2 * e], pb = pairs[2 * e + 1];
+    __syncthreads();
+    load_tile_lds(slot_ptr(b, pa), Qs, tid, 256);
+    if (pb != pa) load_tile_lds(slot_ptr(b, pb), Rs, tid, 256);
+    __syncthreads();
+    mfma_abt_acc(Qs, pb != pa ? Rs : Qs, w, l, acc);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_tasks(TileDev b, const TileTask* __restrict__ tasks,
+                                               const int32_t* __restrict__ pairs, double* __restrict__ Linv,
+                                               const double* __restrict__ r, double* __restrict__ contrib,
+                                               double* __restrict__ y, int* fail) {
+  __shared__ double Ps[T * LD];   // pending diagonal operand L(k, c) -> later L_kk^-1
+  __shared__ double Qs[T * LD];   // pair operand A
+  __shared__ double Rs[T * LD];   // pair operand B
+  __shared__ double As[T * LD];   // own tile (i, k)
   __shared__ double Pcol[2 * T * 4];
   __shared__ double Xrow[2 * 4 * T];
   __shared__ double vv[T];
+  const TileTask tk = tasks[blockIdx.x];
   const int tid = threadIdx.x;
   const int w = tid >> 6, l = tid & 63;
-  const int Dprev = j > 0 ? b.D[j - 1] : 0;
-  if (static_cast<int>(blockIdx.x) >= npanel) {
-    // ---- update block: tile (j-1+d1, j-1+d2) -= L(j-1+d1, j-1) L(j-1+d2, j-1)^T, d2 >= 2
-    int t = blockIdx.x - npanel, d1 = 2;
-    while (t >= d1 - 1) { t -= d1 - 1; ++d1; }
-    const int d2 = t + 2;
-    load_tile_lds(tile_ptr(b, j - 1 + d1, j - 1), Qs, tid, 256);
-    load_tile_lds(tile_ptr(b, j - 1 + d2, j - 1), Ps, tid, 256);
-    __syncthreads();
+  if (tk.kind == 1) {
+    // ---- update: dst -= sum A B^T
     v4d acc[2][2];
-    mfma_abt(Qs, Ps, w, l, acc);
-    double* dst = tile_ptr(b, j - 1 + d1, j - 1 + d2);
+    sum_pairs(b, pairs, tk.po_beg, tk.po_end, Qs, Rs, tid, w, l, acc);
+    double* dst = slot_ptr(b, tk.dst);
 #pragma unroll
     for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
@@ -227,15 +245,24 @@ __global__ __launch_bounds__(256) void k_step(BandDev b, int j, int npanel, doub
         for (int rr = 0; rr < 4; ++rr) dst[MFMA_ROW(w, l, ti, rr) * T + MFMA_COL(w, l, tj)] -= acc[ti][tj][rr];
     return;
   }
-  // ---- panel block d
-  const int d = blockIdx.x;
-  const bool has_prev = Dprev >= 1;             // tile (j, j-1) exists
-  const bool prev_d = d > 0 && Dprev >= d + 1;  // tile (j+d, j-1) exists
-  if (has_prev) load_tile_lds(tile_ptr(b, j, j - 1), Ps, tid, 256);
-  if (d > 0) load_tile_lds(tile_ptr(b, j + d, j), As, tid, 256);
-  if (prev_d) load_tile_lds(tile_ptr(b, j + d, j - 1), Qs, tid, 256);
+  // ---- panel
+  const bool own = tk.i != tk.k;
+  if (own) {
+    // A(i,k) -= sum L(i,c) L(k,c)^T  (pending contributions)
+    load_tile_lds(slot_ptr(b, tk.dst), As, tid, 256);
+    if (tk.po_end > tk.po_beg) {
+      v4d acc[2][2];
+      sum_pairs(b, pairs, tk.po_beg, tk.po_end, Qs, Rs, tid, w, l, acc);
+#pragma unroll
+      for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) As[MFMA_ROW(w, l, ti, rr) * LD + MFMA_COL(w, l, tj)] -= acc[ti][tj][rr];
+    }
+  }
   v4d accA[4], accX[4];
-  const double* diag = tile_ptr(b, j, j);
+  const double* diag = slot_ptr(b, tk.diag);
 #pragma unroll
   for (int TJ = 0; TJ < 4; ++TJ)
 #pragma unroll
@@ -244,10 +271,12 @@ __global__ __launch_bounds__(256) void k_step(BandDev b, int j, int npanel, doub
       accA[TJ][rr] = diag[row * T + col];
       accX[TJ][rr] = row == col ? 1.0 : 0.0;
     }
-  __syncthreads();
   const int li = l & 15, lk = l >> 4;
-  if (has_prev) {
-    // A_jj -= L(j,j-1) L(j,j-1)^T into the accumulators (K = 64)
+  for (int e = tk.pd_beg; e < tk.pd_end; ++e) {
+    // A_kk -= L(k,c) L(k,c)^T into the accumulators (K = 64)
+    __syncthreads();
+    load_tile_lds(slot_ptr(b, pairs[2 * e]), Ps, tid, 256);
+    __syncthreads();
 #pragma unroll 4
     for (int k0 = 0; k0 < T; k0 += 4) {
       const double a = -Ps[(16 * w + li) * LD + k0 + lk];
@@ -256,48 +285,42 @@ __global__ __launch_bounds__(256) void k_step(BandDev b, int j, int npanel, doub
         accA[TJ] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Ps[(16 * TJ + li) * LD + k0 + lk], accA[TJ], 0, 0, 0);
     }
   }
-  if (prev_d) {
-    // A_dj -= L(j+d,j-1) L(j,j-1)^T
-    v4d acc[2][2];
-    mfma_abt(Qs, Ps, w, l, acc);
-#pragma unroll
-    for (int ti = 0; ti < 2; ++ti)
-#pragma unroll
-      for (int tj = 0; tj < 2; ++tj)
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) As[MFMA_ROW(w, l, ti, rr) * LD + MFMA_COL(w, l, tj)] -= acc[ti][tj][rr];
-  }
   __syncthreads();
   const bool ok = factor_tile_mfma(accA, accX, w, l, Pcol, Xrow);
-  if (!ok && d == 0 && tid == 0) *fail = 1;
-  // L_jj^-1 -> Ps (full square; upper part is exactly zero)
+  if (!ok && !own && tid == 0) *fail = 1;
+  // L_kk^-1 -> Ps (full square; upper part is exactly zero)
 #pragma unroll
   for (int TJ = 0; TJ < 4; ++TJ)
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) Ps[ACC_ROW(w, l, rr) * LD + ACC_COL(TJ, l)] = accX[TJ][rr];
-  if (d == 0) {
-    double* dst = Linv + static_cast<int64_t>(j) * T * T;
+  if (!own) {
+    double* dst = Linv + static_cast<int64_t>(tk.k) * T * T;
 #pragma unroll
     for (int TJ = 0; TJ < 4; ++TJ)
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) dst[ACC_ROW(w, l, rr) * T + ACC_COL(TJ, l)] = accX[TJ][rr];
   }
-  const double* rj = r + static_cast<int64_t>(j) * T;
-  if (tid < T) vv[tid] = rj[tid];
+  // r_k minus the contributions L(k,c) y_c of the columns already eliminated
+  if (tid < T) {
+    double v = r[static_cast<int64_t>(tk.k) * T + tid];
+    for (int e = b.row_start[tk.k]; e < b.row_start[tk.k + 1]; ++e)
+      if (b.row_col[e] != tk.k) v -= contrib[static_cast<int64_t>(b.row_slot[e]) * T + tid];
+    vv[tid] = v;
+  }
   __syncthreads();
-  // y_j = L_jj^-1 r_j
+  // y_k = L_kk^-1 r_k
   const double yrow = lower_gemv4(Ps, vv, tid);
   __syncthreads();
   if ((tid & 3) == 0) {
     vv[tid >> 2] = yrow;
-    if (d == 0) y[static_cast<int64_t>(j) * T + (tid >> 2)] = yrow;
+    if (!own) y[static_cast<int64_t>(tk.k) * T + (tid >> 2)] = yrow;
   }
-  if (d == 0) return;
-  // L(j+d, j) = A L^-T
+  if (!own) return;
+  // L(i, k) = A L^-T
   v4d acc[2][2];
   mfma_abt(As, Ps, w, l, acc);
   __syncthreads();
-  double* dst = tile_ptr(b, j + d, j);
+  double* dst = slot_ptr(b, tk.dst);
 #pragma unroll
   for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
@@ -309,82 +332,67 @@ __global__ __launch_bounds__(256) void k_step(BandDev b, int j, int npanel, doub
         As[row * LD + col] = acc[ti][tj][rr];
       }
   __syncthreads();
-  // r_{j+d} -= L(j+d, j) y_j (4 lanes per row)
+  // contribution of this tile to row i's right-hand side: L(i, k) y_k
   {
     const int row = tid >> 2, part = tid & 3;
     double s = 0.0;
     for (int m = part; m < T; m += 4) s += As[row * LD + m] * vv[m];
     s += __shfl_xor(s, 1);
     s += __shfl_xor(s, 2);
-    if (part == 0) r[static_cast<int64_t>(j + d) * T + row] -= s;
+    if (part == 0) contrib[static_cast<int64_t>(tk.dst) * T + row] = s;
   }
 }
 
-// backward substitution with the stored inverses (one workgroup)
-constexpr int kBackThreads = 1024;
-__global__ __launch_bounds__(kBackThreads) void k_band_back(BandDev b, const double* __restrict__ Linv,
-                                                            const double* __restrict__ y, double* __restrict__ x) {
-  constexpr int NP = kBackThreads / T;  // 16 parts
+// one level of the backward substitution: a workgroup per column tile k,
+// x_k = L_kk^-T (y_k - sum_i L(i,k)^T x_i)
+__global__ __launch_bounds__(256) void k_back(TileDev b, const BackTask* __restrict__ tasks,
+                                              const int32_t* __restrict__ ent, const double* __restrict__ Linv,
+                                              const double* __restrict__ y, double* __restrict__ x) {
+  constexpr int NP = 4;
   __shared__ double part[NP][T];
   __shared__ double rv[T];
+  const BackTask tk = tasks[blockIdx.x];
   const int tid = threadIdx.x, c = tid & (T - 1), q = tid >> 6;
-  for (int i = b.NT - 1; i >= 0; --i) {
-    const int D = b.D[i];
-    // sum_d sum_m L(i+d, i)[m][c] x_{i+d}[m]; the D*64 (d, m) rows are split
-    // over 16 parts, 4 independent loads in flight per thread
-    const double* col = b.band + b.off[i] + static_cast<int64_t>(T) * T;
-    const double* xs = x + static_cast<int64_t>(i + 1) * T;
-    const int nrow = D * T;
-    double s = 0.0, s1 = 0.0, s2a = 0.0, s3 = 0.0;
-    int row = q;
-    for (; row + 3 * NP < nrow; row += 4 * NP) {
-      const double a0 = col[static_cast<int64_t>(row) * T + c], a1 = col[static_cast<int64_t>(row + NP) * T + c];
-      const double a2 = col[static_cast<int64_t>(row + 2 * NP) * T + c], a3 = col[static_cast<int64_t>(row + 3 * NP) * T + c];
-      s += a0 * xs[row];
-      s1 += a1 * xs[row + NP];
-      s2a += a2 * xs[row + 2 * NP];
-      s3 += a3 * xs[row + 3 * NP];
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  for (int e = tk.beg; e < tk.end; ++e) {
+    const double* L = slot_ptr(b, ent[2 * e]);
+    const double* xi = x + static_cast<int64_t>(ent[2 * e + 1]) * T;
+    // rows m = q, q+4, ...: 4 independent accumulators
+    for (int m = q; m < T; m += 4 * NP) {
+      s0 += L[m * T + c] * xi[m];
+      s1 += L[(m + NP) * T + c] * xi[m + NP];
+      s2 += L[(m + 2 * NP) * T + c] * xi[m + 2 * NP];
+      s3 += L[(m + 3 * NP) * T + c] * xi[m + 3 * NP];
     }
-    for (; row < nrow; row += NP) s += col[static_cast<int64_t>(row) * T + c] * xs[row];
-    s = (s + s1) + (s2a + s3);
-    part[q][c] = s;
-    __syncthreads();
-    if (tid < T) {
-      double t2 = 0.0;
-#pragma unroll
-      for (int k = 0; k < NP; ++k) t2 += part[k][tid];
-      rv[tid] = y[static_cast<int64_t>(i) * T + tid] - t2;
-    }
-    __syncthreads();
-    // x_i = Linv^T rv : x[c] = sum_{m >= c} Linv[m][c] rv[m]
-    const double* Li = Linv + static_cast<int64_t>(i) * T * T;
-    double s2 = 0.0;
-    for (int m = q; m < T; m += NP)
-      if (m >= c) s2 += Li[m * T + c] * rv[m];
-    part[q][c] = s2;
-    __syncthreads();
-    if (tid < T) {
-      double t3 = 0.0;
-#pragma unroll
-      for (int k = 0; k < NP; ++k) t3 += part[k][tid];
-      x[static_cast<int64_t>(i) * T + tid] = t3;
-    }
-    __syncthreads();
   }
+  part[q][c] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (tid < T) rv[tid] = y[static_cast<int64_t>(tk.k) * T + tid] - ((part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]));
+  __syncthreads();
+  // x_k[c] = sum_{m >= c} Linv[m][c] rv[m]
+  const double* Li = Linv + static_cast<int64_t>(tk.k) * T * T;
+  double t = 0.0;
+  for (int m = q; m < T; m += NP)
+    if (m >= c) t += Li[m * T + c] * rv[m];
+  part[q][c] = t;
+  __syncthreads();
+  if (tid < T)
+    x[static_cast<int64_t>(tk.k) * T + tid] = (part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]);
 }
 
 }  // namespace
 
-void launch_band_cholesky_solve(const BandDev& b, const int32_t* host_D, double* Linv, double* r, double* y,
-                                double* x, int* fail, hipStream_t s) {
-  for (int j = 0; j < b.NT; ++j) {
-    const int npanel = host_D[j] + 1;
-    const int Dp = j > 0 ? host_D[j - 1] : 0;
-    const int nupd = Dp >= 2 ? (Dp - 1) * Dp / 2 : 0;
-    k_step<<<npanel + nupd, 256, 0, s>>>(b, j, npanel, Linv, r, y, fail);
+void launch_tile_cholesky_solve(const TileDev& b, const TileSchedDev& sd, const std::vector<int32_t>& flevel,
+                                const std::vector<int32_t>& blevel, double* Linv, const double* r, double* contrib,
+                                double* y, double* x, int* fail, hipStream_t s) {
+  for (size_t lv = 0; lv + 1 < flevel.size(); ++lv) {
+    const int n = flevel[lv + 1] - flevel[lv];
+    if (n > 0) k_tasks<<<n, 256, 0, s>>>(b, sd.ftask + flevel[lv], sd.pairs, Linv, r, contrib, y, fail);
   }
-  // column NT-1 has no sub-diagonal tiles, so no trailing update is left over
-  if (b.NT > 0) k_band_back<<<1, kBackThreads, 0, s>>>(b, Linv, y, x);
+  for (size_t lv = 0; lv + 1 < blevel.size(); ++lv) {
+    const int n = blevel[lv + 1] - blevel[lv];
+    if (n > 0) k_back<<<n, 256, 0, s>>>(b, sd.btask + blevel[lv], sd.bent, Linv, y, x);
+  }
 }
 
 }  // namespace dynohip

@@ -1,0 +1,354 @@
+// tiles.cpp — tile-level symbolic factorisation and task schedule of the
+// reduced pose system.
+//
+// The reference factors the reduced system inside GTSAM's multifrontal
+// Cholesky. It eliminates the whole graph under a COLAMD ordering on every
+// LM iteration (NonlinearOptimizer.cpp / GaussianFactorGraph::optimize,
+// reached from RGBDBackendModule.cc:220 and :374).
+//
+// Here the points are removed analytically by the chain Schur complement,
+// so the remaining pose system is a banded matrix over frame order. It is
+// partitioned into 64x64 FP64 tiles, and its Cholesky is a DAG of two
+// workgroup task kinds (tilechol.hip):
+//   panel(k, i)    factor the diagonal tile A(k,k) (every panel of column k
+//                  redundantly, in registers), then produce L(i,k). Before
+//                  that it applies the last outstanding update of A(k,k) and
+//                  of A(i,k). It also carries the forward substitution:
+//                  y_k = L_kk^-1 r_k, then r_i -= L(i,k) y_k.
+//   update(i,j,c)  A(i,j) -= L(i,c) L(j,c)^T.
+// Tiles are ordered by nested dissection over frame order: recursive
+// bisection of the tile range with a separator of the band's reach. Every
+// leaf segment of the time axis is factored concurrently, and the
+// separators are eliminated last. The DAG is scheduled in levels (longest
+// path from the sources); one kernel launch runs one level. Natural order
+// (no dissection) reproduces the plain band algorithm, one column per
+// level. The leaf size is picked by a small cost model of the launch
+// sequence.
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <cstdint>
+#include <functional>
+#include <vector>
+
+#include "plan.hpp"
+
+namespace dynohip {
+
+namespace {
+
+struct Sched {
+  int leaf = 0;
+  std::vector<int32_t> order;               // tile at position p
+  std::vector<int32_t> pos;                 // position of tile t
+  std::vector<std::vector<int32_t>> st;     // per column position: row positions (sorted, incl. itself)
+  std::vector<int32_t> slot_base;           // per column position
+  int32_t n_slots = 0;
+  std::vector<TileTask> ftask;
+  std::vector<int32_t> flevel;
+  std::vector<int32_t> pairs;
+  std::vector<BackTask> btask;
+  std::vector<int32_t> blevel;
+  std::vector<int32_t> bent;
+  double cost = 0.0;
+  double flops = 0.0;
+
+  int32_t slot(int rp, int cp) const {
+    const auto& s = st[cp];
+    const auto it = std::lower_bound(s.begin(), s.end(), rp);
+    return slot_base[cp] + static_cast<int32_t>(it - s.begin());
+  }
+};
+
+// nested-dissection order of tiles [lo, hi); maxnb[t] = largest neighbour
+void nd_order(int lo, int hi, int leaf, const std::vector<int32_t>& maxnb, std::vector<int32_t>& out) {
+  const int n = hi - lo;
+  if (leaf <= 0 || n <= leaf) {
+    for (int t = lo; t < hi; ++t) out.push_back(t);
+    return;
+  }
+  const int m = lo + n / 2;
+  int reach = m - 1;
+  for (int t = lo; t < m; ++t) reach = std::max(reach, std::min(maxnb[t], hi - 1));
+  const int s_end = reach + 1;  // separator [m, s_end)
+  if (hi - s_end < 1 || s_end - m >= n / 2) {
+    for (int t = lo; t < hi; ++t) out.push_back(t);
+    return;
+  }
+  nd_order(lo, m, leaf, maxnb, out);
+  nd_order(s_end, hi, leaf, maxnb, out);
+  for (int t = m; t < s_end; ++t) out.push_back(t);
+}
+
+void schedule(int NT, const std::vector<std::vector<int32_t>>& adj, const std::vector<int32_t>& maxnb, int leaf,
+              Sched& S) {
+  S.leaf = leaf;
+  S.order.clear();
+  nd_order(0, NT, leaf, maxnb, S.order);
+  S.pos.assign(NT, 0);
+  for (int p = 0; p < NT; ++p) S.pos[S.order[p]] = p;
+  // ---- symbolic factorisation (elimination tree merge) in position space
+  S.st.assign(NT, {});
+  for (int cp = 0; cp < NT; ++cp) {
+    auto& s = S.st[cp];
+    s.push_back(cp);
+    for (int32_t u : adj[S.order[cp]]) {
+      const int up = S.pos[u];
+      if (up > cp) s.push_back(up);
+    }
+  }
+  for (int cp = 0; cp < NT; ++cp) {
+    auto& s = S.st[cp];
+    std::sort(s.begin(), s.end());
+    s.erase(std::unique(s.begin(), s.end()), s.end());
+    if (s.size() > 1) {
+      auto& par = S.st[s[1]];
+      par.insert(par.end(), s.begin() + 1, s.end());
+    }
+  }
+  S.slot_base.assign(NT, 0);
+  int32_t ns = 0;
+  for (int cp = 0; cp < NT; ++cp) {
+    S.slot_base[cp] = ns;
+    ns += static_cast<int32_t>(S.st[cp].size());
+  }
+  S.n_slots = ns;
+  // ---- tasks with levels (1-based; 0 = available at start). Every stored
+  // tile collects its update contributions (column c, ready level R_c).
+  // Contributions ready one level before the tile's panel are applied by
+  // the panel itself; earlier ones by update tasks. Each update task applies
+  // every contribution ready by then, so a tile's read-modify-write chain
+  // is as long as the number of distinct ready levels, not the number of
+  // columns.
+  struct Contrib {
+    int32_t R, a, b;  // ready level, operand slots (A B^T)
+  };
+  std::vector<std::vector<Contrib>> contrib(ns);
+  std::vector<int32_t> lvlP(ns, 0);
+  struct LT {
+    int32_t lvl;
+    TileTask t;
+    std::vector<int32_t> pd, po;  // pairs
+  };
+  std::vector<LT> tasks;
+  const double T3 = static_cast<double>(kTile) * kTile * kTile;
+  double flops = 0.0;
+  // split contributions (sorted by R) into update tasks finishing before
+  // level P and the pairs the panel at level P absorbs
+  auto plan_tile = [&](int32_t sl, int32_t P, std::vector<int32_t>& absorbed) {
+    auto& cs = contrib[sl];
+    std::sort(cs.begin(), cs.end(), [](const Contrib& x, const Contrib& y) { return x.R < y.R; });
+    size_t q = 0;
+    while (q < cs.size() && cs[q].R <= P - 2) {
+      const int32_t t = cs[q].R + 1;
+      LT u{t, TileTask{1, -1, -1, sl, -1, 0, 0, 0, 0, 0}, {}, {}};
+      while (q < cs.size() && cs[q].R <= t - 1) {
+        u.po.push_back(cs[q].a);
+        u.po.push_back(cs[q].b);
+        ++q;
+      }
+      tasks.push_back(std::move(u));
+    }
+    for (; q < cs.size(); ++q) {
+      absorbed.push_back(cs[q].a);
+      absorbed.push_back(cs[q].b);
+    }
+  };
+  for (int cp = 0; cp < NT; ++cp) {
+    const auto& s = S.st[cp];
+    const int32_t dslot = S.slot(cp, cp);
+    int32_t Rd = 0;
+    for (const Contrib& c : contrib[dslot]) Rd = std::max(Rd, c.R);
+    const int32_t Pd = Rd + 1;
+    std::vector<int32_t> pd;
+    plan_tile(dslot, Pd, pd);
+    flops += T3 / 3.0;
+    for (int32_t rp : s) {
+      const int32_t sl = S.slot(rp, cp);
+      LT t{Pd, TileTask{0, S.order[cp], S.order[rp], sl, dslot, 0, 0, 0, 0, 0}, pd, {}};
+      if (rp != cp) {
+        int32_t Ro = 0;
+        for (const Contrib& c : contrib[sl]) Ro = std::max(Ro, c.R);
+        t.lvl = std::max(Pd, Ro + 1);
+        plan_tile(sl, t.lvl, t.po);
+        flops += T3;
+      }
+      lvlP[sl] = t.lvl;
+      tasks.push_back(std::move(t));
+    }
+    for (size_t x = 1; x < s.size(); ++x)
+      for (size_t y = 1; y <= x; ++y) {
+        const int32_t sa = S.slot(s[x], cp), sb = S.slot(s[y], cp);
+        contrib[S.slot(s[x], s[y])].push_back({std::max(lvlP[sa], lvlP[sb]), sa, sb});
+        flops += 2.0 * T3;
+      }
+  }
+  S.flops = flops;
+  std::stable_sort(tasks.begin(), tasks.end(), [](const LT& x, const LT& y) { return x.lvl < y.lvl; });
+  S.ftask.clear();
+  S.flevel.clear();
+  S.pairs.clear();
+  int cur = 0;
+  for (LT& t : tasks) {
+    while (cur < t.lvl) {
+      S.flevel.push_back(static_cast<int32_t>(S.ftask.size()));
+      ++cur;
+    }
+    auto put = [&](const std::vector<int32_t>& v, int32_t& beg, int32_t& end) {
+      beg = static_cast<int32_t>(S.pairs.size() / 2);
+      S.pairs.insert(S.pairs.end(), v.begin(), v.end());
+      end = static_cast<int32_t>(S.pairs.size() / 2);
+    };
+    put(t.pd, t.t.pd_beg, t.t.pd_end);
+    put(t.po, t.t.po_beg, t.t.po_end);
+    S.ftask.push_back(t.t);
+  }
+  S.flevel.push_back(static_cast<int32_t>(S.ftask.size()));
+  // ---- backward substitution levels
+  std::vector<int32_t> blv(NT, 0);
+  int maxb = 0;
+  for (int cp = NT - 1; cp >= 0; --cp) {
+    int32_t L = 0;
+    for (size_t x = 1; x < S.st[cp].size(); ++x) L = std::max(L, blv[S.st[cp][x]]);
+    blv[cp] = L + 1;
+    maxb = std::max(maxb, L + 1);
+  }
+  S.btask.clear();
+  S.blevel.assign(1, 0);
+  S.bent.clear();
+  for (int lv = 1; lv <= maxb; ++lv) {
+    for (int cp = NT - 1; cp >= 0; --cp) {
+      if (blv[cp] != lv) continue;
+      BackTask b{S.order[cp], static_cast<int32_t>(S.bent.size() / 2), 0, 0};
+      for (size_t x = 1; x < S.st[cp].size(); ++x) {
+        S.bent.push_back(S.slot(S.st[cp][x], cp));
+        S.bent.push_back(S.order[S.st[cp][x]]);
+      }
+      b.end = static_cast<int32_t>(S.bent.size() / 2);
+      S.btask.push_back(b);
+    }
+    S.blevel.push_back(static_cast<int32_t>(S.btask.size()));
+  }
+  // ---- cost model (microseconds): a launch per level; a workgroup round
+  // with a panel is dominated by the in-register diagonal factorisation
+  constexpr int kCUs = 256;
+  double cost = 0.0;
+  const int nlev = static_cast<int>(S.flevel.size()) - 1;
+  for (int l = 0; l < nlev; ++l) {
+    const int n = S.flevel[l + 1] - S.flevel[l];
+    double worst = 0.0;
+    for (int32_t q = S.flevel[l]; q < S.flevel[l + 1]; ++q) {
+      const TileTask& t = S.ftask[q];
+      const int np = (t.pd_end - t.pd_beg) + (t.po_end - t.po_beg);
+      worst = std::max(worst, (t.kind == 0 ? 30.0 : 4.0) + 3.0 * np);
+    }
+    cost += 2.0 + worst * ((n + kCUs - 1) / kCUs);
+  }
+  for (size_t l = 0; l + 1 < S.blevel.size(); ++l) cost += 4.0;
+  S.cost = cost;
+}
+
+int g_leaf_override = -1;
+
+}  // namespace
+
+void build_tile_schedule(Plan& P) {
+  const int NT = P.NT;
+  std::vector<std::vector<int32_t>> adj(NT);
+  std::vector<int32_t> maxnb(NT);
+  for (int t = 0; t < NT; ++t) maxnb[t] = t;
+  for (size_t q = 0; q < P.red_A.size(); ++q) {
+    const int r0 = (6 * P.red_A[q]) / kTile, r1 = (6 * P.red_A[q] + 5) / kTile;
+    const int c0 = (6 * P.red_B[q]) / kTile, c1 = (6 * P.red_B[q] + 5) / kTile;
+    for (int a = r0; a <= r1; ++a)
+      for (int b = c0; b <= c1; ++b) {
+        if (a == b) continue;
+        adj[a].push_back(b);
+        adj[b].push_back(a);
+        maxnb[std::min(a, b)] = std::max(maxnb[std::min(a, b)], std::max(a, b));
+      }
+  }
+  for (auto& v : adj) {
+    std::sort(v.begin(), v.end());
+    v.erase(std::unique(v.begin(), v.end()), v.end());
+  }
+  Sched best;
+  schedule(NT, adj, maxnb, g_leaf_override > 0 ? g_leaf_override : 0, best);
+  if (g_leaf_override < 0) {
+    for (int leaf : {4, 6, 8, 12, 16, 24, 32, 48, 64}) {
+      if (leaf >= NT) break;
+      Sched cand;
+      schedule(NT, adj, maxnb, leaf, cand);
+      if (cand.cost < best.cost) best = std::move(cand);
+    }
+  }
+  P.nd_leaf = best.leaf;
+  P.tile_pos = best.pos;
+  P.n_slots = best.n_slots;
+  P.ftask = std::move(best.ftask);
+  P.pairs = std::move(best.pairs);
+  P.flevel = std::move(best.flevel);
+  P.btask = std::move(best.btask);
+  P.blevel = std::move(best.blevel);
+  P.bent = std::move(best.bent);
+  P.tile_flops = best.flops;
+  // per-row lookup for the assembly: stored tile (row tile, column tile)
+  std::vector<std::vector<std::pair<int32_t, int32_t>>> rows(NT);
+  for (int cp = 0; cp < NT; ++cp)
+    for (int32_t rp : best.st[cp]) rows[best.order[rp]].push_back({best.order[cp], best.slot(rp, cp)});
+  P.row_start.assign(NT + 1, 0);
+  P.row_col.clear();
+  P.row_slot.clear();
+  for (int t = 0; t < NT; ++t) {
+    std::sort(rows[t].begin(), rows[t].end());
+    for (const auto& e : rows[t]) {
+      P.row_col.push_back(e.first);
+      P.row_slot.push_back(e.second);
+    }
+    P.row_start[t + 1] = static_cast<int32_t>(P.row_col.size());
+  }
+}
+
+}  // namespace dynohip
+
+extern "C" void dynohip_set_tile_ordering(int leaf) { dynohip::g_leaf_override = leaf < 0 ? -1 : leaf; }
+
+extern "C" int dynohip_plan_schedule(const dynohip_graph_view* g, const uint64_t* keys, const uint8_t* kind, size_t n,
+                                     dynohip_schedule_info* info, int32_t* tile_pos, int32_t* ftask,
+                                     int32_t* pairs, int32_t* flevel, int32_t* btask, int32_t* blevel, int32_t* bent,
+                                     int32_t* row_start, int32_t* row_col, int32_t* row_slot, int32_t* red_a,
+                                     int32_t* red_b) {
+  using namespace dynohip;
+  if (!g || !info || (n && (!keys || !kind))) return DYNOHIP_EINVAL;
+  Plan P;
+  std::string err;
+  const int rc = build_plan(*g, keys, kind, n, P, err);
+  if (rc) return rc;
+  info->n_pose = P.n_pose;
+  info->n_tiles = P.NT;
+  info->n_slots = P.n_slots;
+  info->n_ftask = static_cast<int64_t>(P.ftask.size());
+  info->n_pairs = static_cast<int64_t>(P.pairs.size() / 2);
+  info->n_flevel = static_cast<int64_t>(P.flevel.size());
+  info->n_btask = static_cast<int64_t>(P.btask.size());
+  info->n_blevel = static_cast<int64_t>(P.blevel.size());
+  info->n_bent = static_cast<int64_t>(P.bent.size() / 2);
+  info->n_red_blocks = static_cast<int64_t>(P.red_A.size());
+  info->nd_leaf = P.nd_leaf;
+  auto put = [](int32_t* dst, const void* src, size_t bytes) {
+    if (dst && bytes) std::memcpy(dst, src, bytes);
+  };
+  put(tile_pos, P.tile_pos.data(), P.tile_pos.size() * 4);
+  put(ftask, P.ftask.data(), P.ftask.size() * sizeof(TileTask));
+  put(pairs, P.pairs.data(), P.pairs.size() * 4);
+  put(flevel, P.flevel.data(), P.flevel.size() * 4);
+  put(btask, P.btask.data(), P.btask.size() * sizeof(BackTask));
+  put(blevel, P.blevel.data(), P.blevel.size() * 4);
+  put(bent, P.bent.data(), P.bent.size() * 4);
+  put(row_start, P.row_start.data(), P.row_start.size() * 4);
+  put(row_col, P.row_col.data(), P.row_col.size() * 4);
+  put(row_slot, P.row_slot.data(), P.row_slot.size() * 4);
+  put(red_a, P.red_A.data(), P.red_A.size() * 4);
+  put(red_b, P.red_B.data(), P.red_B.size() * 4);
+  return DYNOHIP_OK;
+}

@@ -150,3 +150,38 @@ class LevenbergMarquardtOptimizer:
 
     def trace(self):
         return self.solver.trace()
+
+
+def set_tile_ordering(leaf):
+    """Tile ordering for plans built afterwards (process-wide): -1 automatic,
+    0 frame order (plain band), k > 0 nested dissection with k-tile leaves."""
+    _native.load("libdynohip.so").dynohip_set_tile_ordering(int(leaf))
+
+
+def plan_schedule(graph, values):
+    """Host-only: the tile Cholesky schedule the solver would run for this
+    graph and key set (dynohip_plan_schedule). Returns a dict of arrays."""
+    lib = _native.load("libdynohip.so")
+    gv = graph.view()
+    keys = np.ascontiguousarray(values.keys, dtype=np.uint64)
+    kinds = np.ascontiguousarray(values.kinds, dtype=np.uint8)
+    kp = keys.ctypes.data_as(C.POINTER(C.c_uint64))
+    kk = kinds.ctypes.data_as(C.POINTER(C.c_uint8))
+    info = _abi.ScheduleInfo()
+    null = [None] * 12
+    rc = lib.dynohip_plan_schedule(C.byref(gv), kp, kk, keys.shape[0], C.byref(info), *null)
+    _check(lib, None, rc)
+    shapes = {
+        "tile_pos": info.n_tiles, "ftask": (info.n_ftask, 10), "pairs": (info.n_pairs, 2),
+        "flevel": info.n_flevel,
+        "btask": (info.n_btask, 4), "blevel": info.n_blevel, "bent": (info.n_bent, 2),
+        "row_start": info.n_tiles + 1, "row_col": info.n_slots, "row_slot": info.n_slots,
+        "red_a": info.n_red_blocks, "red_b": info.n_red_blocks,
+    }
+    arrs = {k: np.zeros(v, dtype=np.int32) for k, v in shapes.items()}
+    ptrs = [arrs[k].ctypes.data_as(C.POINTER(C.c_int32)) for k in shapes]
+    rc = lib.dynohip_plan_schedule(C.byref(gv), kp, kk, keys.shape[0], C.byref(info), *ptrs)
+    _check(lib, None, rc)
+    out = {k: getattr(info, k) for k, _ in _abi.ScheduleInfo._fields_}
+    out.update(arrs)
+    return out

@@ -201,8 +201,12 @@ int dynohip_values_restore(dynohip_solver* s);
 typedef struct {
   int64_t n_pose, n_point, n_factor, n_chain, n_edge;
   int64_t reduced_dim;       /* 6 * n_pose                                  */
-  int64_t band_tiles;        /* 64x64 tiles stored for the reduced band     */
-  int64_t band_max_tiles;    /* max sub-diagonal tiles in a column          */
+  int64_t tiles_stored;      /* 64x64 tiles stored (lower factor incl. fill) */
+  int64_t band_max_tiles;    /* max sub-diagonal tiles in a column (frame
+                                order)                                      */
+  int64_t chol_levels;       /* launches of the tile factorisation          */
+  int64_t back_levels;       /* launches of the backward substitution       */
+  int64_t nd_leaf;           /* nested-dissection leaf (tiles; 0 = none)    */
   double lin_bytes;          /* algorithmic HBM bytes of one linearisation
                                 (factor records + values read, J|b written) */
   double assembly_bytes;     /* algorithmic bytes of one reduced assembly
@@ -218,6 +222,28 @@ typedef struct {
 int dynohip_get_stats(dynohip_solver* s, dynohip_stats* out);
 /* 1: record HIP events around every phase (default 0: none) */
 int dynohip_set_timing(dynohip_solver* s, int enabled);
+
+/* Host-only plan introspection (no device needed): the tile schedule of
+   the reduced pose system for a graph and key set, for tests and tooling.
+   Call with null arrays to get the sizes in *info, then again with arrays
+   of those sizes. ftask: 10 ints per task (TileTask), pairs: 2 ints per
+   operand pair (A slot, B slot), btask: 4 ints per
+   task, bent: 2 ints per entry (slot, row tile), red_a/red_b: the 6x6
+   pose-pair blocks (A >= B) present in the reduced system. */
+typedef struct {
+  int64_t n_pose, n_tiles, n_slots, n_ftask, n_pairs, n_flevel, n_btask, n_blevel, n_bent, n_red_blocks, nd_leaf;
+} dynohip_schedule_info;
+
+/* Tile ordering of the reduced system for plans built after the call
+   (process-wide): -1 = automatic (cost model, default), 0 = frame order
+   (plain band), k > 0 = nested dissection with leaves of k tiles. */
+void dynohip_set_tile_ordering(int leaf);
+
+int dynohip_plan_schedule(const dynohip_graph_view* g, const uint64_t* keys, const uint8_t* kind, size_t n,
+                          dynohip_schedule_info* info, int32_t* tile_pos, int32_t* ftask, int32_t* pairs,
+                          int32_t* flevel,
+                          int32_t* btask, int32_t* blevel, int32_t* bent, int32_t* row_start, int32_t* row_col,
+                          int32_t* row_slot, int32_t* red_a, int32_t* red_b);
 
 /* ------------------------------------------------------------------ */
 /* Window / batch drivers (integer, bit-exact)                          */
