@@ -76,41 +76,12 @@ __device__ __forceinline__ void mfma_abt(const double* As, const double* Bs, int
 #define MFMA_ROW(wave, lane, ti, r) (32 * ((wave) >> 1) + 16 * (ti) + ((lane) >> 4) + 4 * (r))
 #define MFMA_COL(wave, lane, tj) (32 * ((wave) & 1) + 16 * (tj) + ((lane) & 15))
 
-__device__ __forceinline__ double pivot_ok(double x, bool& ok) {
-  if (!(x > 0.0) || !isfinite(x)) {
-    ok = false;
-    return 1.0;
-  }
-  return x;
-}
-
 // 1/sqrt(x): hardware estimate + two Newton steps (full FP64 accuracy)
 __device__ __forceinline__ double rsqrt_nr(double x) {
   double y = __builtin_amdgcn_rsq(x);
   y = y * (1.5 - 0.5 * x * y * y);
   y = y * (1.5 - 0.5 * x * y * y);
   return y;
-}
-
-// 4x4 Cholesky + inverse of a lower 4x4 (row-major a[4][4]); m receives
-// L^-1 (lower). Only the reciprocal pivots r_i = 1/l_ii are formed.
-// ok is cleared on a non-positive pivot.
-__device__ __forceinline__ void chol_inv4(const double (&a)[4][4], double (&m)[4][4], bool& ok) {
-  const double r0 = rsqrt_nr(pivot_ok(a[0][0], ok));
-  const double l10 = a[1][0] * r0, l20 = a[2][0] * r0, l30 = a[3][0] * r0;
-  const double r1 = rsqrt_nr(pivot_ok(a[1][1] - l10 * l10, ok));
-  const double l21 = (a[2][1] - l20 * l10) * r1, l31 = (a[3][1] - l30 * l10) * r1;
-  const double r2 = rsqrt_nr(pivot_ok(a[2][2] - l20 * l20 - l21 * l21, ok));
-  const double l32 = (a[3][2] - l30 * l20 - l31 * l21) * r2;
-  const double r3 = rsqrt_nr(pivot_ok(a[3][3] - l30 * l30 - l31 * l31 - l32 * l32, ok));
-  m[0][0] = r0; m[1][1] = r1; m[2][2] = r2; m[3][3] = r3;
-  m[1][0] = -r1 * (l10 * r0);
-  m[2][1] = -r2 * (l21 * r1);
-  m[3][2] = -r3 * (l32 * r2);
-  m[2][0] = -r2 * (l20 * r0 + l21 * m[1][0]);
-  m[3][1] = -r3 * (l31 * r1 + l32 * m[2][1]);
-  m[3][0] = -r3 * (l30 * r0 + l31 * m[1][0] + l32 * m[2][0]);
-  m[0][1] = m[0][2] = m[0][3] = m[1][2] = m[1][3] = m[2][3] = 0.0;
 }
 
 __device__ __forceinline__ double* slot_ptr(const TileDev& b, int32_t slot) {
@@ -123,70 +94,119 @@ __device__ __forceinline__ double* slot_ptr(const TileDev& b, int32_t slot) {
 #define ACC_ROW(w, l, r) (16 * (w) + ((l) >> 4) + 4 * (r))
 #define ACC_COL(TJ, l) (16 * (TJ) + ((l) & 15))
 
-// Factor the diagonal tile held in accumulator layout (accA) and build its
-// inverse (accX, starting from I). Right-looking, 4 pivots per step:
-//   publish column block kb of A and row block kb of the running inverse
-//   to LDS (double-buffered), one barrier; every lane forms M = L_kk^-1
-//   (4x4) redundantly, the panel entries it feeds to the MFMAs
-//   (L = A_panel M^T, zero for rows <= 4kb+3) and the finalised inverse
-//   rows Xf = M X_kb; then accA -= L L^T and accX -= L Xf (4+4
-//   v_mfma_f64_16x16x4 per wave) and X rows 4kb.. are replaced by Xf.
-__device__ bool factor_tile_mfma(v4d (&accA)[4], v4d (&accX)[4], int w, int l, double* Pcol, double* Xrow) {
+// ---- 16x16 in-wave factorisation (no barriers) --------------------------
+// A 16x16 block in MFMA accumulator layout: lane l, register r holds
+// element (row (l>>4) + 4r, column l&15). The same registers serve as the
+// B operand of v_mfma_f64_16x16x4 for K-slice r, and as the A operand of
+// the block's transpose.
+
+__device__ __forceinline__ double bcast_row_lane(double v, int p) {
+  // lane p of every 16-lane row -> the whole row (DPP row_newbcast)
+  switch (p) {
+#define NB(q) case q: return __builtin_amdgcn_update_dpp(v, v, 0x150 + q, 0xf, 0xf, false);
+    NB(0) NB(1) NB(2) NB(3) NB(4) NB(5) NB(6) NB(7) NB(8) NB(9) NB(10) NB(11) NB(12) NB(13) NB(14) NB(15)
+#undef NB
+  }
+  return v;
+}
+
+__device__ __forceinline__ double pull_lane(double v, int src) {
+  const int a = src << 2;
+  const int lo = __builtin_amdgcn_ds_bpermute(a, __double2loint(v));
+  const int hi = __builtin_amdgcn_ds_bpermute(a, __double2hiint(v));
+  return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double read_lane(double v, int lane) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+  return __hiloint2double(hi, lo);
+}
+
+// B (symmetric, full) = U^T U; on return W = U^-1 (upper) and B is
+// scratch. Right-looking by rows: pivot p's row is pulled across row
+// groups (ds_bpermute), its column broadcast within them (DPP). Entries
+// of B in rows or columns <= p are never read after pivot p, so the
+// trailing update runs unmasked on the registers that still hold rows > p.
+// W is updated unscaled (W~[c][i] -= W~[c][p] U[p][i] / U[p][p]) and each
+// column is scaled by its 1/U[j][j] once at the end.
+__device__ __forceinline__ void factor16_wave(v4d& B, v4d& W, int l, bool& ok) {
+  const int j = l & 15;
+  double myrs = 1.0;
+  bool good = true;
+#pragma unroll
+  for (int p = 0; p < 16; ++p) {
+    const int rp = p >> 2, gp = p & 3;
+    const double d = read_lane(B[rp], 16 * gp + p);
+    good = good && (d > 0.0) && (d < 1e300);
+    const double rowp = pull_lane(B[rp], j + 16 * gp);  // B[p][j]
+    const double rs = rsqrt_nr(d);
+    const double f = rowp * (rs * rs);                   // U[p][j] / U[p][p]
+    const double fm = j > p ? f : 0.0;
+    myrs = j == p ? rs : myrs;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (4 * r + 3 > p) B[r] -= bcast_row_lane(B[r], p) * f;     // rows g+4r > p
+      if (4 * r <= p) W[r] -= bcast_row_lane(W[r], p) * fm;      // W~[c][p] != 0 only for c <= p
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) W[r] *= myrs;
+  ok = ok && good;
+}
+
+// acc (+)= Y^T Z for 16x16 blocks Y, Z in accumulator layout (K = 16)
+__device__ __forceinline__ v4d mfma_tn(const v4d& Y, const v4d& Z, v4d acc, bool neg) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(neg ? -Y[r] : Y[r], Z[r], acc, 0, 0, 0);
+  return acc;
+}
+
+// Factor the 64x64 tile held as upper 16x16 blocks (wave w: accA[TJ] =
+// block (w, TJ), TJ >= w, full symmetric input) and build L^-1 in accX
+// (wave w: block row w; starts as I). Four block steps KB, one barrier each:
+//   wave KB: U_KK, W = U_KK^-1 in-wave; U row KB = W^T A[KB][TJ] (TJ > KB);
+//            X row KB = W^T X[KB][TJ] (final, TJ <= KB); publish both
+//   waves v > KB: A[v][TJ] -= U[KB][v]^T U[KB][TJ] (TJ >= v),
+//                 X[v][TJ] -= U[KB][v]^T X[KB][TJ] (TJ <= KB)
+// xch: 2 x 4 blocks x 256 doubles of LDS.
+__device__ bool factor_tile_blk(v4d (&accA)[4], v4d (&accX)[4], int w, int l, double* xch) {
   bool ok = true;
-  const int li = l & 15, lk = l >> 4;
+#pragma unroll
   for (int KB = 0; KB < 4; ++KB) {
+    double* xb = xch + (KB & 1) * 4 * 256;
+    if (w == KB) {
+      v4d W = v4d{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const int kb = 4 * KB + kk, p = kk & 1;
-      double* P = Pcol + p * (T * 4);
-      double* X = Xrow + p * (4 * T);
-      // publish A[:, 4kb..4kb+3] (tile column KB, in-tile cols 4kk..4kk+3)
-      if (li >= 4 * kk && li < 4 * kk + 4) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) P[ACC_ROW(w, l, r) * 4 + (li - 4 * kk)] = accA[KB][r];
-      }
-      // publish X[4kb..4kb+3, :] (wave KB, register kk)
-      if (w == KB) {
-#pragma unroll
-        for (int TJ = 0; TJ < 4; ++TJ) X[lk * T + ACC_COL(TJ, l)] = accX[TJ][kk];
-      }
-      __syncthreads();
-      // M = L_kk^-1 of the 4x4 pivot block (every lane, redundantly)
-      double a4[4][4], M[4][4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) a4[u][q] = P[(4 * kb + u) * 4 + q];
-      chol_inv4(a4, M, ok);
-      // panel entries fed to the MFMAs: L[i][k] = sum_{m<=k} A[i][m] M[k][m]
-      auto panel = [&](int i) {
-        double s = 0.0;
-#pragma unroll
-        for (int m = 0; m < 4; ++m) s += P[i * 4 + m] * M[lk][m];
-        return i > 4 * kb + 3 ? s : 0.0;
-      };
-      const double aL = -panel(16 * w + li);
-      double bL[4], xf[4];
+      for (int r = 0; r < 4; ++r) W[r] = ((l >> 4) + 4 * r == (l & 15)) ? 1.0 : 0.0;
+      factor16_wave(accA[KB], W, l, ok);
 #pragma unroll
       for (int TJ = 0; TJ < 4; ++TJ) {
-        bL[TJ] = panel(16 * TJ + li);
-        double s = 0.0;
+        v4d z = v4d{0.0, 0.0, 0.0, 0.0};
+        if (TJ > KB) {
+          accA[TJ] = mfma_tn(W, accA[TJ], z, false);
 #pragma unroll
-        for (int m = 0; m < 4; ++m) s += M[lk][m] * X[m * T + ACC_COL(TJ, l)];
-        xf[TJ] = s;
-      }
-      // only active 16x16 tiles: rows > 4kb+3 (w >= KB); A lower (KB <= TJ <= w),
-      // inverse columns <= 4kb+3 (TJ <= KB)
-      if (w >= KB) {
+          for (int r = 0; r < 4; ++r) xb[TJ * 256 + r * 64 + l] = accA[TJ][r];
+        } else {
+          accX[TJ] = mfma_tn(W, accX[TJ], z, false);
 #pragma unroll
-        for (int TJ = 0; TJ < 4; ++TJ) {
-          if (TJ >= KB && TJ <= w) accA[TJ] = __builtin_amdgcn_mfma_f64_16x16x4f64(aL, bL[TJ], accA[TJ], 0, 0, 0);
-          if (TJ <= KB) accX[TJ] = __builtin_amdgcn_mfma_f64_16x16x4f64(aL, xf[TJ], accX[TJ], 0, 0, 0);
+          for (int r = 0; r < 4; ++r) xb[TJ * 256 + r * 64 + l] = accX[TJ][r];
         }
       }
-      if (w == KB) {
+    }
+    __syncthreads();
+    if (w > KB) {
+      v4d Uv;
 #pragma unroll
-        for (int TJ = 0; TJ < 4; ++TJ) accX[TJ][kk] = xf[TJ];
+      for (int r = 0; r < 4; ++r) Uv[r] = xb[w * 256 + r * 64 + l];
+#pragma unroll
+      for (int TJ = 0; TJ < 4; ++TJ) {
+        if (TJ < w && TJ > KB) continue;
+        v4d Z;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Z[r] = xb[TJ * 256 + r * 64 + l];
+        if (TJ >= w) accA[TJ] = mfma_tn(Uv, Z, accA[TJ], true);
+        else accX[TJ] = mfma_tn(Uv, Z, accX[TJ], true);
       }
     }
   }
@@ -226,8 +246,6 @@ __global__ __launch_bounds__(256) void k_tasks(TileDev b, const TileTask* __rest
   __shared__ double Qs[T * LD];   // pair operand A
   __shared__ double Rs[T * LD];   // pair operand B
   __shared__ double As[T * LD];   // own tile (i, k)
-  __shared__ double Pcol[2 * T * 4];
-  __shared__ double Xrow[2 * 4 * T];
   __shared__ double vv[T];
   const TileTask tk = tasks[blockIdx.x];
   const int tid = threadIdx.x;
@@ -268,7 +286,9 @@ __global__ __launch_bounds__(256) void k_tasks(TileDev b, const TileTask* __rest
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
       const int row = ACC_ROW(w, l, rr), col = ACC_COL(TJ, l);
-      accA[TJ][rr] = diag[row * T + col];
+      // the slot holds the lower triangle; the factorisation reads the
+      // upper blocks (w, TJ >= w), so mirror it
+      accA[TJ][rr] = row >= col ? diag[row * T + col] : diag[col * T + row];
       accX[TJ][rr] = row == col ? 1.0 : 0.0;
     }
   const int li = l & 15, lk = l >> 4;
@@ -286,7 +306,7 @@ __global__ __launch_bounds__(256) void k_tasks(TileDev b, const TileTask* __rest
     }
   }
   __syncthreads();
-  const bool ok = factor_tile_mfma(accA, accX, w, l, Pcol, Xrow);
+  const bool ok = factor_tile_blk(accA, accX, w, l, Rs);
   if (!ok && !own && tid == 0) *fail = 1;
   // L_kk^-1 -> Ps (full square; upper part is exactly zero)
 #pragma unroll
@@ -344,30 +364,49 @@ __global__ __launch_bounds__(256) void k_tasks(TileDev b, const TileTask* __rest
 }
 
 // one level of the backward substitution: a workgroup per column tile k,
-// x_k = L_kk^-T (y_k - sum_i L(i,k)^T x_i)
-__global__ __launch_bounds__(256) void k_back(TileDev b, const BackTask* __restrict__ tasks,
-                                              const int32_t* __restrict__ ent, const double* __restrict__ Linv,
-                                              const double* __restrict__ y, double* __restrict__ x) {
-  constexpr int NP = 4;
+// x_k = L_kk^-T (y_k - sum_i L(i,k)^T x_i). The (entry, row) pairs of the
+// column are flattened over 16 row groups of 64 lanes (lane = column of
+// the tile), four independent loads in flight per lane.
+constexpr int kBackThreads = 1024;
+__global__ __launch_bounds__(kBackThreads) void k_back(TileDev b, const BackTask* __restrict__ tasks,
+                                                       const int32_t* __restrict__ ent,
+                                                       const double* __restrict__ Linv,
+                                                       const double* __restrict__ y, double* __restrict__ x) {
+  constexpr int NP = kBackThreads / T;
   __shared__ double part[NP][T];
   __shared__ double rv[T];
+  __shared__ const double* Lp[64];
+  __shared__ const double* Xp[64];
   const BackTask tk = tasks[blockIdx.x];
   const int tid = threadIdx.x, c = tid & (T - 1), q = tid >> 6;
   double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-  for (int e = tk.beg; e < tk.end; ++e) {
-    const double* L = slot_ptr(b, ent[2 * e]);
-    const double* xi = x + static_cast<int64_t>(ent[2 * e + 1]) * T;
-    // rows m = q, q+4, ...: 4 independent accumulators
-    for (int m = q; m < T; m += 4 * NP) {
-      s0 += L[m * T + c] * xi[m];
-      s1 += L[(m + NP) * T + c] * xi[m + NP];
-      s2 += L[(m + 2 * NP) * T + c] * xi[m + 2 * NP];
-      s3 += L[(m + 3 * NP) * T + c] * xi[m + 3 * NP];
+  for (int e0 = tk.beg; e0 < tk.end; e0 += 64) {
+    const int ne = min(64, tk.end - e0);
+    __syncthreads();
+    if (tid < ne) {
+      Lp[tid] = slot_ptr(b, ent[2 * (e0 + tid)]);
+      Xp[tid] = x + static_cast<int64_t>(ent[2 * (e0 + tid) + 1]) * T;
     }
+    __syncthreads();
+    const int nrow = ne * T;
+    int idx = q;
+    for (; idx + 3 * NP < nrow; idx += 4 * NP) {
+      const int i0 = idx, i1 = idx + NP, i2 = idx + 2 * NP, i3 = idx + 3 * NP;
+      s0 += Lp[i0 >> 6][(i0 & 63) * T + c] * Xp[i0 >> 6][i0 & 63];
+      s1 += Lp[i1 >> 6][(i1 & 63) * T + c] * Xp[i1 >> 6][i1 & 63];
+      s2 += Lp[i2 >> 6][(i2 & 63) * T + c] * Xp[i2 >> 6][i2 & 63];
+      s3 += Lp[i3 >> 6][(i3 & 63) * T + c] * Xp[i3 >> 6][i3 & 63];
+    }
+    for (; idx < nrow; idx += NP) s0 += Lp[idx >> 6][(idx & 63) * T + c] * Xp[idx >> 6][idx & 63];
   }
   part[q][c] = (s0 + s1) + (s2 + s3);
   __syncthreads();
-  if (tid < T) rv[tid] = y[static_cast<int64_t>(tk.k) * T + tid] - ((part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]));
+  if (tid < T) {
+    double t = 0.0;
+#pragma unroll
+    for (int k = 0; k < NP; ++k) t += part[k][tid];
+    rv[tid] = y[static_cast<int64_t>(tk.k) * T + tid] - t;
+  }
   __syncthreads();
   // x_k[c] = sum_{m >= c} Linv[m][c] rv[m]
   const double* Li = Linv + static_cast<int64_t>(tk.k) * T * T;
@@ -376,8 +415,12 @@ __global__ __launch_bounds__(256) void k_back(TileDev b, const BackTask* __restr
     if (m >= c) t += Li[m * T + c] * rv[m];
   part[q][c] = t;
   __syncthreads();
-  if (tid < T)
-    x[static_cast<int64_t>(tk.k) * T + tid] = (part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]);
+  if (tid < T) {
+    double u = 0.0;
+#pragma unroll
+    for (int k = 0; k < NP; ++k) u += part[k][tid];
+    x[static_cast<int64_t>(tk.k) * T + tid] = u;
+  }
 }
 
 }  // namespace
@@ -391,7 +434,7 @@ void launch_tile_cholesky_solve(const TileDev& b, const TileSchedDev& sd, const 
   }
   for (size_t lv = 0; lv + 1 < blevel.size(); ++lv) {
     const int n = blevel[lv + 1] - blevel[lv];
-    if (n > 0) k_back<<<n, 256, 0, s>>>(b, sd.btask + blevel[lv], sd.bent, Linv, y, x);
+    if (n > 0) k_back<<<n, kBackThreads, 0, s>>>(b, sd.btask + blevel[lv], sd.bent, Linv, y, x);
   }
 }
 
