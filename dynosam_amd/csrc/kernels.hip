@@ -439,46 +439,6 @@ __global__ __launch_bounds__(kBlock) void k_gather_thread(const int64_t* __restr
   for (int j = 0; j < R * CC; ++j) o[j] = acc[j];
 }
 
-// wave-per-target gather of sum sign * A^T B (R x CC) with fixed butterfly
-template <int R, int CC>
-__device__ __forceinline__ void wave_gather(const int64_t* __restrict__ start, const GEntry* __restrict__ ent, int t,
-                                            const double* __restrict__ arena, double* acc) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int j = 0; j < R * CC; ++j) acc[j] = 0.0;
-  const int64_t e1 = start[t + 1];
-  for (int64_t e = start[t] + lane; e < e1; e += 64) {
-    const GEntry g = ent[e];
-    const double* A = arena + g.a;
-    const double* B = arena + g.b;
-    for (int k = 0; k < g.k; ++k) {
-      double a[R], b[CC];
-#pragma unroll
-      for (int r = 0; r < R; ++r) a[r] = A[k * R + r];
-#pragma unroll
-      for (int c = 0; c < CC; ++c) b[c] = B[k * CC + c];
-      if (g.sign > 0) {
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-#pragma unroll
-          for (int c = 0; c < CC; ++c) acc[r * CC + c] += a[r] * b[c];
-      } else {
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-#pragma unroll
-          for (int c = 0; c < CC; ++c) acc[r * CC + c] -= a[r] * b[c];
-      }
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < R * CC; ++j) {
-    double v = acc[j];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    acc[j] = v;
-  }
-}
-
 // element (row, col), row >= col, of the reduced matrix -> its stored tile
 // element (the tile is transposed when col's tile is eliminated later)
 __device__ __forceinline__ int64_t tile_index(const TileDev& b, int row, int col) {
@@ -495,42 +455,114 @@ __device__ __forceinline__ int64_t tile_index(const TileDev& b, int row, int col
   return static_cast<int64_t>(b.row_slot[lo]) * kTile * kTile + ri * kTile + cj;
 }
 
+// ---- gathers of the reduced system --------------------------------------
+// Lanes of a group accumulate the entries q, q+G, ... of one target; the
+// sums are then reduce-scattered (each xor step halves the vector a lane
+// holds), so the reduction costs ~N shuffles instead of N log2(G). The
+// gathers are bound by memory-level parallelism on the dependent entry
+// loads, so targets get many lanes.
+template <int N, int M>
+__device__ __forceinline__ void rs_step(const double (&in)[N], double (&out)[(N + 1) / 2], bool bit) {
+  constexpr int H = (N + 1) / 2;
+#pragma unroll
+  for (int i = 0; i < H; ++i) {
+    const double lo = in[i];
+    const double hi = (i + H < N) ? in[i + H] : 0.0;
+    out[i] = (bit ? hi : lo) + __shfl_xor(bit ? lo : hi, M);
+  }
+}
+
+// after the six halvings (xor 32, 16, 8, 4, 2, 1) of an N0-vector, the
+// value left in lane q is element rs_index<N0>(q) of the sum (-1: padding).
+// Walking back from the last step: a set bit means the lane kept the upper
+// half, which starts at the size left after that step.
+template <int N0>
+__device__ __forceinline__ int rs_index(int q) {
+  constexpr int S1 = (N0 + 1) / 2, S2 = (S1 + 1) / 2, S3 = (S2 + 1) / 2, S4 = (S3 + 1) / 2, S5 = (S4 + 1) / 2,
+                S6 = (S5 + 1) / 2;
+  static_assert(S6 == 1, "six halvings must leave one value per lane");
+  int idx = (q & 1) ? S6 : 0;
+  if (idx >= S5) return -1;
+  idx += (q & 2) ? S5 : 0;
+  if (idx >= S4) return -1;
+  idx += (q & 4) ? S4 : 0;
+  if (idx >= S3) return -1;
+  idx += (q & 8) ? S3 : 0;
+  if (idx >= S2) return -1;
+  idx += (q & 16) ? S2 : 0;
+  if (idx >= S1) return -1;
+  idx += (q & 32) ? S1 : 0;
+  return idx < N0 ? idx : -1;
+}
+
+template <int R, int CC, int G>
+__device__ __forceinline__ void group_accumulate(const int64_t* __restrict__ start, const GEntry* __restrict__ ent,
+                                                 int t, int q, const double* __restrict__ arena,
+                                                 double (&acc)[R * CC]) {
+#pragma unroll
+  for (int j = 0; j < R * CC; ++j) acc[j] = 0.0;
+  const int64_t e1 = start[t + 1];
+  for (int64_t e = start[t] + q; e < e1; e += G) {
+    const GEntry g = ent[e];
+    const double* A = arena + g.a;
+    const double* B = arena + g.b;
+    const double sg = static_cast<double>(g.sign);
+    for (int k = 0; k < g.k; ++k) {
+      double a[R], b[CC];
+#pragma unroll
+      for (int r = 0; r < R; ++r) a[r] = sg * A[k * R + r];
+#pragma unroll
+      for (int c = 0; c < CC; ++c) b[c] = B[k * CC + c];
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int c = 0; c < CC; ++c) acc[r * CC + c] += a[r] * b[c];
+    }
+  }
+}
+
+// a wave per 6x6 target
 __global__ __launch_bounds__(kBlock) void k_gather_band(const int64_t* __restrict__ start,
                                                         const GEntry* __restrict__ ent, int nt,
                                                         const double* __restrict__ arena,
                                                         const int32_t* __restrict__ tA,
                                                         const int32_t* __restrict__ tB, TileDev b, double lambda) {
   const int t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int q = threadIdx.x & 63;
   if (t >= nt) return;
-  double acc[36];
-  wave_gather<6, 6>(start, ent, t, arena, acc);
-  const int lane = threadIdx.x & 63;
-  if (lane >= 36) return;
-  double v = 0.0;
-#pragma unroll
-  for (int j = 0; j < 36; ++j)
-    if (j == lane) v = acc[j];
+  double acc[36], a18[18], a9[9], a5[5], a3[3], a2[2], a1[1];
+  group_accumulate<6, 6, 64>(start, ent, t, q, arena, acc);
+  rs_step<36, 32>(acc, a18, q & 32);
+  rs_step<18, 16>(a18, a9, q & 16);
+  rs_step<9, 8>(a9, a5, q & 8);
+  rs_step<5, 4>(a5, a3, q & 4);
+  rs_step<3, 2>(a3, a2, q & 2);
+  rs_step<2, 1>(a2, a1, q & 1);
+  const int idx = rs_index<36>(q);
+  if (idx < 0) return;
   const int A = tA[t], B = tB[t];
-  const int r = lane / 6, c = lane % 6;
+  const int r = idx / 6, c = idx % 6;
   if (A == B && r < c) return;
-  if (A == B && r == c) v += lambda;
-  b.slots[tile_index(b, 6 * A + r, 6 * B + c)] = v;
+  b.slots[tile_index(b, 6 * A + r, 6 * B + c)] = a1[0] + (A == B && r == c ? lambda : 0.0);
 }
 
+// a wave per pose gradient
 __global__ __launch_bounds__(kBlock) void k_gather_grad(const int64_t* __restrict__ start,
                                                         const GEntry* __restrict__ ent, int nt,
                                                         const double* __restrict__ arena, double* __restrict__ gred) {
   const int t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int q = threadIdx.x & 63;
   if (t >= nt) return;
-  double acc[6];
-  wave_gather<6, 1>(start, ent, t, arena, acc);
-  const int lane = threadIdx.x & 63;
-  if (lane >= 6) return;
-  double v = 0.0;
-#pragma unroll
-  for (int j = 0; j < 6; ++j)
-    if (j == lane) v = acc[j];
-  gred[6 * t + lane] = v;
+  double acc[6], a3[3], a2[2], a1[1], b1[1], c1[1], d1[1];
+  group_accumulate<6, 1, 64>(start, ent, t, q, arena, acc);
+  rs_step<6, 32>(acc, a3, q & 32);
+  rs_step<3, 16>(a3, a2, q & 16);
+  rs_step<2, 8>(a2, a1, q & 8);
+  rs_step<1, 4>(a1, b1, q & 4);
+  rs_step<1, 2>(b1, c1, q & 2);
+  rs_step<1, 1>(c1, d1, q & 1);
+  const int idx = rs_index<6>(q);
+  if (idx >= 0) gred[6 * t + idx] = d1[0];
 }
 
 // ---------------------------------------------------------------- chains

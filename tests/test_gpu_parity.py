@@ -90,6 +90,30 @@ def test_free_running_optimize(gpu_available, name, kw):
         assert a["lam"] == b["lam"]
 
 
+def test_cliques_fixture_matches_golden(gpu_available):
+    """The reference's exact-input testCliques graph (test_rgbd_backend.cc:272-486),
+    read from the graph-file fixture; GPU run vs the committed oracle trace."""
+    import json
+    import os
+    from dynosam_amd import graphio
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    gold = json.load(open(os.path.join(here, "lm_cliques.json")))
+    g, v = graphio.read(os.path.join(here, "cliques.graph"))
+    s = Solver(0)
+    s.set_graph(g)
+    s.set_values(v)
+    sg = s.optimize()
+    assert (sg.iterations, sg.inner_iterations) == (gold["iterations"], gold["inner_iterations"])
+    assert sg.final_error == pytest.approx(gold["final_error"], rel=1e-9)
+    for a, b in zip(s.trace(), gold["trace"]):
+        assert (a["lam"], a["accepted"]) == (b["lam"], b["accepted"])
+    out = s.values_data()
+    off = v._offsets()
+    for i, k in enumerate(v.keys):
+        ref = np.asarray(gold["final_values"][str(int(k))])
+        assert rel(out[off[i]:off[i + 1]], ref) < PER_ITER_TOL
+
+
 def test_llworld_formulation(gpu_available):
     g, v, _, s = make("T2", formulation=1)
     sg = s.optimize()
