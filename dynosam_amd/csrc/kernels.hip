@@ -401,44 +401,6 @@ __global__ __launch_bounds__(kBlock) void k_reduce(const double* __restrict__ pa
 }
 
 // ---------------------------------------------------------------- gathers
-template <int R, int CC>
-__global__ __launch_bounds__(kBlock) void k_gather_thread(const int64_t* __restrict__ start,
-                                                          const GEntry* __restrict__ ent, int nt,
-                                                          const double* __restrict__ arena,
-                                                          double* __restrict__ dst) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nt) return;
-  double acc[R * CC];
-#pragma unroll
-  for (int j = 0; j < R * CC; ++j) acc[j] = 0.0;
-  for (int64_t e = start[t]; e < start[t + 1]; ++e) {
-    const GEntry g = ent[e];
-    const double* A = arena + g.a;
-    const double* B = arena + g.b;
-    for (int k = 0; k < g.k; ++k) {
-      double a[R], b[CC];
-#pragma unroll
-      for (int r = 0; r < R; ++r) a[r] = A[k * R + r];
-#pragma unroll
-      for (int c = 0; c < CC; ++c) b[c] = B[k * CC + c];
-      if (g.sign > 0) {
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-#pragma unroll
-          for (int c = 0; c < CC; ++c) acc[r * CC + c] += a[r] * b[c];
-      } else {
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-#pragma unroll
-          for (int c = 0; c < CC; ++c) acc[r * CC + c] -= a[r] * b[c];
-      }
-    }
-  }
-  double* o = dst + static_cast<int64_t>(t) * R * CC;
-#pragma unroll
-  for (int j = 0; j < R * CC; ++j) o[j] = acc[j];
-}
-
 // element (row, col), row >= col, of the reduced matrix -> its stored tile
 // element (the tile is transposed when col's tile is eliminated later)
 __device__ __forceinline__ int64_t tile_index(const TileDev& b, int row, int col) {
@@ -461,6 +423,17 @@ __device__ __forceinline__ int64_t tile_index(const TileDev& b, int row, int col
 // holds), so the reduction costs ~N shuffles instead of N log2(G). The
 // gathers are bound by memory-level parallelism on the dependent entry
 // loads, so targets get many lanes.
+// XCD-aware block order: blocks b and b + 8 share an XCD (observed
+// round-robin dispatch, MI355X_MICROARCH.md §Workgroup dispatch), so give
+// each residue class b % 8 one contiguous chunk of the logical range.
+// Targets that are close in the logical order share operands, and those
+// re-reads then hit one XCD's L2. Bijective on [0, nb); speed only.
+__device__ __forceinline__ int xcd_block(int b, int nb) {
+  const int per = (nb + 7) / 8, full = (nb % 8 == 0) ? 8 : nb % 8;
+  const int x = b % 8, i = b / 8;
+  return x < full ? x * per + i : full * per + (x - full) * (per - 1) + i;
+}
+
 template <int N, int M>
 __device__ __forceinline__ void rs_step(const double (&in)[N], double (&out)[(N + 1) / 2], bool bit) {
   constexpr int H = (N + 1) / 2;
@@ -495,30 +468,61 @@ __device__ __forceinline__ int rs_index(int q) {
   return idx < N0 ? idx : -1;
 }
 
-template <int R, int CC, int G>
+// Entry dimensions k are 3 or 6 (the row counts of the factor and point
+// blocks), so each entry is consumed in slices of S rows (S divides 3) whose
+// operand loads are all issued before the FMAs; the next entry's
+// descriptor is fetched while the current one is computed. Wide outputs use
+// S = 1 to keep registers (and occupancy) for the 36 accumulators.
+template <int R, int CC, int G, int S = 3>
 __device__ __forceinline__ void group_accumulate(const int64_t* __restrict__ start, const GEntry* __restrict__ ent,
                                                  int t, int q, const double* __restrict__ arena,
                                                  double (&acc)[R * CC]) {
 #pragma unroll
   for (int j = 0; j < R * CC; ++j) acc[j] = 0.0;
   const int64_t e1 = start[t + 1];
-  for (int64_t e = start[t] + q; e < e1; e += G) {
-    const GEntry g = ent[e];
+  int64_t e = start[t] + q;
+  GEntry g = e < e1 ? ent[e] : GEntry{0, 0, 0, 0};
+  while (e < e1) {
+    const int64_t en = e + G;
+    const GEntry gn = en < e1 ? ent[en] : GEntry{0, 0, 0, 0};
     const double* A = arena + g.a;
     const double* B = arena + g.b;
     const double sg = static_cast<double>(g.sign);
-    for (int k = 0; k < g.k; ++k) {
-      double a[R], b[CC];
+    for (int k0 = 0; k0 < g.k; k0 += S) {
+      double a[S][R], b[S][CC];
 #pragma unroll
-      for (int r = 0; r < R; ++r) a[r] = sg * A[k * R + r];
+      for (int k = 0; k < S; ++k) {
 #pragma unroll
-      for (int c = 0; c < CC; ++c) b[c] = B[k * CC + c];
+        for (int r = 0; r < R; ++r) a[k][r] = A[(k0 + k) * R + r];
 #pragma unroll
-      for (int r = 0; r < R; ++r)
+        for (int c = 0; c < CC; ++c) b[k][c] = B[(k0 + k) * CC + c];
+      }
 #pragma unroll
-        for (int c = 0; c < CC; ++c) acc[r * CC + c] += a[r] * b[c];
+      for (int k = 0; k < S; ++k)
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const double ar = sg * a[k][r];
+#pragma unroll
+          for (int c = 0; c < CC; ++c) acc[r * CC + c] += ar * b[k][c];
+        }
     }
+    e = en;
+    g = gn;
   }
+}
+
+template <int R, int CC>
+__global__ __launch_bounds__(kBlock) void k_gather_thread(const int64_t* __restrict__ start,
+                                                          const GEntry* __restrict__ ent, int nt,
+                                                          const double* __restrict__ arena,
+                                                          double* __restrict__ dst) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nt) return;
+  double acc[R * CC];
+  group_accumulate<R, CC, 1>(start, ent, t, 0, arena, acc);
+  double* o = dst + static_cast<int64_t>(t) * R * CC;
+#pragma unroll
+  for (int j = 0; j < R * CC; ++j) o[j] = acc[j];
 }
 
 // a wave per 6x6 target
@@ -527,11 +531,11 @@ __global__ __launch_bounds__(kBlock) void k_gather_band(const int64_t* __restric
                                                         const double* __restrict__ arena,
                                                         const int32_t* __restrict__ tA,
                                                         const int32_t* __restrict__ tB, TileDev b, double lambda) {
-  const int t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int t = (xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x) >> 6;
   const int q = threadIdx.x & 63;
   if (t >= nt) return;
   double acc[36], a18[18], a9[9], a5[5], a3[3], a2[2], a1[1];
-  group_accumulate<6, 6, 64>(start, ent, t, q, arena, acc);
+  group_accumulate<6, 6, 64, 1>(start, ent, t, q, arena, acc);
   rs_step<36, 32>(acc, a18, q & 32);
   rs_step<18, 16>(a18, a9, q & 16);
   rs_step<9, 8>(a9, a5, q & 8);
@@ -550,7 +554,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_band(const int64_t* __restric
 __global__ __launch_bounds__(kBlock) void k_gather_grad(const int64_t* __restrict__ start,
                                                         const GEntry* __restrict__ ent, int nt,
                                                         const double* __restrict__ arena, double* __restrict__ gred) {
-  const int t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int t = (xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x) >> 6;
   const int q = threadIdx.x & 63;
   if (t >= nt) return;
   double acc[6], a3[3], a2[2], a1[1], b1[1], c1[1], d1[1];
