@@ -29,6 +29,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector/matrix dense peak (spec)
+PROFILE_ROUND = "r01"       # profiles/<round>/ holding this round's rocprof summaries
 
 
 def parse():
@@ -147,31 +148,46 @@ def main():
     dominant = max(phases, key=phases.get)
     nsolve = max(st["n_solves"], 1)
     nlin = max(st["n_linearize"], 1)
-    if dominant == "cholesky":
-        per = st["ms_cholesky"] / nsolve
-        achieved = st["chol_flops"] / (per * 1e-3) / 1e12
-        roof = {"kernel": f"tile_cholesky (one factorisation + solve = {st['chol_levels']} k_tasks levels + "
-                          f"{st['back_levels']} k_back levels; nested-dissection leaf {st['nd_leaf']} tiles)",
-                "bound": "mfma",
-                "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
-                "algorithmic": f"{st['chol_flops']:.3e} envelope-Cholesky flops per factorisation "
-                               f"(tile schedule issues {st['chol_tile_flops']:.3e} incl. fill)",
-                "ms_per_launch": per}
-    elif dominant == "linearize":
-        per = st["ms_linearize"] / nlin
-        achieved = st["lin_bytes"] / (per * 1e-3) / 1e9
-        roof = {"kernel": "linearize (k_linearize<T> + point-block gathers)", "bound": "hbm",
-                "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None, "algorithmic": f"{st['lin_bytes']:.3e} bytes per linearisation",
-                "ms_per_launch": per}
-    else:
+    def phase_roofline(phase):
+        if phase == "cholesky":
+            per = st["ms_cholesky"] / nsolve
+            achieved = st["chol_flops"] / (per * 1e-3) / 1e12
+            return {"kernel": f"tile_cholesky (one factorisation + solve = {st['chol_levels']} k_tasks levels + "
+                              f"{st['back_levels']} k_back levels; nested-dissection leaf {st['nd_leaf']} tiles)",
+                    "bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
+                    "algorithmic": f"{st['chol_flops']:.3e} envelope-Cholesky flops per factorisation "
+                                   f"(tile schedule issues {st['chol_tile_flops']:.3e} incl. fill)",
+                    "ms_per_launch": per}
+        if phase == "linearize":
+            per = st["ms_linearize"] / nlin
+            achieved = st["lin_bytes"] / (per * 1e-3) / 1e9
+            return {"kernel": "linearize (k_linearize<T> per factor type + point-block gathers)", "bound": "hbm",
+                    "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                    "traffic": None, "algorithmic": f"{st['lin_bytes']:.3e} bytes per linearisation",
+                    "ms_per_launch": per}
         per = st["ms_assembly"] / nsolve
         achieved = st["assembly_bytes"] / (per * 1e-3) / 1e9
-        roof = {"kernel": f"{dominant} (reduced assembly bytes model)", "bound": "hbm",
+        return {"kernel": "assembly (k_gather_band + k_gather_grad: reduced system)", "bound": "hbm",
                 "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                 "traffic": None, "algorithmic": f"{st['assembly_bytes']:.3e} bytes per assembly",
                 "ms_per_launch": per}
+
+    roof = phase_roofline(dominant if dominant in ("cholesky", "linearize") else "assembly")
+    # HBM traffic from the committed rocprofv3 PMC passes of this command
+    # (tools/pmc_pass.sh + tools/pmc_traffic.py; gfx950 FETCH_SIZE x2)
+    pmc = os.path.join(ROOT, "profiles", PROFILE_ROUND, f"pmc_traffic_{args.config}.json")
+    if os.path.exists(pmc):
+        pm = json.load(open(pmc))
+        if roof["bound"] == "mfma" and pm.get("traffic_bytes_per_factorisation"):
+            roof["traffic"] = pm["traffic_bytes_per_factorisation"]
+            roof["traffic_unit"] = "bytes per factorisation"
+        elif roof["kernel"].startswith("assembly"):
+            kk = pm["kernels"]
+            roof["traffic"] = sum(kk[k]["traffic_bytes_per_launch"] for k in ("k_gather_band", "k_gather_grad") if k in kk)
+            roof["traffic_unit"] = "bytes per assembly"
+        roof["traffic_source"] = os.path.relpath(pmc, ROOT)
+    secondary = {ph: phase_roofline(ph) for ph in ("cholesky", "linearize", "assembly")}
 
     out = {
         "metric": "LM iterations/sec + ms/iter, full-batch dynamic factor graph",
@@ -200,6 +216,8 @@ def main():
         },
         "phases_ms_per_optimize": {k: round(v, 4) for k, v in phases.items()},
         "roofline": roof,
+        "phase_rooflines": {k: {f: v[f] for f in ("bound", "achieved", "unit", "frac", "ms_per_launch")}
+                            for k, v in secondary.items()},
     }
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(graph, values, args.cpu_seconds)

@@ -547,7 +547,16 @@ __global__ __launch_bounds__(kBlock) void k_gather_band(const int64_t* __restric
   const int A = tA[t], B = tB[t];
   const int r = idx / 6, c = idx % 6;
   if (A == B && r < c) return;
-  b.slots[tile_index(b, 6 * A + r, 6 * B + c)] = a1[0] + (A == B && r == c ? lambda : 0.0);
+  const int row = 6 * A + r, col = 6 * B + c;
+  const double val = a1[0] + (A == B && r == c ? lambda : 0.0);
+  const int64_t at = tile_index(b, row, col);
+  b.slots[at] = val;
+  // diagonal tiles are stored full (symmetric), so the factorisation reads
+  // them with plain coalesced loads
+  if (row / kTile == col / kTile && row != col) {
+    const int64_t base = at - (row % kTile) * kTile - (col % kTile);
+    b.slots[base + (col % kTile) * kTile + (row % kTile)] = val;
+  }
 }
 
 // a wave per pose gradient

@@ -170,11 +170,22 @@ __device__ __forceinline__ v4d mfma_tn(const v4d& Y, const v4d& Z, v4d acc, bool
 //   waves v > KB: A[v][TJ] -= U[KB][v]^T U[KB][TJ] (TJ >= v),
 //                 X[v][TJ] -= U[KB][v]^T X[KB][TJ] (TJ <= KB)
 // xch: 2 x 4 blocks x 256 doubles of LDS.
-__device__ bool factor_tile_blk(v4d (&accA)[4], v4d (&accX)[4], int w, int l, double* xch) {
+// Hooks let the caller use otherwise idle waves: idle0() runs on waves 1-3
+// while wave 0 factors block 0 (before the first barrier), idle1() on wave 0
+// during step 1.
+struct NoHook {
+  __device__ void operator()() const {}
+};
+
+template <class Idle0 = NoHook, class Idle1 = NoHook>
+__device__ bool factor_tile_blk(v4d (&accA)[4], v4d (&accX)[4], int w, int l, double* xch, Idle0&& idle0 = Idle0(),
+                                Idle1&& idle1 = Idle1()) {
   bool ok = true;
 #pragma unroll
   for (int KB = 0; KB < 4; ++KB) {
     double* xb = xch + (KB & 1) * 4 * 256;
+    if (KB == 0 && w != 0) idle0();
+    if (KB == 1 && w == 0) idle1();
     if (w == KB) {
       v4d W = v4d{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -238,6 +249,54 @@ __device__ __forceinline__ void sum_pairs(const TileDev& b, const int32_t* __res
   }
 }
 
+// Issue the loads of up to four 64x64 tiles into LDS before any of the
+// stores, so their latencies overlap (one round trip instead of four).
+__device__ __forceinline__ void load_tiles_lds(const double* const (&src)[4], double* const (&dst)[4], int n,
+                                               int tid) {
+  double2 v[4][8];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+    if (t < n) {
+      const double2* s2 = reinterpret_cast<const double2*>(src[t]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[t][i] = s2[tid + 256 * i];
+    }
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+    if (t < n) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int e = tid + 256 * i, rr = (2 * e) / T, cc = (2 * e) % T;
+        dst[t][rr * LD + cc] = v[t][i].x;
+        dst[t][rr * LD + cc + 1] = v[t][i].y;
+      }
+    }
+}
+
+// A_kk -= L(k,c) L(k,c)^T on this wave's upper blocks (w, TJ >= w), K = 64
+__device__ __forceinline__ void diag_pending(v4d (&accA)[4], const double* Ps, int w, int l) {
+  const int li = l & 15, lk = l >> 4;
+#pragma unroll 4
+  for (int k0 = 0; k0 < T; k0 += 4) {
+    const double a = -Ps[(16 * w + li) * LD + k0 + lk];
+#pragma unroll
+    for (int TJ = 0; TJ < 4; ++TJ)
+      if (TJ >= w) accA[TJ] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Ps[(16 * TJ + li) * LD + k0 + lk], accA[TJ], 0, 0, 0);
+  }
+}
+
+// As -= Qs Rs^T on this wave's 32x32 quadrant
+__device__ __forceinline__ void own_pending_quadrant(double* As, const double* Qs, const double* Rs, int w, int l) {
+  v4d acc[2][2];
+  mfma_abt(Qs, Rs, w, l, acc);
+#pragma unroll
+  for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) As[MFMA_ROW(w, l, ti, rr) * LD + MFMA_COL(w, l, tj)] -= acc[ti][tj][rr];
+}
+
 __global__ __launch_bounds__(256) void k_tasks(TileDev b, const TileTask* __restrict__ tasks,
                                                const int32_t* __restrict__ pairs, double* __restrict__ Linv,
                                                const double* __restrict__ r, double* __restrict__ contrib,
@@ -246,39 +305,40 @@ __global__ __launch_bounds__(256) void k_tasks(TileDev b, const TileTask* __rest
   __shared__ double Qs[T * LD];   // pair operand A
   __shared__ double Rs[T * LD];   // pair operand B
   __shared__ double As[T * LD];   // own tile (i, k)
+  __shared__ double Xch[2 * 4 * 256];
+  __shared__ double rpart[4][T];
   __shared__ double vv[T];
   const TileTask tk = tasks[blockIdx.x];
   const int tid = threadIdx.x;
   const int w = tid >> 6, l = tid & 63;
   if (tk.kind == 1) {
-    // ---- update: dst -= sum A B^T
-    v4d acc[2][2];
-    sum_pairs(b, pairs, tk.po_beg, tk.po_end, Qs, Rs, tid, w, l, acc);
+    // ---- update: dst -= sum A B^T (destination prefetched under the GEMM)
     double* dst = slot_ptr(b, tk.dst);
+    double old[2][2][4];
 #pragma unroll
     for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
       for (int tj = 0; tj < 2; ++tj)
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr) dst[MFMA_ROW(w, l, ti, rr) * T + MFMA_COL(w, l, tj)] -= acc[ti][tj][rr];
+        for (int rr = 0; rr < 4; ++rr) old[ti][tj][rr] = dst[MFMA_ROW(w, l, ti, rr) * T + MFMA_COL(w, l, tj)];
+    v4d acc[2][2];
+    sum_pairs(b, pairs, tk.po_beg, tk.po_end, Qs, Rs, tid, w, l, acc);
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+          dst[MFMA_ROW(w, l, ti, rr) * T + MFMA_COL(w, l, tj)] = old[ti][tj][rr] - acc[ti][tj][rr];
     return;
   }
   // ---- panel
   const bool own = tk.i != tk.k;
-  if (own) {
-    // A(i,k) -= sum L(i,c) L(k,c)^T  (pending contributions)
-    load_tile_lds(slot_ptr(b, tk.dst), As, tid, 256);
-    if (tk.po_end > tk.po_beg) {
-      v4d acc[2][2];
-      sum_pairs(b, pairs, tk.po_beg, tk.po_end, Qs, Rs, tid, w, l, acc);
-#pragma unroll
-      for (int ti = 0; ti < 2; ++ti)
-#pragma unroll
-        for (int tj = 0; tj < 2; ++tj)
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr) As[MFMA_ROW(w, l, ti, rr) * LD + MFMA_COL(w, l, tj)] -= acc[ti][tj][rr];
-    }
-  }
+  const int npd = tk.pd_end - tk.pd_beg, npo = own ? tk.po_end - tk.po_beg : 0;
+  const bool fast = npd <= 1 && npo <= 1;
+  // (1) issue everything that is ready at the start of the level together:
+  // the diagonal tile (stored symmetric) into registers, the right-hand side
+  // contributions L(k,c) y_c of eliminated columns, and the operand tiles
   v4d accA[4], accX[4];
   const double* diag = slot_ptr(b, tk.diag);
 #pragma unroll
@@ -286,27 +346,63 @@ __global__ __launch_bounds__(256) void k_tasks(TileDev b, const TileTask* __rest
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
       const int row = ACC_ROW(w, l, rr), col = ACC_COL(TJ, l);
-      // the slot holds the lower triangle; the factorisation reads the
-      // upper blocks (w, TJ >= w), so mirror it
-      accA[TJ][rr] = row >= col ? diag[row * T + col] : diag[col * T + row];
+      accA[TJ][rr] = TJ >= w ? diag[row * T + col] : 0.0;
       accX[TJ][rr] = row == col ? 1.0 : 0.0;
     }
-  const int li = l & 15, lk = l >> 4;
-  for (int e = tk.pd_beg; e < tk.pd_end; ++e) {
-    // A_kk -= L(k,c) L(k,c)^T into the accumulators (K = 64)
-    __syncthreads();
-    load_tile_lds(slot_ptr(b, pairs[2 * e]), Ps, tid, 256);
-    __syncthreads();
-#pragma unroll 4
-    for (int k0 = 0; k0 < T; k0 += 4) {
-      const double a = -Ps[(16 * w + li) * LD + k0 + lk];
+  {
+    double sacc = 0.0;
+    for (int e = b.row_start[tk.k] + w; e < b.row_start[tk.k + 1]; e += 4)
+      if (b.row_col[e] != tk.k) sacc += contrib[static_cast<int64_t>(b.row_slot[e]) * T + l];
+    rpart[w][l] = sacc;
+  }
+  if (fast) {
+    const double* src[4] = {nullptr, nullptr, nullptr, nullptr};
+    double* dst[4] = {nullptr, nullptr, nullptr, nullptr};
+    int n = 0;
+    if (npd) { src[n] = slot_ptr(b, pairs[2 * tk.pd_beg]); dst[n++] = Ps; }
+    if (own) { src[n] = slot_ptr(b, tk.dst); dst[n++] = As; }
+    if (npo) {
+      src[n] = slot_ptr(b, pairs[2 * tk.po_beg]); dst[n++] = Qs;
+      src[n] = slot_ptr(b, pairs[2 * tk.po_beg + 1]); dst[n++] = Rs;
+    }
+    load_tiles_lds(src, dst, n, tid);
+  } else {
+    // several pending pairs (rare): apply them one by one before the factor
+    if (own) {
+      load_tile_lds(slot_ptr(b, tk.dst), As, tid, 256);
+      if (npo) {
+        v4d acc[2][2];
+        sum_pairs(b, pairs, tk.po_beg, tk.po_end, Qs, Rs, tid, w, l, acc);
 #pragma unroll
-      for (int TJ = 0; TJ < 4; ++TJ)
-        accA[TJ] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Ps[(16 * TJ + li) * LD + k0 + lk], accA[TJ], 0, 0, 0);
+        for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+          for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) As[MFMA_ROW(w, l, ti, rr) * LD + MFMA_COL(w, l, tj)] -= acc[ti][tj][rr];
+      }
+    }
+    for (int e = tk.pd_beg; e < tk.pd_end; ++e) {
+      __syncthreads();
+      load_tile_lds(slot_ptr(b, pairs[2 * e]), Ps, tid, 256);
+      __syncthreads();
+      diag_pending(accA, Ps, w, l);
     }
   }
   __syncthreads();
-  const bool ok = factor_tile_blk(accA, accX, w, l, Rs);
+  if (tid < T) vv[tid] = r[static_cast<int64_t>(tk.k) * T + tid] - ((rpart[0][tid] + rpart[1][tid]) + (rpart[2][tid] + rpart[3][tid]));
+  // (2) pending updates: wave 0's diagonal blocks before the factorisation;
+  // waves 1-3 apply theirs, plus their quadrant of the own tile's update,
+  // while wave 0 factors block 0; wave 0 does its quadrant during step 1
+  const bool dp = fast && npd, op = fast && npo;
+  if (dp && w == 0) diag_pending(accA, Ps, w, l);
+  auto idle0 = [&]() {
+    if (dp) diag_pending(accA, Ps, w, l);
+    if (op) own_pending_quadrant(As, Qs, Rs, w, l);
+  };
+  auto idle1 = [&]() {
+    if (op) own_pending_quadrant(As, Qs, Rs, w, l);
+  };
+  const bool ok = factor_tile_blk(accA, accX, w, l, Xch, idle0, idle1);
   if (!ok && !own && tid == 0) *fail = 1;
   // L_kk^-1 -> Ps (full square; upper part is exactly zero)
 #pragma unroll
@@ -319,13 +415,6 @@ __global__ __launch_bounds__(256) void k_tasks(TileDev b, const TileTask* __rest
     for (int TJ = 0; TJ < 4; ++TJ)
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) dst[ACC_ROW(w, l, rr) * T + ACC_COL(TJ, l)] = accX[TJ][rr];
-  }
-  // r_k minus the contributions L(k,c) y_c of the columns already eliminated
-  if (tid < T) {
-    double v = r[static_cast<int64_t>(tk.k) * T + tid];
-    for (int e = b.row_start[tk.k]; e < b.row_start[tk.k + 1]; ++e)
-      if (b.row_col[e] != tk.k) v -= contrib[static_cast<int64_t>(b.row_slot[e]) * T + tid];
-    vv[tid] = v;
   }
   __syncthreads();
   // y_k = L_kk^-1 r_k

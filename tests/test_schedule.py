@@ -7,7 +7,8 @@ numpy: the panel and update semantics of k_tasks / k_back
 csrc/kernels.hip). The replay checks three things:
   * no two tasks of one level conflict (write/write or read/write on a
     tile, a right-hand-side block or an output);
-  * the assembly finds a slot for every nonzero 64x64 block;
+  * the assembly finds a slot for every nonzero 64x64 block (diagonal
+    tiles stored full and symmetric, as k_gather_band writes them);
   * the replayed factor and solve reproduce numpy.linalg.solve on a random
     SPD matrix with the plan's block sparsity.
 This covers frame order (the plain band), forced nested dissection and the
@@ -58,7 +59,7 @@ def assemble(sched, M):
             if not blk.any():
                 continue
             if ti == tj:
-                slots[slot_of(sched, ti, ti)] += np.tril(blk)
+                slots[slot_of(sched, ti, ti)] += blk     # diagonal tiles are stored symmetric
             elif pos[ti] >= pos[tj]:
                 slots[slot_of(sched, ti, tj)] += blk
             else:
@@ -111,8 +112,7 @@ def replay(sched, M, rhs):
             for e in range(pdb, pde):
                 assert pairs[e][0] == pairs[e][1]
             A = slots[diag] - psum(pdb, pde)
-            A = np.tril(A)
-            A = A + np.tril(A, -1).T
+            assert np.allclose(A, A.T, rtol=0, atol=1e-9 * np.abs(A).max())
             Li = np.linalg.inv(np.linalg.cholesky(A))
             rk = r[k] - sum((contrib[rsl[e]] for e in range(rs[k], rs[k + 1]) if rc[e] != k), np.zeros(T))
             yk = Li @ rk
