@@ -53,11 +53,20 @@ struct TileDev {
   const int32_t* row_slot = nullptr;
 };
 
+// parts of the one-launch backward solve: at most this many workgroups, so
+// that all of them are resident at once (256 CUs x several 256-thread,
+// 10 KB-LDS workgroups each)
+constexpr int kBackPersistMax = 1024;
+
 struct TileSchedDev {
   const TileTask* ftask = nullptr;
   const int32_t* pairs = nullptr;
-  const BackTask* btask = nullptr;
+  const BackPart* bpart = nullptr;
   const int32_t* bent = nullptr;
+  double* partials = nullptr;  // n_partials x 64
+  int* arrive = nullptr;       // NT arrival counters (zero between launches)
+  unsigned* done = nullptr;    // NT column-done stamps of the one-launch backward solve
+  unsigned epoch = 0;          // stamp of the current solve (never 0)
 };
 
 // ---- launchers (all asynchronous on `s`) ----
@@ -87,7 +96,7 @@ void launch_tile_pad(const TileDev& b, hipStream_t s);
 // factor the tiles and solve (L L^T) x = r (forward substitution fused
 // into the factorisation: contrib holds L(i,k) y_k per stored tile). Linv
 // receives the NT diagonal inverse tiles, y the forward result. One launch
-// per level of the host schedule (flevel / blevel).
+// per level of the host schedule (flevel / bplevel).
 void launch_tile_cholesky_solve(const TileDev& b, const TileSchedDev& sd, const std::vector<int32_t>& flevel,
                                 const std::vector<int32_t>& blevel, double* Linv, const double* r,
                                 double* contrib, double* y, double* x, int* fail, hipStream_t s);

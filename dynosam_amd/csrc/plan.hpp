@@ -72,6 +72,17 @@ struct BackTask {
   int32_t pad;
 };
 
+// one workgroup of a backward level: a slice [beg, end) of column k's
+// entries; the nparts workgroups of a column meet through partial sums at
+// partials + (pbase + part) * 64 and a per-column arrival counter
+struct BackPart {
+  int32_t k;
+  int32_t beg, end;
+  int32_t nparts, part, pbase;
+  int32_t pad0, pad1;
+};
+constexpr int kBackPartTiles = 2;  // entries (64x64 tiles) per backward workgroup
+
 struct GatherList {
   std::vector<int64_t> start;  // ntargets + 1
   std::vector<GEntry> ent;
@@ -134,6 +145,9 @@ struct Plan {
   std::vector<BackTask> btask;
   std::vector<int32_t> blevel;
   std::vector<int32_t> bent;            // pairs (slot, row tile)
+  std::vector<BackPart> bpart;          // backward workgroups, grouped by level
+  std::vector<int32_t> bplevel;         // level l = bpart [bplevel[l], bplevel[l+1])
+  int32_t n_partials = 0;
   double tile_flops = 0.0;              // tile-level factorisation flops (incl. fill)
 };
 

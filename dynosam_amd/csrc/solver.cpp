@@ -109,7 +109,10 @@ struct dynohip_solver {
   DevBuf<double> slots, gred, xy, dpt, linv, contrib;
   DevBuf<int32_t> tile_pos, row_start, row_col, row_slot, bent, pairs;
   DevBuf<TileTask> ftask;
-  DevBuf<BackTask> btask;
+  DevBuf<BackPart> bpart;
+  DevBuf<double> bpartials;
+  DevBuf<int> arrive;
+  DevBuf<unsigned> done;
   DevBuf<double> partials, result;
   DevBuf<int> fail;
   int partial_slots = 0;
@@ -207,7 +210,13 @@ int upload_plan(dynohip_solver* s) {
   HIPCHK(s, s->ftask.upload(P.ftask, st));
   HIPCHK(s, s->pairs.upload(P.pairs, st));
   HIPCHK(s, s->contrib.alloc(static_cast<size_t>(P.n_slots) * kTile));
-  HIPCHK(s, s->btask.upload(P.btask, st));
+  HIPCHK(s, s->bpart.upload(P.bpart, st));
+  HIPCHK(s, s->bpartials.alloc(static_cast<size_t>(P.n_partials) * kTile + 1));
+  HIPCHK(s, s->arrive.alloc(static_cast<size_t>(P.NT) + 1));
+  HIPCHK(s, hipMemsetAsync(s->arrive.p, 0, (static_cast<size_t>(P.NT) + 1) * sizeof(int), st));
+  HIPCHK(s, s->done.alloc(static_cast<size_t>(P.NT) + 1));
+  HIPCHK(s, hipMemsetAsync(s->done.p, 0, (static_cast<size_t>(P.NT) + 1) * sizeof(unsigned), st));
+  s->sd.epoch = 0;
   const size_t nrp = static_cast<size_t>(P.NT) * kTile;
   HIPCHK(s, s->gred.alloc(nrp > 0 ? nrp : 1));
   HIPCHK(s, s->xy.alloc(2 * (nrp > 0 ? nrp : 1)));
@@ -242,7 +251,10 @@ int upload_plan(dynohip_solver* s) {
   b.row_slot = s->row_slot.p;
   s->sd.ftask = s->ftask.p;
   s->sd.pairs = s->pairs.p;
-  s->sd.btask = s->btask.p;
+  s->sd.bpart = s->bpart.p;
+  s->sd.partials = s->bpartials.p;
+  s->sd.arrive = s->arrive.p;
+  s->sd.done = s->done.p;
   s->sd.bent = s->bent.p;
   HIPCHK(s, hipStreamSynchronize(st));
   return 0;
@@ -306,7 +318,8 @@ void enqueue_try(dynohip_solver* s, double lambda) {
   if (timed) (void)hipEventRecord(s->ev[4], st);
   double* y = s->xy.p;
   double* x = s->xy.p + nrp;
-  launch_tile_cholesky_solve(s->bd, s->sd, P.flevel, P.blevel, s->linv.p, s->gred.p, s->contrib.p, y, x,
+  if (++s->sd.epoch == 0) s->sd.epoch = 1;  // stamps of earlier solves never match
+  launch_tile_cholesky_solve(s->bd, s->sd, P.flevel, P.bplevel, s->linv.p, s->gred.p, s->contrib.p, y, x,
                              s->fail.p, st);
   if (timed) (void)hipEventRecord(s->ev[5], st);
   if (timed) (void)hipEventRecord(s->ev[6], st);
@@ -408,6 +421,7 @@ int lm_iterate(dynohip_solver* s) {
         s->phase_ms[k - 1] += ms;
       }
     }
+    if (fail & 2) return set_err(s, DYNOHIP_EHIP, "backward solve: dependency wait timed out");
     const int solved = fail == 0 && std::isfinite(res[0]);
     te.solved = solved;
     bool step_ok = false, stop = false;

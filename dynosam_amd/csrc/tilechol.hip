@@ -452,63 +452,190 @@ __global__ __launch_bounds__(256) void k_tasks(TileDev b, const TileTask* __rest
   }
 }
 
-// one level of the backward substitution: a workgroup per column tile k,
-// x_k = L_kk^-T (y_k - sum_i L(i,k)^T x_i). The (entry, row) pairs of the
-// column are flattened over 16 row groups of 64 lanes (lane = column of
-// the tile), four independent loads in flight per lane.
-constexpr int kBackThreads = 1024;
-__global__ __launch_bounds__(kBackThreads) void k_back(TileDev b, const BackTask* __restrict__ tasks,
+// one level of the backward substitution,
+//   x_k = L_kk^-T (y_k - sum_i L(i,k)^T x_i),
+// with every column's entries split over workgroups of <= kBackPartTiles
+// tiles (BackPart). A workgroup sums L(i,k)^T x_i over its tiles (lane =
+// column of the tile, 4 row groups, all loads of a tile issued together).
+// A column with one part finishes directly. Otherwise each part stores its
+// partial sum, releases it (agent-scope fence) and bumps the column's
+// arrival counter; the last part acquires, adds the partials in part order
+// (deterministic), applies L_kk^-T and re-arms the counter.
+constexpr int kBackThreads = 256;
+__global__ __launch_bounds__(kBackThreads) void k_back(TileDev b, const BackPart* __restrict__ parts,
                                                        const int32_t* __restrict__ ent,
                                                        const double* __restrict__ Linv,
-                                                       const double* __restrict__ y, double* __restrict__ x) {
+                                                       const double* __restrict__ y, double* __restrict__ x,
+                                                       double* __restrict__ partials, int* __restrict__ arrive) {
   constexpr int NP = kBackThreads / T;
   __shared__ double part[NP][T];
   __shared__ double rv[T];
-  __shared__ const double* Lp[64];
-  __shared__ const double* Xp[64];
-  const BackTask tk = tasks[blockIdx.x];
+  __shared__ int last;
+  const BackPart pt = parts[blockIdx.x];
   const int tid = threadIdx.x, c = tid & (T - 1), q = tid >> 6;
-  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-  for (int e0 = tk.beg; e0 < tk.end; e0 += 64) {
-    const int ne = min(64, tk.end - e0);
-    __syncthreads();
-    if (tid < ne) {
-      Lp[tid] = slot_ptr(b, ent[2 * (e0 + tid)]);
-      Xp[tid] = x + static_cast<int64_t>(ent[2 * (e0 + tid) + 1]) * T;
-    }
-    __syncthreads();
-    const int nrow = ne * T;
-    int idx = q;
-    for (; idx + 3 * NP < nrow; idx += 4 * NP) {
-      const int i0 = idx, i1 = idx + NP, i2 = idx + 2 * NP, i3 = idx + 3 * NP;
-      s0 += Lp[i0 >> 6][(i0 & 63) * T + c] * Xp[i0 >> 6][i0 & 63];
-      s1 += Lp[i1 >> 6][(i1 & 63) * T + c] * Xp[i1 >> 6][i1 & 63];
-      s2 += Lp[i2 >> 6][(i2 & 63) * T + c] * Xp[i2 >> 6][i2 & 63];
-      s3 += Lp[i3 >> 6][(i3 & 63) * T + c] * Xp[i3 >> 6][i3 & 63];
-    }
-    for (; idx < nrow; idx += NP) s0 += Lp[idx >> 6][(idx & 63) * T + c] * Xp[idx >> 6][idx & 63];
-  }
-  part[q][c] = (s0 + s1) + (s2 + s3);
-  __syncthreads();
-  if (tid < T) {
-    double t = 0.0;
+  double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int e = pt.beg; e < pt.end; ++e) {
+    const double* L = slot_ptr(b, ent[2 * e]);
+    const double* xi = x + static_cast<int64_t>(ent[2 * e + 1]) * T;
+    double lv[16], xv[16];
 #pragma unroll
-    for (int k = 0; k < NP; ++k) t += part[k][tid];
-    rv[tid] = y[static_cast<int64_t>(tk.k) * T + tid] - t;
+    for (int m = 0; m < 16; ++m) {
+      lv[m] = L[(q + NP * m) * T + c];
+      xv[m] = xi[q + NP * m];
+    }
+#pragma unroll
+    for (int m = 0; m < 16; ++m) s[m & 7] += lv[m] * xv[m];
   }
+  part[q][c] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  __syncthreads();
+  double sum = 0.0;
+  if (tid < T) sum = (part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]);
+  if (pt.nparts > 1) {
+    if (tid < T) partials[static_cast<int64_t>(pt.pbase + pt.part) * T + tid] = sum;
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      const int prev = __hip_atomic_fetch_add(arrive + pt.k, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = prev == pt.nparts - 1;
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        arrive[pt.k] = 0;
+      }
+    }
+    __syncthreads();
+    if (!last) return;
+    if (tid < T) {
+      sum = 0.0;
+      for (int p = 0; p < pt.nparts; ++p) sum += partials[static_cast<int64_t>(pt.pbase + p) * T + tid];
+    }
+  }
+  if (tid < T) rv[tid] = y[static_cast<int64_t>(pt.k) * T + tid] - sum;
   __syncthreads();
   // x_k[c] = sum_{m >= c} Linv[m][c] rv[m]
-  const double* Li = Linv + static_cast<int64_t>(tk.k) * T * T;
+  const double* Li = Linv + static_cast<int64_t>(pt.k) * T * T;
   double t = 0.0;
+#pragma unroll 4
   for (int m = q; m < T; m += NP)
     if (m >= c) t += Li[m * T + c] * rv[m];
   part[q][c] = t;
   __syncthreads();
-  if (tid < T) {
-    double u = 0.0;
+  if (tid < T)
+    x[static_cast<int64_t>(pt.k) * T + tid] = (part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]);
+}
+
+// The whole backward substitution in one launch: workgroup b runs part b of
+// the parts listed in backward-level order (a topological order). A part
+// waits until the columns it reads are done in this solve (done[i] ==
+// epoch). The launcher only uses it when every part can be resident at
+// once, so each wait is for a workgroup that is already running. Every wait
+// is still bounded: after ~2^22 polls the part sets bit 1 of *fail and
+// gives up, so a broken schedule ends in an error, not a hang.
+// Hand-offs follow cdna_hip_programming.md Guideline 16, R1. The payloads
+// (x_k and the partial sums) are written with agent-scope relaxed atomic
+// stores (write-through sc1) and drained (vmcnt(0)) by every storing wave
+// before one lane stores the flag or adds to the counter. Consumers read
+// them only with agent-scope atomic loads (sc1, to registers), so neither a
+// release nor an acquire fence is needed. Operands that no workgroup of
+// this launch writes (L tiles, L^-1, y) are fetched before the wait.
+constexpr int kSpinLimit = 1 << 22;
+
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(kBackThreads) void k_back_persist(TileDev b, const BackPart* __restrict__ parts,
+                                                               const int32_t* __restrict__ ent,
+                                                               const double* __restrict__ Linv,
+                                                               const double* __restrict__ y, double* x,
+                                                               double* partials, int* arrive, unsigned* done,
+                                                               unsigned epoch, int* fail) {
+  constexpr int NP = kBackThreads / T;
+  static_assert(kBackPartTiles == 2, "prefetch below holds two tiles");
+  __shared__ double part[NP][T];
+  __shared__ double rv[T];
+  __shared__ double xs[kBackPartTiles][T];
+  __shared__ int last, abort_;
+  const BackPart pt = parts[blockIdx.x];
+  const int tid = threadIdx.x, c = tid & (T - 1), q = tid >> 6;
+  const int ne = pt.end - pt.beg;
+  // (1) prefetch what does not depend on other columns
+  double lv[kBackPartTiles][16];
 #pragma unroll
-    for (int k = 0; k < NP; ++k) u += part[k][tid];
-    x[static_cast<int64_t>(tk.k) * T + tid] = u;
+  for (int j = 0; j < kBackPartTiles; ++j)
+    if (j < ne) {
+      const double* L = slot_ptr(b, ent[2 * (pt.beg + j)]);
+#pragma unroll
+      for (int m = 0; m < 16; ++m) lv[j][m] = L[(q + NP * m) * T + c];
+    }
+  const double* Li = Linv + static_cast<int64_t>(pt.k) * T * T;
+  double li[16];
+#pragma unroll
+  for (int m = 0; m < 16; ++m) li[m] = Li[(q + NP * m) * T + c];
+  const double yk = tid < T ? y[static_cast<int64_t>(pt.k) * T + tid] : 0.0;
+  // (2) wait for the columns this part reads (one lane polls, relaxed)
+  if (tid == 0) {
+    int ok = 1;
+    for (int e = pt.beg; e < pt.end && ok; ++e) {
+      const unsigned* d = done + ent[2 * e + 1];
+      int spins = 0;
+      while (__hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+        if (++spins > kSpinLimit) { ok = 0; break; }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    if (!ok) atomicOr(fail, 2);
+    abort_ = !ok;
+  }
+  __syncthreads();
+  if (abort_) return;
+  // (3) x of the rows read, sc1 loads (lane-varying: vector path)
+  if (tid < ne * T) xs[tid >> 6][c] = ld_sc1(x + static_cast<int64_t>(ent[2 * (pt.beg + (tid >> 6)) + 1]) * T + c);
+  __syncthreads();
+  double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < kBackPartTiles; ++j)
+    if (j < ne) {
+#pragma unroll
+      for (int m = 0; m < 16; ++m) s[m & 7] += lv[j][m] * xs[j][q + NP * m];
+    }
+  part[q][c] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  __syncthreads();
+  double sum = 0.0;
+  if (tid < T) sum = (part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]);
+  if (pt.nparts > 1) {
+    if (tid < T) st_sc1(partials + static_cast<int64_t>(pt.pbase + pt.part) * T + tid, sum);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const int prev = __hip_atomic_fetch_add(arrive + pt.k, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = prev == pt.nparts - 1;
+      if (last) __hip_atomic_store(arrive + pt.k, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!last) return;
+    if (tid < T) {
+      sum = 0.0;
+      for (int p = 0; p < pt.nparts; ++p) sum += ld_sc1(partials + static_cast<int64_t>(pt.pbase + p) * T + tid);
+    }
+  }
+  if (tid < T) rv[tid] = yk - sum;
+  __syncthreads();
+  // x_k[c] = sum_{m >= c} Linv[m][c] rv[m]
+  double t = 0.0;
+#pragma unroll
+  for (int m = 0; m < 16; ++m) {
+    const int row = q + NP * m;
+    if (row >= c) t += li[m] * rv[row];
+  }
+  part[q][c] = t;
+  __syncthreads();
+  if (tid < T) {
+    st_sc1(x + static_cast<int64_t>(pt.k) * T + tid, (part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (tid == 0) __hip_atomic_store(done + pt.k, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -521,9 +648,15 @@ void launch_tile_cholesky_solve(const TileDev& b, const TileSchedDev& sd, const 
     const int n = flevel[lv + 1] - flevel[lv];
     if (n > 0) k_tasks<<<n, 256, 0, s>>>(b, sd.ftask + flevel[lv], sd.pairs, Linv, r, contrib, y, fail);
   }
+  const int nparts = blevel.empty() ? 0 : blevel.back();
+  if (nparts > 0 && nparts <= kBackPersistMax) {
+    k_back_persist<<<nparts, kBackThreads, 0, s>>>(b, sd.bpart, sd.bent, Linv, y, x, sd.partials, sd.arrive, sd.done,
+                                                   sd.epoch, fail);
+    return;
+  }
   for (size_t lv = 0; lv + 1 < blevel.size(); ++lv) {
     const int n = blevel[lv + 1] - blevel[lv];
-    if (n > 0) k_back<<<n, kBackThreads, 0, s>>>(b, sd.btask + blevel[lv], sd.bent, Linv, y, x);
+    if (n > 0) k_back<<<n, kBackThreads, 0, s>>>(b, sd.bpart + blevel[lv], sd.bent, Linv, y, x, sd.partials, sd.arrive);
   }
 }
 

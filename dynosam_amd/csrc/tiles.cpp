@@ -291,6 +291,24 @@ void build_tile_schedule(Plan& P) {
   P.btask = std::move(best.btask);
   P.blevel = std::move(best.blevel);
   P.bent = std::move(best.bent);
+  // split every backward task into workgroups of <= kBackPartTiles entries
+  P.bpart.clear();
+  P.bplevel.assign(1, 0);
+  P.n_partials = 0;
+  for (size_t l = 0; l + 1 < P.blevel.size(); ++l) {
+    for (int32_t q = P.blevel[l]; q < P.blevel[l + 1]; ++q) {
+      const BackTask& t = P.btask[q];
+      const int32_t n = t.end - t.beg;
+      const int32_t np = std::max<int32_t>(1, (n + kBackPartTiles - 1) / kBackPartTiles);
+      const int32_t pbase = np > 1 ? P.n_partials : -1;
+      if (np > 1) P.n_partials += np;
+      for (int32_t part = 0; part < np; ++part) {
+        const int32_t b0 = t.beg + part * kBackPartTiles;
+        P.bpart.push_back({t.k, b0, std::min(t.end, b0 + kBackPartTiles), np, part, pbase, 0, 0});
+      }
+    }
+    P.bplevel.push_back(static_cast<int32_t>(P.bpart.size()));
+  }
   P.tile_flops = best.flops;
   // per-row lookup for the assembly: stored tile (row tile, column tile)
   std::vector<std::vector<std::pair<int32_t, int32_t>>> rows(NT);
