@@ -53,11 +53,6 @@ struct TileDev {
   const int32_t* row_slot = nullptr;
 };
 
-// parts of the one-launch backward solve: at most this many workgroups, so
-// that all of them are resident at once (256 CUs x several 256-thread,
-// 10 KB-LDS workgroups each)
-constexpr int kBackPersistMax = 1024;
-
 struct TileSchedDev {
   const TileTask* ftask = nullptr;
   const int32_t* pairs = nullptr;

@@ -81,7 +81,9 @@ struct BackPart {
   int32_t nparts, part, pbase;
   int32_t pad0, pad1;
 };
-constexpr int kBackPartTiles = 2;  // entries (64x64 tiles) per backward workgroup
+// the one-launch backward solve keeps all its workgroups resident: at most
+// this many (256 CUs x several 256-thread, few-KB-LDS workgroups each)
+constexpr int kBackPersistMax = 1024;
 
 struct GatherList {
   std::vector<int64_t> start;  // ntargets + 1
@@ -145,6 +147,7 @@ struct Plan {
   std::vector<BackTask> btask;
   std::vector<int32_t> blevel;
   std::vector<int32_t> bent;            // pairs (slot, row tile)
+  int32_t back_part_tiles = 2;          // entries (64x64 tiles) per backward workgroup
   std::vector<BackPart> bpart;          // backward workgroups, grouped by level
   std::vector<int32_t> bplevel;         // level l = bpart [bplevel[l], bplevel[l+1])
   int32_t n_partials = 0;

@@ -454,7 +454,7 @@ __global__ __launch_bounds__(256) void k_tasks(TileDev b, const TileTask* __rest
 
 // one level of the backward substitution,
 //   x_k = L_kk^-T (y_k - sum_i L(i,k)^T x_i),
-// with every column's entries split over workgroups of <= kBackPartTiles
+// with every column's entries split over workgroups of <= back_part_tiles
 // tiles (BackPart). A workgroup sums L(i,k)^T x_i over its tiles (lane =
 // column of the tile, 4 row groups, all loads of a tile issued together).
 // A column with one part finishes directly. Otherwise each part stores its
@@ -553,18 +553,18 @@ __global__ __launch_bounds__(kBackThreads) void k_back_persist(TileDev b, const 
                                                                double* partials, int* arrive, unsigned* done,
                                                                unsigned epoch, int* fail) {
   constexpr int NP = kBackThreads / T;
-  static_assert(kBackPartTiles == 2, "prefetch below holds two tiles");
+  constexpr int CH = 2;  // entries per chunk; the first chunk is fetched before the wait
   __shared__ double part[NP][T];
   __shared__ double rv[T];
-  __shared__ double xs[kBackPartTiles][T];
+  __shared__ double xs[CH][T];
   __shared__ int last, abort_;
   const BackPart pt = parts[blockIdx.x];
   const int tid = threadIdx.x, c = tid & (T - 1), q = tid >> 6;
   const int ne = pt.end - pt.beg;
   // (1) prefetch what does not depend on other columns
-  double lv[kBackPartTiles][16];
+  double lv[CH][16];
 #pragma unroll
-  for (int j = 0; j < kBackPartTiles; ++j)
+  for (int j = 0; j < CH; ++j)
     if (j < ne) {
       const double* L = slot_ptr(b, ent[2 * (pt.beg + j)]);
 #pragma unroll
@@ -591,16 +591,30 @@ __global__ __launch_bounds__(kBackThreads) void k_back_persist(TileDev b, const 
   }
   __syncthreads();
   if (abort_) return;
-  // (3) x of the rows read, sc1 loads (lane-varying: vector path)
-  if (tid < ne * T) xs[tid >> 6][c] = ld_sc1(x + static_cast<int64_t>(ent[2 * (pt.beg + (tid >> 6)) + 1]) * T + c);
-  __syncthreads();
+  // (3) x of the rows read, sc1 loads (lane-varying: vector path), chunk
+  // by chunk; later chunks' L tiles are loaded after the wait
   double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int j0 = 0; j0 < ne; j0 += CH) {
+    if (j0 > 0) {
+      __syncthreads();
 #pragma unroll
-  for (int j = 0; j < kBackPartTiles; ++j)
-    if (j < ne) {
+      for (int j = 0; j < CH; ++j)
+        if (j0 + j < ne) {
+          const double* L = slot_ptr(b, ent[2 * (pt.beg + j0 + j)]);
 #pragma unroll
-      for (int m = 0; m < 16; ++m) s[m & 7] += lv[j][m] * xs[j][q + NP * m];
+          for (int m = 0; m < 16; ++m) lv[j][m] = L[(q + NP * m) * T + c];
+        }
     }
+    if (tid < min(CH, ne - j0) * T)
+      xs[tid >> 6][c] = ld_sc1(x + static_cast<int64_t>(ent[2 * (pt.beg + j0 + (tid >> 6)) + 1]) * T + c);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < CH; ++j)
+      if (j0 + j < ne) {
+#pragma unroll
+        for (int m = 0; m < 16; ++m) s[m & 7] += lv[j][m] * xs[j][q + NP * m];
+      }
+  }
   part[q][c] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
   __syncthreads();
   double sum = 0.0;

@@ -285,13 +285,25 @@ void build_tile_schedule(Plan& P) {
   P.nd_leaf = best.leaf;
   P.tile_pos = best.pos;
   P.n_slots = best.n_slots;
+  P.tile_flops = best.flops;
   P.ftask = std::move(best.ftask);
   P.pairs = std::move(best.pairs);
   P.flevel = std::move(best.flevel);
   P.btask = std::move(best.btask);
   P.blevel = std::move(best.blevel);
   P.bent = std::move(best.bent);
-  // split every backward task into workgroups of <= kBackPartTiles entries
+  // split every backward task into workgroups of <= back_part_tiles entries:
+  // the smallest power of two (>= 2) whose part count lets the one-launch
+  // backward solve keep every workgroup resident
+  auto count_parts = [&](int tpp) {
+    int64_t n = 0;
+    for (const BackTask& t : P.btask) n += std::max<int32_t>(1, (t.end - t.beg + tpp - 1) / tpp);
+    return n;
+  };
+  P.back_part_tiles = 2;
+  while (count_parts(P.back_part_tiles) > kBackPersistMax && P.back_part_tiles < 64) P.back_part_tiles *= 2;
+  if (count_parts(P.back_part_tiles) > kBackPersistMax) P.back_part_tiles = 2;  // level launches
+  const int32_t tpp = P.back_part_tiles;
   P.bpart.clear();
   P.bplevel.assign(1, 0);
   P.n_partials = 0;
@@ -299,17 +311,16 @@ void build_tile_schedule(Plan& P) {
     for (int32_t q = P.blevel[l]; q < P.blevel[l + 1]; ++q) {
       const BackTask& t = P.btask[q];
       const int32_t n = t.end - t.beg;
-      const int32_t np = std::max<int32_t>(1, (n + kBackPartTiles - 1) / kBackPartTiles);
+      const int32_t np = std::max<int32_t>(1, (n + tpp - 1) / tpp);
       const int32_t pbase = np > 1 ? P.n_partials : -1;
       if (np > 1) P.n_partials += np;
       for (int32_t part = 0; part < np; ++part) {
-        const int32_t b0 = t.beg + part * kBackPartTiles;
-        P.bpart.push_back({t.k, b0, std::min(t.end, b0 + kBackPartTiles), np, part, pbase, 0, 0});
+        const int32_t b0 = t.beg + part * tpp;
+        P.bpart.push_back({t.k, b0, std::min(t.end, b0 + tpp), np, part, pbase, 0, 0});
       }
     }
     P.bplevel.push_back(static_cast<int32_t>(P.bpart.size()));
   }
-  P.tile_flops = best.flops;
   // per-row lookup for the assembly: stored tile (row tile, column tile)
   std::vector<std::vector<std::pair<int32_t, int32_t>>> rows(NT);
   for (int cp = 0; cp < NT; ++cp)
