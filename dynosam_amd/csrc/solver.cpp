@@ -114,7 +114,7 @@ struct dynohip_solver {
   DevBuf<int> arrive;
   DevBuf<unsigned> done;
   DevBuf<double> partials, result;
-  DevBuf<int> fail;
+  int* failp = nullptr;  // inside `result` (doubles [0..3] results, [4] fail flag as int)
   int partial_slots = 0;
   ChainDev cd;
   TileDev bd;
@@ -122,6 +122,11 @@ struct dynohip_solver {
   // LM state
   dynohip_lm_params prm{};
   double lambda = 1e-5, error = 0.0;
+  // the arena holds the linearisation at the current values (left there by
+  // the speculative linearisation of an accepted step); next_oldlin is its
+  // linear error at delta = 0
+  bool lin_valid = false;
+  double next_oldlin = 0.0;
   int iterations = 0, inner = 0, converged = 0;
   std::vector<dynohip_trace_entry> trace;
   // values snapshot (bench hook)
@@ -186,7 +191,7 @@ int upload_plan(dynohip_solver* s) {
   s->partial_slots = slots;
   HIPCHK(s, s->partials.alloc(2ull * slots));
   HIPCHK(s, s->result.alloc(8));
-  HIPCHK(s, s->fail.alloc(1));
+  s->failp = reinterpret_cast<int*>(s->result.p + 4);
   if (upload_gather(s, P.gD, s->gD) || upload_gather(s, P.gE, s->gE) || upload_gather(s, P.gGp, s->gGp) ||
       upload_gather(s, P.gW, s->gW) || upload_gather(s, P.gRed, s->gRed) || upload_gather(s, P.gGred, s->gGred))
     return DYNOHIP_EHIP;
@@ -287,10 +292,10 @@ int compute_error(dynohip_solver* s, const double* pose, const double* pt, doubl
 }
 
 // linearisation + point-side blocks (once per outer iteration)
-void enqueue_linearize(dynohip_solver* s) {
+void enqueue_linearize(dynohip_solver* s, const double* pose, const double* pt) {
   Plan& P = s->plan;
   double* A = s->arena.p;
-  for (int t = 0; t < kNTypes; ++t) launch_linearize(t, s->td[t], s->pose.p, s->pt.p, A, s->stream);
+  for (int t = 0; t < kNTypes; ++t) launch_linearize(t, s->td[t], pose, pt, A, s->stream);
   launch_gather_3x3(s->gD.dev(P.gD.ntargets()), A, A + P.off_D, s->stream);
   launch_gather_3x3(s->gE.dev(P.gE.ntargets()), A, A + P.off_E, s->stream);
   launch_gather_3x1(s->gGp.dev(P.gGp.ntargets()), A, A + P.off_gp, s->stream);
@@ -306,10 +311,10 @@ void enqueue_try(dynohip_solver* s, double lambda) {
   double* A = s->arena.p;
   const size_t nrp = static_cast<size_t>(P.NT) * kTile;
   if (timed) (void)hipEventRecord(s->ev[2], st);
-  (void)hipMemsetAsync(s->fail.p, 0, sizeof(int), st);
+  (void)hipMemsetAsync(s->failp, 0, sizeof(double), st);
   (void)hipMemsetAsync(s->slots.p, 0, static_cast<size_t>(P.n_slots) * kTile * kTile * sizeof(double), st);
   (void)hipMemsetAsync(s->gred.p, 0, nrp * sizeof(double), st);
-  launch_chain_factor(s->cd, A, lambda, s->fail.p, st);
+  launch_chain_factor(s->cd, A, lambda, s->failp, st);
   launch_chain_solve_y(s->cd, A, st);
   if (timed) (void)hipEventRecord(s->ev[3], st);
   launch_gather_band(s->gRed.dev(P.gRed.ntargets()), A, s->redA.p, s->redB.p, s->bd, lambda, st);
@@ -320,7 +325,7 @@ void enqueue_try(dynohip_solver* s, double lambda) {
   double* x = s->xy.p + nrp;
   if (++s->sd.epoch == 0) s->sd.epoch = 1;  // stamps of earlier solves never match
   launch_tile_cholesky_solve(s->bd, s->sd, P.flevel, P.bplevel, s->linv.p, s->gred.p, s->contrib.p, y, x,
-                             s->fail.p, st);
+                             s->failp, st);
   if (timed) (void)hipEventRecord(s->ev[5], st);
   if (timed) (void)hipEventRecord(s->ev[6], st);
   // pose deltas are x[0 .. 6 n_pose) in pose-index order
@@ -387,19 +392,27 @@ void compute_base_stats(dynohip_solver* s) {
 // LevenbergMarquardtOptimizer::iterate()
 int lm_iterate(dynohip_solver* s) {
   hipStream_t st = s->stream;
-  if (s->timing) (void)hipEventRecord(s->ev[0], st);
-  enqueue_linearize(s);
-  if (s->timing) (void)hipEventRecord(s->ev[1], st);
-  enqueue_linerr(s, nullptr, nullptr, s->partials.p, s->result.p + 2);
+  // Speculation: right after each try, the linearisation at the candidate
+  // values is enqueued too (before the host has seen whether the step is
+  // accepted), so the GPU is not idle while the host decides. Accepted: the
+  // arena already holds the next iteration's linearisation. Rejected: the
+  // current values are re-linearised before the next try. Results are
+  // identical either way; phase timing runs without speculation.
+  const bool speculate = !s->timing;
   double oldLin = 0.0;
-  HIPCHK(s, hipMemcpyAsync(&oldLin, s->result.p + 2, sizeof(double), hipMemcpyDeviceToHost, st));
-  HIPCHK(s, hipStreamSynchronize(st));
-  s->n_lin++;
-  if (s->timing) {
-    float ms = 0.f;
-    (void)hipEventElapsedTime(&ms, s->ev[0], s->ev[1]);
-    s->phase_ms[0] += ms;
+  bool have_old = false;
+  if (s->lin_valid) {
+    oldLin = s->next_oldlin;
+    have_old = true;
+  } else {
+    if (s->timing) (void)hipEventRecord(s->ev[0], st);
+    enqueue_linearize(s, s->pose.p, s->pt.p);
+    if (s->timing) (void)hipEventRecord(s->ev[1], st);
+    enqueue_linerr(s, nullptr, nullptr, s->partials.p, s->result.p + 2);
   }
+  s->lin_valid = false;
+  s->n_lin++;
+  bool relinearize = false;
   for (;;) {
     dynohip_trace_entry te{};
     te.outer_iteration = s->iterations;
@@ -407,12 +420,32 @@ int lm_iterate(dynohip_solver* s) {
     te.current_error = s->error;
     te.new_error = INFINITY;
     te.old_linear_error = oldLin;
+    if (relinearize) {
+      // a rejected speculative step left the candidate's linearisation
+      enqueue_linearize(s, s->pose.p, s->pt.p);
+      s->n_lin++;
+      relinearize = false;
+    }
     enqueue_try(s, s->lambda);
-    double res[2];
-    int fail = 0;
-    HIPCHK(s, hipMemcpyAsync(res, s->result.p, 2 * sizeof(double), hipMemcpyDeviceToHost, st));
-    HIPCHK(s, hipMemcpyAsync(&fail, s->fail.p, sizeof(int), hipMemcpyDeviceToHost, st));
+    if (speculate) {
+      enqueue_linearize(s, s->pose_c.p, s->pt_c.p);
+      enqueue_linerr(s, nullptr, nullptr, s->partials.p, s->result.p + 3);
+    }
+    double res[5];
+    HIPCHK(s, hipMemcpyAsync(res, s->result.p, 5 * sizeof(double), hipMemcpyDeviceToHost, st));
     HIPCHK(s, hipStreamSynchronize(st));
+    int fail = 0;
+    std::memcpy(&fail, &res[4], sizeof(int));
+    if (!have_old) {
+      oldLin = res[2];
+      te.old_linear_error = oldLin;
+      have_old = true;
+      if (s->timing) {
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, s->ev[0], s->ev[1]);
+        s->phase_ms[0] += ms;
+      }
+    }
     s->n_solves++;
     if (s->timing) {
       float ms = 0.f;
@@ -448,6 +481,10 @@ int lm_iterate(dynohip_solver* s) {
     if (step_ok) {
       std::swap(s->pose.p, s->pose_c.p);
       std::swap(s->pt.p, s->pt_c.p);
+      if (speculate) {
+        s->lin_valid = true;
+        s->next_oldlin = res[3];
+      }
       s->error = newError;
       s->lambda /= s->prm.lambda_factor;
       if (s->lambda < s->prm.lambda_lower_bound) s->lambda = s->prm.lambda_lower_bound;
@@ -458,6 +495,7 @@ int lm_iterate(dynohip_solver* s) {
       s->lambda *= s->prm.lambda_factor;
       s->inner++;
       if (s->lambda >= s->prm.lambda_upper_bound) break;
+      relinearize = speculate;
     } else {
       break;
     }
@@ -555,6 +593,7 @@ int dynohip_set_graph(dynohip_solver* s, const dynohip_graph_view* g) {
   }
   s->graph = std::move(gc);
   s->has_graph = true;
+  s->lin_valid = false;
   s->has_plan = false;
   s->has_values = false;
   return DYNOHIP_OK;
@@ -577,6 +616,7 @@ int dynohip_set_values(dynohip_solver* s, const uint64_t* keys, const uint8_t* k
     s->has_plan = true;
     compute_base_stats(s);
   }
+  s->lin_valid = false;
   Plan& P = s->plan;
   std::vector<double> hp(12ull * P.n_pose), hq(3ull * P.n_pt);
   size_t off = 0;
@@ -633,6 +673,7 @@ int dynohip_lm_reset(dynohip_solver* s, const dynohip_lm_params* p) {
     return set_err(s, DYNOHIP_EINVAL, "only diagonalDamping=false, useFixedLambdaFactor=true are supported");
   (void)hipSetDevice(s->device);
   s->prm = *p;
+  s->lin_valid = false;
   s->lambda = p->lambda_initial;
   s->iterations = 0;
   s->inner = 0;
@@ -706,7 +747,8 @@ int dynohip_linearize(dynohip_solver* s, double* out, size_t n_doubles) {
   if (rc) return rc;
   if (n_doubles < dynohip_linearize_size(s)) return set_err(s, DYNOHIP_EINVAL, "output buffer too small");
   (void)hipSetDevice(s->device);
-  enqueue_linearize(s);
+  s->lin_valid = false;
+  enqueue_linearize(s, s->pose.p, s->pt.p);
   const Plan& P = s->plan;
   std::vector<double> rec;
   size_t o = 0;
@@ -751,6 +793,7 @@ int dynohip_values_restore(dynohip_solver* s) {
   const Plan& P = s->plan;
   if ((P.n_pose && !s->pose_snap.p) || (P.n_pt && !s->pt_snap.p)) return set_err(s, DYNOHIP_ESTATE, "no snapshot");
   (void)hipSetDevice(s->device);
+  s->lin_valid = false;
   if (P.n_pose) HIPCHK(s, hipMemcpyAsync(s->pose.p, s->pose_snap.p, 12ull * P.n_pose * sizeof(double), hipMemcpyDeviceToDevice, s->stream));
   if (P.n_pt) HIPCHK(s, hipMemcpyAsync(s->pt.p, s->pt_snap.p, 3ull * P.n_pt * sizeof(double), hipMemcpyDeviceToDevice, s->stream));
   HIPCHK(s, hipStreamSynchronize(s->stream));
