@@ -580,6 +580,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_grad(const int64_t* __restric
 
 // ---------------------------------------------------------------- chains
 // 3x3 helpers (row-major)
+// 3x3 Cholesky (divisions rounded exactly, as the oracle's C code)
 __device__ __forceinline__ bool chol3(const double* A, double* L) {
   const double a00 = A[0];
   if (!(a00 > 0.0)) return false;
@@ -636,27 +637,38 @@ __device__ __forceinline__ void sub_mtx(const double* M, const double* X, double
     for (int c = 0; c < N; ++c) B[r * N + c] -= M[r] * X[c] + M[3 + r] * X[N + c] + M[6 + r] * X[2 * N + c];
 }
 
+template <int K>
+__device__ __forceinline__ void ldk(const double* __restrict__ src, double (&dst)[K]) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) dst[k] = src[k];
+}
+
 // block Cholesky of each point chain C = tridiag(D_i + lambda I, E_i):
 //   M_i = E_{i-1} L_{i-1}^-T, L_i L_i^T = D_i + lambda I - M_i M_i^T;
-// then v = C^-1 gp
+// then v = C^-1 gp. Thread per chain; the next point's D, g_p and E are
+// fetched while the current point is factored.
 __global__ __launch_bounds__(kBlock) void k_chain_factor(ChainDev cd, double* __restrict__ arena, double lambda,
                                                          int* fail) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= cd.n_comp) return;
   const int i0 = cd.comp_start[c], i1 = cd.comp_start[c + 1];
   double Lp[9], z[3];
+  double Dn[9], gn[3], En[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  ldk(arena + cd.off_D + 9ll * i0, Dn);
+  ldk(arena + cd.off_gp + 3ll * i0, gn);
   for (int i = i0; i < i1; ++i) {
-    double Dm[9];
-    const double* D = arena + cd.off_D + 9ll * i;
+    double Dm[9], g[3], E[9];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) Dm[k] = D[k];
+    for (int k = 0; k < 9; ++k) { Dm[k] = Dn[k]; E[k] = En[k]; }
+    g[0] = gn[0]; g[1] = gn[1]; g[2] = gn[2];
+    if (i + 1 < i1) {
+      ldk(arena + cd.off_D + 9ll * (i + 1), Dn);
+      ldk(arena + cd.off_gp + 3ll * (i + 1), gn);
+      ldk(arena + cd.off_E + 9ll * i, En);
+    }
     Dm[0] += lambda; Dm[4] += lambda; Dm[8] += lambda;
-    double g[3];
-    const double* gp = arena + cd.off_gp + 3ll * i;
-    g[0] = gp[0]; g[1] = gp[1]; g[2] = gp[2];
     if (i > i0) {
       // M = E L^-T  <=>  L M^T = E^T
-      const double* E = arena + cd.off_E + 9ll * (i - 1);
       double Mt[9];
 #pragma unroll
       for (int r = 0; r < 3; ++r)
@@ -702,7 +714,8 @@ __global__ __launch_bounds__(kBlock) void k_chain_factor(ChainDev cd, double* __
   }
 }
 
-// Y(:, b) = C^-1 W(:, b) for one (component, neighbour pose) pair per thread
+// Y = C^-1 W for one (chain, neighbour pose) pair: thread per pair, the
+// next point's L, M and W prefetched in the forward sweep.
 __global__ __launch_bounds__(kBlock) void k_chain_solve_y(ChainDev cd, double* __restrict__ arena) {
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= cd.n_nb) return;
@@ -714,40 +727,74 @@ __global__ __launch_bounds__(kBlock) void k_chain_solve_y(ChainDev cd, double* _
   double* Y = arena + cd.comp_y_base[c];
   int ep = cd.nbedge_start[q];
   const int ep1 = cd.nbedge_start[q + 1];
-  double Z[18];
-  for (int i = 0; i < n; ++i) {
-    double rhs[18];
+  // rhs of point i: W of edge (i, b) if the point sees pose b, else 0
+  auto load_rhs = [&](int i, double (&rhs)[18]) {
     if (ep < ep1 && cd.nbedge_pt[ep] == i) {
-      const double* W = arena + cd.nbedge_w[ep];
-#pragma unroll
-      for (int k = 0; k < 18; ++k) rhs[k] = W[k];
+      ldk(arena + cd.nbedge_w[ep], rhs);
       ++ep;
     } else {
 #pragma unroll
       for (int k = 0; k < 18; ++k) rhs[k] = 0.0;
     }
-    if (i > 0) sub_mx<6>(arena + cd.off_M + 9ll * (i0 + i), Z, rhs);
-    lsolve<6>(arena + cd.off_L + 9ll * (i0 + i), rhs);
+  };
+  double Z[18], rn[18], Ln[9], Mn[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  load_rhs(0, rn);
+  ldk(arena + cd.off_L + 9ll * i0, Ln);
+  for (int i = 0; i < n; ++i) {
+    double rhs[18], L[9], M[9];
+#pragma unroll
+    for (int k = 0; k < 18; ++k) rhs[k] = rn[k];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) { L[k] = Ln[k]; M[k] = Mn[k]; }
+    if (i + 1 < n) {
+      load_rhs(i + 1, rn);
+      ldk(arena + cd.off_L + 9ll * (i0 + i + 1), Ln);
+      ldk(arena + cd.off_M + 9ll * (i0 + i + 1), Mn);
+    }
+    if (i > 0) sub_mx<6>(M, Z, rhs);
+    lsolve<6>(L, rhs);
     double* yo = Y + 18ll * (static_cast<int64_t>(i) * m + b);
 #pragma unroll
     for (int k = 0; k < 18; ++k) { yo[k] = rhs[k]; Z[k] = rhs[k]; }
   }
+  // backward (Z holds Y_{n-1} after the forward sweep)
   double Yn[18];
   for (int i = n - 1; i >= 0; --i) {
     double* yo = Y + 18ll * (static_cast<int64_t>(i) * m + b);
     double x[18];
+    if (i == n - 1) {
 #pragma unroll
-    for (int k = 0; k < 18; ++k) x[k] = yo[k];
-    if (i < n - 1) sub_mtx<6>(arena + cd.off_M + 9ll * (i0 + i + 1), Yn, x);
+      for (int k = 0; k < 18; ++k) x[k] = Z[k];
+    } else {
+      ldk(yo, x);
+      sub_mtx<6>(arena + cd.off_M + 9ll * (i0 + i + 1), Yn, x);
+    }
     ltsolve<6>(arena + cd.off_L + 9ll * (i0 + i), x);
 #pragma unroll
     for (int k = 0; k < 18; ++k) { yo[k] = x[k]; Yn[k] = x[k]; }
   }
 }
 
-// dp = C^-1 (gp - W dX)
+// t_e = W_e dX_pose(e) for every point-pose edge (edge-parallel)
+__global__ __launch_bounds__(kBlock) void k_wdx(ChainDev cd, int n_edge, const double* __restrict__ arena,
+                                                const double* __restrict__ dpose, double* __restrict__ t) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n_edge) return;
+  double W[18], dx[6];
+  ldk(arena + cd.off_W + 18ll * e, W);
+  ldk(dpose + 6ll * cd.edge_pose[e], dx);
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    double v = 0.0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) v += W[6 * r + k] * dx[k];
+    t[3ll * e + r] = v;
+  }
+}
+
+// dp = C^-1 (gp - W dX), the W dX products from k_wdx
 __global__ __launch_bounds__(kBlock) void k_backsub(ChainDev cd, const double* __restrict__ arena,
-                                                    const double* __restrict__ dpose, double* __restrict__ dpt) {
+                                                    const double* __restrict__ t, double* __restrict__ dpt) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= cd.n_comp) return;
   const int i0 = cd.comp_start[c], i1 = cd.comp_start[c + 1];
@@ -756,12 +803,7 @@ __global__ __launch_bounds__(kBlock) void k_backsub(ChainDev cd, const double* _
     const double* gp = arena + cd.off_gp + 3ll * i;
     double g[3] = {gp[0], gp[1], gp[2]};
     for (int e = cd.pt_edge_start[i]; e < cd.pt_edge_start[i + 1]; ++e) {
-      const double* W = arena + cd.off_W + 18ll * e;
-      const double* dx = dpose + 6ll * cd.edge_pose[e];
-#pragma unroll
-      for (int r = 0; r < 3; ++r)
-#pragma unroll
-        for (int k = 0; k < 6; ++k) g[r] -= W[6 * r + k] * dx[k];
+      g[0] -= t[3ll * e]; g[1] -= t[3ll * e + 1]; g[2] -= t[3ll * e + 2];
     }
     if (i > i0) sub_mx<1>(arena + cd.off_M + 9ll * i, z, g);
     lsolve<1>(arena + cd.off_L + 9ll * i, g);
@@ -871,9 +913,11 @@ void launch_chain_solve_y(const ChainDev& c, double* arena, hipStream_t s) {
   if (c.n_nb == 0) return;
   k_chain_solve_y<<<nblocks(c.n_nb), kBlock, 0, s>>>(c, arena);
 }
-void launch_backsub(const ChainDev& c, const double* arena, const double* dpose, double* dpt, hipStream_t s) {
+void launch_backsub(const ChainDev& c, int n_edge, const double* arena, const double* dpose, double* wdx, double* dpt,
+                    hipStream_t s) {
   if (c.n_comp == 0) return;
-  k_backsub<<<nblocks(c.n_comp), kBlock, 0, s>>>(c, arena, dpose, dpt);
+  if (n_edge > 0) k_wdx<<<nblocks(n_edge), kBlock, 0, s>>>(c, n_edge, arena, dpose, wdx);
+  k_backsub<<<nblocks(c.n_comp), kBlock, 0, s>>>(c, arena, wdx, dpt);
 }
 
 void launch_tile_pad(const TileDev& b, hipStream_t s) {

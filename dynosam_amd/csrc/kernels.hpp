@@ -85,7 +85,9 @@ void launch_gather_grad(const GatherDev& g, const double* arena, double* gred, h
 
 void launch_chain_factor(const ChainDev& c, double* arena, double lambda, int* fail, hipStream_t s);
 void launch_chain_solve_y(const ChainDev& c, double* arena, hipStream_t s);
-void launch_backsub(const ChainDev& c, const double* arena, const double* dpose, double* dpt, hipStream_t s);
+// dpt = C^-1 (gp - W dpose); wdx: scratch of 3 doubles per point-pose edge
+void launch_backsub(const ChainDev& c, int n_edge, const double* arena, const double* dpose, double* wdx, double* dpt,
+                    hipStream_t s);
 
 void launch_tile_pad(const TileDev& b, hipStream_t s);
 // factor the tiles and solve (L L^T) x = r (forward substitution fused

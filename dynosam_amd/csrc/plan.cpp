@@ -148,8 +148,8 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
   }
   {
     std::vector<char> seen(n, 0);
-    int32_t next_pt = 0;
-    P.comp_start.push_back(0);
+    // chains in walk order from the endpoint with the smallest key
+    std::vector<std::vector<int32_t>> chains;
     for (size_t i = 0; i < n; ++i) {
       if (kind[i] != DYNOHIP_POINT3 || seen[i]) continue;
       // collect component
@@ -164,22 +164,35 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
           if (!seen[w]) { seen[w] = 1; comp.push_back(w); }
       }
       if (nedges2 / 2 != comp.size() - 1) { err = "point component is not a chain (cycle)"; return DYNOHIP_ESTRUCT; }
-      // endpoint with the smallest key
       int32_t start = -1;
       for (int32_t u : comp)
         if (adj[u].size() <= 1 && (start < 0 || keys[u] < keys[start])) start = u;
+      std::vector<int32_t> walk;
       int32_t prev = -1, cur = start;
       for (size_t q = 0; q < comp.size(); ++q) {
-        P.user_idx[cur] = next_pt++;
-        P.pt_key.push_back(keys[cur]);
+        walk.push_back(cur);
         int32_t nxt = -1;
         for (int32_t w : adj[cur])
           if (w != prev) nxt = w;
         prev = cur;
         cur = nxt;
       }
+      chains.push_back(std::move(walk));
+    }
+    // longest chains first (stable): the chain kernels run a thread per
+    // chain, so a wave then holds chains of one length and the long ones
+    // start first
+    std::stable_sort(chains.begin(), chains.end(),
+                     [](const std::vector<int32_t>& x, const std::vector<int32_t>& y) { return x.size() > y.size(); });
+    int32_t next_pt = 0;
+    P.comp_start.push_back(0);
+    for (const auto& walk : chains) {
+      for (int32_t u : walk) {
+        P.user_idx[u] = next_pt++;
+        P.pt_key.push_back(keys[u]);
+      }
       P.comp_start.push_back(next_pt);
-      P.max_chain = std::max(P.max_chain, static_cast<int>(comp.size()));
+      P.max_chain = std::max(P.max_chain, static_cast<int>(walk.size()));
     }
     P.n_pt = next_pt;
     P.n_comp = static_cast<int>(P.comp_start.size()) - 1;

@@ -106,7 +106,7 @@ struct dynohip_solver {
   DevBuf<int32_t> comp_start, comp_nb_start, nb_comp, nbedge_start, nbedge_pt, pt_edge_start, edge_pose;
   DevBuf<int64_t> comp_y_base;
   DevBuf<uint32_t> nbedge_w;
-  DevBuf<double> slots, gred, xy, dpt, linv, contrib;
+  DevBuf<double> slots, gred, xy, dpt, wdx, linv, contrib;
   DevBuf<int32_t> tile_pos, row_start, row_col, row_slot, bent, pairs;
   DevBuf<TileTask> ftask;
   DevBuf<BackPart> bpart;
@@ -227,6 +227,7 @@ int upload_plan(dynohip_solver* s) {
   HIPCHK(s, s->xy.alloc(2 * (nrp > 0 ? nrp : 1)));
   HIPCHK(s, s->linv.alloc(static_cast<size_t>(P.NT) * kTile * kTile + 1));
   HIPCHK(s, s->dpt.alloc(3ull * P.n_pt + 1));
+  HIPCHK(s, s->wdx.alloc(3ull * P.n_edge + 1));
   ChainDev& c = s->cd;
   c.n_comp = P.n_comp;
   c.n_nb = static_cast<int>(P.nb_pose.size());
@@ -329,7 +330,7 @@ void enqueue_try(dynohip_solver* s, double lambda) {
   if (timed) (void)hipEventRecord(s->ev[5], st);
   if (timed) (void)hipEventRecord(s->ev[6], st);
   // pose deltas are x[0 .. 6 n_pose) in pose-index order
-  launch_backsub(s->cd, A, x, s->dpt.p, st);
+  launch_backsub(s->cd, P.n_edge, A, x, s->wdx.p, s->dpt.p, st);
   enqueue_linerr(s, x, s->dpt.p, s->partials.p, s->result.p);
   if (timed) (void)hipEventRecord(s->ev[7], st);
   launch_retract(P.n_pose, P.n_pt, s->pose.p, s->pt.p, x, s->dpt.p, s->pose_c.p, s->pt_c.p, st);
