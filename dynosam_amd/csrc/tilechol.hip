@@ -165,14 +165,19 @@ __device__ __forceinline__ v4d mfma_tn(const v4d& Y, const v4d& Z, v4d acc, bool
 // Factor the 64x64 tile held as upper 16x16 blocks (wave w: accA[TJ] =
 // block (w, TJ), TJ >= w, full symmetric input) and build L^-1 in accX
 // (wave w: block row w; starts as I). Four block steps KB, one barrier each:
-//   wave KB: U_KK, W = U_KK^-1 in-wave; U row KB = W^T A[KB][TJ] (TJ > KB);
-//            X row KB = W^T X[KB][TJ] (final, TJ <= KB); publish both
-//   waves v > KB: A[v][TJ] -= U[KB][v]^T U[KB][TJ] (TJ >= v),
-//                 X[v][TJ] -= U[KB][v]^T X[KB][TJ] (TJ <= KB)
+//   wave KB:   U_KK and W = U_KK^-1 in-wave; U row KB = W^T A[KB][TJ]
+//              (TJ > KB), published;
+//   wave KB-1: finishes row KB-1 of the inverse, Xf = W_{KB-1}^T X[KB-1][TJ]
+//              (TJ <= KB-1), published in the slots the U row leaves free;
+//   waves v > KB, after the barrier: A[v][TJ] -= U[KB][v]^T U[KB][TJ] (TJ >= v),
+//              and the inverse rows lagging one step,
+//              X[v][TJ] -= U[KB-1][v]^T Xf[KB-1][TJ] (TJ <= KB-1).
+// The inverse work thus runs on waves that would otherwise wait, and only
+// the last inverse row follows the final barrier. Each wave keeps its
+// previous U block and its own W in registers.
 // xch: 2 x 4 blocks x 256 doubles of LDS.
-// Hooks let the caller use otherwise idle waves: idle0() runs on waves 1-3
-// while wave 0 factors block 0 (before the first barrier), idle1() on wave 0
-// during step 1.
+// Hooks use otherwise idle waves: idle0() runs on waves 1-3 while wave 0
+// factors block 0 (before the first barrier), idle1() on wave 0 during step 1.
 struct NoHook {
   __device__ void operator()() const {}
 };
@@ -181,28 +186,48 @@ template <class Idle0 = NoHook, class Idle1 = NoHook>
 __device__ bool factor_tile_blk(v4d (&accA)[4], v4d (&accX)[4], int w, int l, double* xch, Idle0&& idle0 = Idle0(),
                                 Idle1&& idle1 = Idle1()) {
   bool ok = true;
+  v4d Wmine = v4d{0.0, 0.0, 0.0, 0.0};   // W of this wave's diagonal block
+  v4d Uprev = v4d{0.0, 0.0, 0.0, 0.0};   // U[KB-1][w]
+  v4d Udefer = v4d{0.0, 0.0, 0.0, 0.0};  // U[KB-2][w] of the deferred inverse update
+  // the inverse update of the wave that factors next is deferred past its
+  // own factorisation; xch slots < KB-1 of the previous buffer stay intact
+  // for it (nobody else writes them before it reads)
+  auto x_update = [&](const v4d& U, const double* buf, int nblk) {
+#pragma unroll
+    for (int TJ = 0; TJ < 4; ++TJ)
+      if (TJ < nblk) {
+        v4d Z;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Z[r] = buf[TJ * 256 + r * 64 + l];
+        accX[TJ] = mfma_tn(U, Z, accX[TJ], true);
+      }
+  };
 #pragma unroll
   for (int KB = 0; KB < 4; ++KB) {
     double* xb = xch + (KB & 1) * 4 * 256;
+    double* xp = xch + ((KB + 1) & 1) * 4 * 256;  // previous step's buffer
     if (KB == 0 && w != 0) idle0();
     if (KB == 1 && w == 0) idle1();
     if (w == KB) {
-      v4d W = v4d{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int r = 0; r < 4; ++r) W[r] = ((l >> 4) + 4 * r == (l & 15)) ? 1.0 : 0.0;
-      factor16_wave(accA[KB], W, l, ok);
+      for (int r = 0; r < 4; ++r) Wmine[r] = ((l >> 4) + 4 * r == (l & 15)) ? 1.0 : 0.0;
+      factor16_wave(accA[KB], Wmine, l, ok);
 #pragma unroll
-      for (int TJ = 0; TJ < 4; ++TJ) {
+      for (int TJ = KB + 1; TJ < 4; ++TJ) {
         v4d z = v4d{0.0, 0.0, 0.0, 0.0};
-        if (TJ > KB) {
-          accA[TJ] = mfma_tn(W, accA[TJ], z, false);
+        accA[TJ] = mfma_tn(Wmine, accA[TJ], z, false);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) xb[TJ * 256 + r * 64 + l] = accA[TJ][r];
-        } else {
-          accX[TJ] = mfma_tn(W, accX[TJ], z, false);
+        for (int r = 0; r < 4; ++r) xb[TJ * 256 + r * 64 + l] = accA[TJ][r];
+      }
+    }
+    if (KB >= 1 && w == KB - 1) {
+      // final inverse row KB-1 (all its updates from rows < KB-1 applied)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) xb[TJ * 256 + r * 64 + l] = accX[TJ][r];
-        }
+      for (int TJ = 0; TJ < KB; ++TJ) {
+        v4d z = v4d{0.0, 0.0, 0.0, 0.0};
+        accX[TJ] = mfma_tn(Wmine, accX[TJ], z, false);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xb[TJ * 256 + r * 64 + l] = accX[TJ][r];
       }
     }
     __syncthreads();
@@ -212,13 +237,31 @@ __device__ bool factor_tile_blk(v4d (&accA)[4], v4d (&accX)[4], int w, int l, do
       for (int r = 0; r < 4; ++r) Uv[r] = xb[w * 256 + r * 64 + l];
 #pragma unroll
       for (int TJ = 0; TJ < 4; ++TJ) {
-        if (TJ < w && TJ > KB) continue;
+        if (TJ < w) continue;
         v4d Z;
 #pragma unroll
         for (int r = 0; r < 4; ++r) Z[r] = xb[TJ * 256 + r * 64 + l];
-        if (TJ >= w) accA[TJ] = mfma_tn(Uv, Z, accA[TJ], true);
-        else accX[TJ] = mfma_tn(Uv, Z, accX[TJ], true);
+        accA[TJ] = mfma_tn(Uv, Z, accA[TJ], true);
       }
+      if (w == KB + 1) {
+        Udefer = Uprev;            // Xf[KB-1] (slots < KB of xb) applied after my factorisation
+      } else if (KB >= 1) {
+        x_update(Uprev, xb, KB);   // Xf[KB-1]
+      }
+      Uprev = Uv;
+    } else if (w == KB) {
+      // after my factorisation: the deferred Xf[KB-2] (previous buffer),
+      // then Xf[KB-1]
+      if (KB >= 2) x_update(Udefer, xp, KB - 1);
+      if (KB >= 1) x_update(Uprev, xb, KB);
+    }
+  }
+  if (w == 3) {
+    // last inverse row
+#pragma unroll
+    for (int TJ = 0; TJ < 4; ++TJ) {
+      v4d z = v4d{0.0, 0.0, 0.0, 0.0};
+      accX[TJ] = mfma_tn(Wmine, accX[TJ], z, false);
     }
   }
   return ok;

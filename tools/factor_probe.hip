@@ -11,6 +11,46 @@
 
 using namespace dynohip;
 
+// ablation: the blocked factor without the inverse (X) work
+__device__ bool factor_tile_noX(v4d (&accA)[4], int w, int l, double* xch) {
+  bool ok = true;
+#pragma unroll
+  for (int KB = 0; KB < 4; ++KB) {
+    double* xb = xch + (KB & 1) * 4 * 256;
+    if (w == KB) {
+      v4d W = v4d{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) W[r] = ((l >> 4) + 4 * r == (l & 15)) ? 1.0 : 0.0;
+      factor16_wave(accA[KB], W, l, ok);
+#pragma unroll
+      for (int TJ = 0; TJ < 4; ++TJ) {
+        v4d z = v4d{0.0, 0.0, 0.0, 0.0};
+        if (TJ > KB) {
+          accA[TJ] = mfma_tn(W, accA[TJ], z, false);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) xb[TJ * 256 + r * 64 + l] = accA[TJ][r];
+        }
+      }
+    }
+    __syncthreads();
+    if (w > KB) {
+      v4d Uv;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Uv[r] = xb[w * 256 + r * 64 + l];
+#pragma unroll
+      for (int TJ = 0; TJ < 4; ++TJ) {
+        if (TJ < w) continue;
+        v4d Z;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Z[r] = xb[TJ * 256 + r * 64 + l];
+        accA[TJ] = mfma_tn(Uv, Z, accA[TJ], true);
+      }
+    }
+  }
+  return ok;
+}
+
+
 template <int V>
 __global__ __launch_bounds__(256) void k_fact(const double* A, double* X, long long* cyc, int* okout) {
   __shared__ double buf[2 * T * 4 + 2 * 4 * T + 2 * 4 * 256];
@@ -25,7 +65,8 @@ __global__ __launch_bounds__(256) void k_fact(const double* A, double* X, long l
   __syncthreads();
   const long long t0 = clock64();
   bool ok;
-  ok = factor_tile_blk(accA, accX, w, l, buf);
+  if (V == 1) ok = factor_tile_blk(accA, accX, w, l, buf);
+  else ok = factor_tile_noX(accA, w, l, buf);
   __syncthreads();
   const long long t1 = clock64();
   for (int TJ = 0; TJ < 4; ++TJ)
@@ -66,8 +107,8 @@ int main() {
   hipMalloc(&dA, T * T * 8); hipMalloc(&dX, T * T * 8); hipMalloc(&cyc, 8 * 1024); hipMalloc(&ok, 4);
   hipMemcpy(dA, A.data(), T * T * 8, hipMemcpyHostToDevice);
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
-  for (int V = 1; V < 2; ++V) {
-    auto launch = [&](int n) { if (V == 0) k_fact<0><<<n, 256>>>(dA, dX, cyc, ok); else k_fact<1><<<n, 256>>>(dA, dX, cyc, ok); };
+  for (int V = 1; V < 3; ++V) {
+    auto launch = [&](int n) { if (V == 1) k_fact<1><<<n, 256>>>(dA, dX, cyc, ok); else k_fact<2><<<n, 256>>>(dA, dX, cyc, ok); };
     launch(1);
     hipDeviceSynchronize();
     std::vector<double> X(T * T); int okh; long long c;
