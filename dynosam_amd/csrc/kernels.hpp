@@ -94,9 +94,13 @@ void launch_tile_pad(const TileDev& b, hipStream_t s);
 // into the factorisation: contrib holds L(i,k) y_k per stored tile). Linv
 // receives the NT diagonal inverse tiles, y the forward result. One launch
 // per level of the host schedule (flevel / bplevel).
+// Wide levels (many update tasks) run their updates as a separate
+// small-LDS kernel on `side`, concurrently with the level's panels on `s`
+// (joined through ev_main / ev_side).
 void launch_tile_cholesky_solve(const TileDev& b, const TileSchedDev& sd, const std::vector<int32_t>& flevel,
-                                const std::vector<int32_t>& blevel, double* Linv, const double* r,
-                                double* contrib, double* y, double* x, int* fail, hipStream_t s);
+                                const std::vector<int32_t>& fpanels, const std::vector<int32_t>& blevel,
+                                double* Linv, const double* r, double* contrib, double* y, double* x, int* fail,
+                                hipStream_t s, hipStream_t side, hipEvent_t ev_main, hipEvent_t ev_side);
 
 void launch_retract(int n_pose, int n_pt, const double* pose, const double* pt, const double* dpose,
                     const double* dpt, double* pose_out, double* pt_out, hipStream_t s);

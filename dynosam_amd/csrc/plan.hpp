@@ -144,6 +144,7 @@ struct Plan {
   std::vector<TileTask> ftask;          // forward tasks, grouped by level
   std::vector<int32_t> pairs;           // operand pairs (A slot, B slot) of the tasks
   std::vector<int32_t> flevel;          // level l = tasks [flevel[l], flevel[l+1])
+  std::vector<int32_t> fpanels;         // panels of level l (they come first within the level)
   std::vector<BackTask> btask;
   std::vector<int32_t> blevel;
   std::vector<int32_t> bent;            // pairs (slot, row tile)

@@ -90,6 +90,8 @@ struct GatherBufs {
 struct dynohip_solver {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t side = nullptr;       // update tasks of wide factorisation levels
+  hipEvent_t ev_main = nullptr, ev_side = nullptr;
   std::string err;
   GraphCopy graph;
   bool has_graph = false;
@@ -325,8 +327,8 @@ void enqueue_try(dynohip_solver* s, double lambda) {
   double* y = s->xy.p;
   double* x = s->xy.p + nrp;
   if (++s->sd.epoch == 0) s->sd.epoch = 1;  // stamps of earlier solves never match
-  launch_tile_cholesky_solve(s->bd, s->sd, P.flevel, P.bplevel, s->linv.p, s->gred.p, s->contrib.p, y, x,
-                             s->failp, st);
+  launch_tile_cholesky_solve(s->bd, s->sd, P.flevel, P.fpanels, P.bplevel, s->linv.p, s->gred.p, s->contrib.p, y,
+                             x, s->failp, st, s->side, s->ev_main, s->ev_side);
   if (timed) (void)hipEventRecord(s->ev[5], st);
   if (timed) (void)hipEventRecord(s->ev[6], st);
   // pose deltas are x[0 .. 6 n_pose) in pose-index order
@@ -553,10 +555,13 @@ int dynohip_create(int device_id, dynohip_solver** out) {
   if (hipSetDevice(device_id) != hipSuccess) return DYNOHIP_EHIP;
   dynohip_solver* s = new dynohip_solver();
   s->device = device_id;
-  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking) != hipSuccess) {
     delete s;
     return DYNOHIP_EHIP;
   }
+  (void)hipEventCreateWithFlags(&s->ev_main, hipEventDisableTiming);
+  (void)hipEventCreateWithFlags(&s->ev_side, hipEventDisableTiming);
   for (auto& e : s->ev) (void)hipEventCreate(&e);
   dynohip_lm_params_default(&s->prm);
   *out = s;
@@ -569,6 +574,10 @@ void dynohip_destroy(dynohip_solver* s) {
   if (s->stream) (void)hipStreamSynchronize(s->stream);
   for (auto& e : s->ev)
     if (e) (void)hipEventDestroy(e);
+  if (s->side) (void)hipStreamSynchronize(s->side);
+  if (s->ev_main) (void)hipEventDestroy(s->ev_main);
+  if (s->ev_side) (void)hipEventDestroy(s->ev_side);
+  if (s->side) (void)hipStreamDestroy(s->side);
   if (s->stream) (void)hipStreamDestroy(s->stream);
   delete s;
 }

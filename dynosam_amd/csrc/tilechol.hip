@@ -316,6 +316,39 @@ __device__ __forceinline__ void load_tiles_lds(const double* const (&src)[4], do
     }
 }
 
+// dst -= sum over the task's pairs of A B^T: the destination and the first
+// pair's operands are fetched in one round trip; further pairs (rare) one
+// by one
+__device__ __forceinline__ void run_update(const TileDev& b, const TileTask& tk, const int32_t* __restrict__ pairs,
+                                           double* Qs, double* Rs, int tid, int w, int l) {
+  double* dst = slot_ptr(b, tk.dst);
+  double old[2][2][4];
+#pragma unroll
+  for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) old[ti][tj][rr] = dst[MFMA_ROW(w, l, ti, rr) * T + MFMA_COL(w, l, tj)];
+  v4d acc[2][2];
+  zero_acc(acc);
+  for (int e = tk.po_beg; e < tk.po_end; ++e) {
+    const int32_t pa = pairs[2 * e], pb = pairs[2 * e + 1];
+    if (e > tk.po_beg) __syncthreads();
+    const double* src[4] = {slot_ptr(b, pa), slot_ptr(b, pb), nullptr, nullptr};
+    double* dsts[4] = {Qs, Rs, nullptr, nullptr};
+    load_tiles_lds(src, dsts, pb != pa ? 2 : 1, tid);
+    __syncthreads();
+    mfma_abt_acc(Qs, pb != pa ? Rs : Qs, w, l, acc);
+  }
+#pragma unroll
+  for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        dst[MFMA_ROW(w, l, ti, rr) * T + MFMA_COL(w, l, tj)] = old[ti][tj][rr] - acc[ti][tj][rr];
+}
+
 // A_kk -= L(k,c) L(k,c)^T on this wave's upper blocks (w, TJ >= w), K = 64
 __device__ __forceinline__ void diag_pending(v4d (&accA)[4], const double* Ps, int w, int l) {
   const int li = l & 15, lk = l >> 4;
@@ -355,24 +388,7 @@ __global__ __launch_bounds__(256) void k_tasks(TileDev b, const TileTask* __rest
   const int tid = threadIdx.x;
   const int w = tid >> 6, l = tid & 63;
   if (tk.kind == 1) {
-    // ---- update: dst -= sum A B^T (destination prefetched under the GEMM)
-    double* dst = slot_ptr(b, tk.dst);
-    double old[2][2][4];
-#pragma unroll
-    for (int ti = 0; ti < 2; ++ti)
-#pragma unroll
-      for (int tj = 0; tj < 2; ++tj)
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) old[ti][tj][rr] = dst[MFMA_ROW(w, l, ti, rr) * T + MFMA_COL(w, l, tj)];
-    v4d acc[2][2];
-    sum_pairs(b, pairs, tk.po_beg, tk.po_end, Qs, Rs, tid, w, l, acc);
-#pragma unroll
-    for (int ti = 0; ti < 2; ++ti)
-#pragma unroll
-      for (int tj = 0; tj < 2; ++tj)
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr)
-          dst[MFMA_ROW(w, l, ti, rr) * T + MFMA_COL(w, l, tj)] = old[ti][tj][rr] - acc[ti][tj][rr];
+    run_update(b, tk, pairs, Qs, Rs, tid, w, l);
     return;
   }
   // ---- panel
@@ -493,6 +509,17 @@ __global__ __launch_bounds__(256) void k_tasks(TileDev b, const TileTask* __rest
     s += __shfl_xor(s, 2);
     if (part == 0) contrib[static_cast<int64_t>(tk.dst) * T + row] = s;
   }
+}
+
+// update tasks of a wide level: dst -= sum A B^T, with only the two
+// operand tiles in LDS (two workgroups per CU)
+__global__ __launch_bounds__(256) void k_updates(TileDev b, const TileTask* __restrict__ tasks,
+                                                 const int32_t* __restrict__ pairs) {
+  __shared__ double Qs[T * LD];
+  __shared__ double Rs[T * LD];
+  const TileTask tk = tasks[blockIdx.x];
+  const int tid = threadIdx.x;
+  run_update(b, tk, pairs, Qs, Rs, tid, tid >> 6, tid & 63);
 }
 
 // one level of the backward substitution,
@@ -699,11 +726,25 @@ __global__ __launch_bounds__(kBackThreads) void k_back_persist(TileDev b, const 
 }  // namespace
 
 void launch_tile_cholesky_solve(const TileDev& b, const TileSchedDev& sd, const std::vector<int32_t>& flevel,
-                                const std::vector<int32_t>& blevel, double* Linv, const double* r, double* contrib,
-                                double* y, double* x, int* fail, hipStream_t s) {
+                                const std::vector<int32_t>& fpanels, const std::vector<int32_t>& blevel,
+                                double* Linv, const double* r, double* contrib, double* y, double* x, int* fail,
+                                hipStream_t s, hipStream_t side, hipEvent_t ev_main, hipEvent_t ev_side) {
+  // a level is "wide" when its update tasks alone need more than one
+  // round of the CUs: they then run as k_updates on the side stream
+  constexpr int kWideUpdates = 256;
   for (size_t lv = 0; lv + 1 < flevel.size(); ++lv) {
     const int n = flevel[lv + 1] - flevel[lv];
-    if (n > 0) k_tasks<<<n, 256, 0, s>>>(b, sd.ftask + flevel[lv], sd.pairs, Linv, r, contrib, y, fail);
+    const int np = fpanels[lv], nu = n - np;
+    if (nu > kWideUpdates && side) {
+      (void)hipEventRecord(ev_main, s);
+      (void)hipStreamWaitEvent(side, ev_main, 0);
+      if (np > 0) k_tasks<<<np, 256, 0, s>>>(b, sd.ftask + flevel[lv], sd.pairs, Linv, r, contrib, y, fail);
+      k_updates<<<nu, 256, 0, side>>>(b, sd.ftask + flevel[lv] + np, sd.pairs);
+      (void)hipEventRecord(ev_side, side);
+      (void)hipStreamWaitEvent(s, ev_side, 0);
+    } else if (n > 0) {
+      k_tasks<<<n, 256, 0, s>>>(b, sd.ftask + flevel[lv], sd.pairs, Linv, r, contrib, y, fail);
+    }
   }
   const int nparts = blevel.empty() ? 0 : blevel.back();
   if (nparts > 0 && nparts <= kBackPersistMax) {

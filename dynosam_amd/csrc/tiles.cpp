@@ -46,6 +46,7 @@ struct Sched {
   int32_t n_slots = 0;
   std::vector<TileTask> ftask;
   std::vector<int32_t> flevel;
+  std::vector<int32_t> fpanels;
   std::vector<int32_t> pairs;
   std::vector<BackTask> btask;
   std::vector<int32_t> blevel;
@@ -184,7 +185,11 @@ void schedule(int NT, const std::vector<std::vector<int32_t>>& adj, const std::v
       }
   }
   S.flops = flops;
-  std::stable_sort(tasks.begin(), tasks.end(), [](const LT& x, const LT& y) { return x.lvl < y.lvl; });
+  // by level; within a level panels first, then updates (wide levels run
+  // their updates as a separate, concurrent kernel)
+  std::stable_sort(tasks.begin(), tasks.end(), [](const LT& x, const LT& y) {
+    return x.lvl != y.lvl ? x.lvl < y.lvl : x.t.kind < y.t.kind;
+  });
   S.ftask.clear();
   S.flevel.clear();
   S.pairs.clear();
@@ -204,6 +209,9 @@ void schedule(int NT, const std::vector<std::vector<int32_t>>& adj, const std::v
     S.ftask.push_back(t.t);
   }
   S.flevel.push_back(static_cast<int32_t>(S.ftask.size()));
+  S.fpanels.assign(S.flevel.size() - 1, 0);
+  for (size_t l = 0; l + 1 < S.flevel.size(); ++l)
+    for (int32_t q = S.flevel[l]; q < S.flevel[l + 1]; ++q) S.fpanels[l] += S.ftask[q].kind == 0;
   // ---- backward substitution levels
   std::vector<int32_t> blv(NT, 0);
   int maxb = 0;
@@ -229,20 +237,25 @@ void schedule(int NT, const std::vector<std::vector<int32_t>>& adj, const std::v
     }
     S.blevel.push_back(static_cast<int32_t>(S.btask.size()));
   }
-  // ---- cost model (microseconds): a launch per level; a workgroup round
-  // with a panel is dominated by the in-register diagonal factorisation
+  // ---- cost model (microseconds, calibrated with per-task clock64 stamps
+  // on MI355X): a level costs its launch plus the longer of its longest task
+  // and its total task time spread over the CUs (one 158 KB-LDS workgroup
+  // per CU). A panel is ~24 us (dominated by the in-register diagonal
+  // factorisation), an update ~5 us, plus ~1.7 us per operand pair (a 64^3
+  // FP64 MFMA GEMM on one CU).
   constexpr int kCUs = 256;
   double cost = 0.0;
   const int nlev = static_cast<int>(S.flevel.size()) - 1;
   for (int l = 0; l < nlev; ++l) {
-    const int n = S.flevel[l + 1] - S.flevel[l];
-    double worst = 0.0;
+    double worst = 0.0, total = 0.0;
     for (int32_t q = S.flevel[l]; q < S.flevel[l + 1]; ++q) {
       const TileTask& t = S.ftask[q];
       const int np = (t.pd_end - t.pd_beg) + (t.po_end - t.po_beg);
-      worst = std::max(worst, (t.kind == 0 ? 30.0 : 4.0) + 3.0 * np);
+      const double c = (t.kind == 0 ? 24.0 : 5.0) + 1.7 * np;
+      worst = std::max(worst, c);
+      total += c;
     }
-    cost += 2.0 + worst * ((n + kCUs - 1) / kCUs);
+    cost += 1.0 + std::max(worst, total / kCUs);
   }
   for (size_t l = 0; l + 1 < S.blevel.size(); ++l) cost += 4.0;
   S.cost = cost;
@@ -275,7 +288,7 @@ void build_tile_schedule(Plan& P) {
   Sched best;
   schedule(NT, adj, maxnb, g_leaf_override > 0 ? g_leaf_override : 0, best);
   if (g_leaf_override < 0) {
-    for (int leaf : {4, 6, 8, 12, 16, 24, 32, 48, 64}) {
+    for (int leaf : {4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128, 192, 256}) {
       if (leaf >= NT) break;
       Sched cand;
       schedule(NT, adj, maxnb, leaf, cand);
@@ -289,6 +302,7 @@ void build_tile_schedule(Plan& P) {
   P.ftask = std::move(best.ftask);
   P.pairs = std::move(best.pairs);
   P.flevel = std::move(best.flevel);
+  P.fpanels = std::move(best.fpanels);
   P.btask = std::move(best.btask);
   P.blevel = std::move(best.blevel);
   P.bent = std::move(best.bent);
