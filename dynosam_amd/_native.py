@@ -96,6 +96,8 @@ def _declare(name, lib):
         lib.dynohip_sliding_window_init.restype = None
         lib.dynohip_sliding_window_check.argtypes = [P(_abi.SlidingWindowState), C.c_uint64, P(C.c_uint64), P(C.c_uint64)]
         lib.dynohip_sliding_window_check.restype = C.c_int
+        lib.dynohip_set_exec_options.argtypes = [vp, C.c_int, C.c_int]
+        lib.dynohip_set_exec_options.restype = C.c_int
         lib.dynohip_set_tile_ordering.argtypes = [C.c_int]
         lib.dynohip_set_tile_ordering.restype = None
         I32 = P(C.c_int32)

@@ -62,6 +62,8 @@ struct TileSchedDev {
   int* arrive = nullptr;       // NT arrival counters (zero between launches)
   unsigned* done = nullptr;    // NT column-done stamps of the one-launch backward solve
   unsigned epoch = 0;          // stamp of the current solve (never 0)
+  int wide_updates = 256;      // levels with more update tasks use the side-stream kernel
+  bool level_backward = false; // force one backward launch per level
 };
 
 // ---- launchers (all asynchronous on `s`) ----

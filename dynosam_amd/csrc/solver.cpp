@@ -825,6 +825,13 @@ int dynohip_get_stats(dynohip_solver* s, dynohip_stats* out) {
   return DYNOHIP_OK;
 }
 
+int dynohip_set_exec_options(dynohip_solver* s, int wide_updates, int level_backward) {
+  if (!s || wide_updates < 0) return DYNOHIP_EINVAL;
+  s->sd.wide_updates = wide_updates;
+  s->sd.level_backward = level_backward != 0;
+  return DYNOHIP_OK;
+}
+
 int dynohip_set_timing(dynohip_solver* s, int enabled) {
   if (!s) return DYNOHIP_EINVAL;
   s->timing = enabled != 0;

@@ -730,12 +730,12 @@ void launch_tile_cholesky_solve(const TileDev& b, const TileSchedDev& sd, const 
                                 double* Linv, const double* r, double* contrib, double* y, double* x, int* fail,
                                 hipStream_t s, hipStream_t side, hipEvent_t ev_main, hipEvent_t ev_side) {
   // a level is "wide" when its update tasks alone need more than one
-  // round of the CUs: they then run as k_updates on the side stream
-  constexpr int kWideUpdates = 256;
+  // round of the CUs (sd.wide_updates, default 256): they then run as
+  // k_updates on the side stream
   for (size_t lv = 0; lv + 1 < flevel.size(); ++lv) {
     const int n = flevel[lv + 1] - flevel[lv];
     const int np = fpanels[lv], nu = n - np;
-    if (nu > kWideUpdates && side) {
+    if (nu > 0 && nu > sd.wide_updates && side) {
       (void)hipEventRecord(ev_main, s);
       (void)hipStreamWaitEvent(side, ev_main, 0);
       if (np > 0) k_tasks<<<np, 256, 0, s>>>(b, sd.ftask + flevel[lv], sd.pairs, Linv, r, contrib, y, fail);
@@ -747,7 +747,7 @@ void launch_tile_cholesky_solve(const TileDev& b, const TileSchedDev& sd, const 
     }
   }
   const int nparts = blevel.empty() ? 0 : blevel.back();
-  if (nparts > 0 && nparts <= kBackPersistMax) {
+  if (nparts > 0 && nparts <= kBackPersistMax && !sd.level_backward) {
     k_back_persist<<<nparts, kBackThreads, 0, s>>>(b, sd.bpart, sd.bent, Linv, y, x, sd.partials, sd.arrive, sd.done,
                                                    sd.epoch, fail);
     return;

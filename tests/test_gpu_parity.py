@@ -114,6 +114,22 @@ def test_cliques_fixture_matches_golden(gpu_available):
         assert rel(out[off[i]:off[i + 1]], ref) < PER_ITER_TOL
 
 
+@pytest.mark.parametrize("name", ["C1", "C2"])
+def test_execution_paths_agree(gpu_available, name):
+    """The concurrent update kernel (every level split) and the level-launched
+    backward substitution give the same LM iterates as the default paths:
+    the same per-task arithmetic in the same order, bit for bit."""
+    results = []
+    for opts in ({}, {"wide_updates": 0}, {"level_backward": True}, {"wide_updates": 0, "level_backward": True}):
+        g, v, _, s = make(name)
+        s.set_exec_options(**opts)
+        for _ in range(3):
+            s.iterate()
+        results.append(s.values_data())
+    for r in results[1:]:
+        assert np.array_equal(r, results[0])
+
+
 def test_llworld_formulation(gpu_available):
     g, v, _, s = make("T2", formulation=1)
     sg = s.optimize()

@@ -41,12 +41,12 @@ def main():
             "traffic_bytes_per_launch": 2.0 * sum(f) / max(len(f), 1) + sum(w) / max(len(w), 1),
         }
     # one damped solve = one k_gather_band dispatch; the factorisation is the
-    # k_tasks + k_back launches of that solve
+    # k_tasks (+ k_updates) levels and the backward launch(es) of that solve
     nsolve = kernels.get("k_gather_band", {}).get("dispatches", 0)
     fac = None
     if nsolve:
         tot = 0.0
-        for k in ("k_tasks", "k_back"):
+        for k in ("k_tasks", "k_updates", "k_back", "k_back_persist"):
             if k in kernels:
                 tot += kernels[k]["traffic_bytes_per_launch"] * kernels[k]["dispatches"]
         fac = tot / nsolve
