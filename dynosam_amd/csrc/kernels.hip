@@ -11,6 +11,8 @@
 // bit-reproducible run to run.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "kernels.hpp"
 #include "se3.hpp"
 
@@ -275,13 +277,14 @@ __device__ __forceinline__ void factor_vars(const TypeDev& tp, int i, const doub
   }
 }
 
+// ---- per-factor bodies ----------------------------------------------------
 // NoiseModelFactor::linearize: b = -r; whiten (x 1/sigma); Robust Huber block
-// reweight by sqrt(w(||b||)) (RGBDBackendModule.cc:97-113)
+// reweight by sqrt(w(||b||)) (RGBDBackendModule.cc:97-113). Returns the
+// factor's linear error at delta = 0, 0.5 ||b||^2, summed exactly as
+// linerr_one sums it (0 - b is exact), so the fused value is bit-identical.
 template <int T>
-__global__ __launch_bounds__(kBlock) void k_linearize(TypeDev tp, const double* __restrict__ pose,
-                                                      const double* __restrict__ pt, double* __restrict__ arena) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= tp.n) return;
+__device__ __forceinline__ double linearize_one(const TypeDev& tp, int i, const double* __restrict__ pose,
+                                                const double* __restrict__ pt, double* __restrict__ arena) {
   constexpr int d = kDim[T], cols = kCols[T], nk = kNKeys[T];
   const double* v[4];
   factor_vars<T>(tp, i, pose, pt, v);
@@ -319,84 +322,180 @@ __global__ __launch_bounds__(kBlock) void k_linearize(TypeDev tp, const double* 
       }
     }
   }
+  double e = 0.0;
 #pragma unroll
-  for (int k = 0; k < d; ++k) rec[d * cols + k] = hk > 0.0 ? b[k] * sw : b[k];
+  for (int k = 0; k < d; ++k) {
+    const double bk = hk > 0.0 ? b[k] * sw : b[k];
+    rec[d * cols + k] = bk;
+    const double rk = 0.0 - bk;
+    e += rk * rk;
+  }
+  return e * 0.5;
 }
 
 // NoiseModelFactor::error: Gaussian 0.5 d^2, Robust Huber rho(sqrt(d^2))
 template <int T>
-__global__ __launch_bounds__(kBlock) void k_error(TypeDev tp, const double* __restrict__ pose,
-                                                  const double* __restrict__ pt, double* __restrict__ partials) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  double e = 0.0;
-  if (i < tp.n) {
-    constexpr int d = kDim[T];
-    const double* v[4];
-    factor_vars<T>(tp, i, pose, pt, v);
-    const double* meas = kMeasDim[T] ? tp.meas + static_cast<int64_t>(i) * kMeasDim[T] : nullptr;
-    double r[6];
-    residual<T>(v, meas, r);
-    double d2 = 0.0;
+__device__ __forceinline__ double error_one(const TypeDev& tp, int i, const double* __restrict__ pose,
+                                            const double* __restrict__ pt) {
+  constexpr int d = kDim[T];
+  const double* v[4];
+  factor_vars<T>(tp, i, pose, pt, v);
+  const double* meas = kMeasDim[T] ? tp.meas + static_cast<int64_t>(i) * kMeasDim[T] : nullptr;
+  double r[6];
+  residual<T>(v, meas, r);
+  double d2 = 0.0;
 #pragma unroll
-    for (int k = 0; k < d; ++k) {
-      const double w = r[k] * tp.isig[static_cast<int64_t>(i) * d + k];
-      d2 += w * w;
-    }
-    const double hk = tp.hk[i];
-    if (hk > 0.0) {
-      const double a = sqrt(d2);
-      e = a <= hk ? a * a / 2 : hk * (a - (hk / 2));
-    } else {
-      e = 0.5 * d2;
-    }
+  for (int k = 0; k < d; ++k) {
+    const double w = r[k] * tp.isig[static_cast<int64_t>(i) * d + k];
+    d2 += w * w;
   }
-  const double s = block_sum(e);
-  if (threadIdx.x == 0) partials[blockIdx.x] = s;
+  const double hk = tp.hk[i];
+  if (hk > 0.0) {
+    const double a = sqrt(d2);
+    return a <= hk ? a * a / 2 : hk * (a - (hk / 2));
+  }
+  return 0.5 * d2;
 }
 
 // JacobianFactor::error(delta) = 0.5 ||A delta - b||^2
 template <int T>
-__global__ __launch_bounds__(kBlock) void k_linerr(TypeDev tp, const double* __restrict__ arena,
-                                                   const double* __restrict__ dpose, const double* __restrict__ dpt,
-                                                   double* __restrict__ partials) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ double linerr_one(const TypeDev& tp, int i, const double* __restrict__ arena,
+                                             const double* __restrict__ dpose, const double* __restrict__ dpt) {
+  constexpr int d = kDim[T], cols = kCols[T], nk = kNKeys[T];
+  const double* rec = arena + tp.base + static_cast<uint64_t>(tp.stride) * i;
+  double acc[6];
+#pragma unroll
+  for (int k = 0; k < d; ++k) acc[k] = 0.0;
+  if (dpose) {
+#pragma unroll
+    for (int s = 0; s < nk; ++s) {
+      const int id = tp.idx[i * nk + s];
+      const bool ps = kSlotKind[T][s] == 0;
+      const int ds = ps ? 6 : 3;
+      const double* dl = ps ? dpose + 6ll * id : dpt + 3ll * id;
+      const double* blk = rec + d * kColStart[T][s];
+#pragma unroll
+      for (int k = 0; k < d; ++k)
+#pragma unroll
+        for (int c = 0; c < 6; ++c)
+          if (c < ds) acc[k] += blk[k * ds + c] * dl[c];
+    }
+  }
   double e = 0.0;
-  if (i < tp.n) {
-    constexpr int d = kDim[T], cols = kCols[T], nk = kNKeys[T];
-    const double* rec = arena + tp.base + static_cast<uint64_t>(tp.stride) * i;
-    double acc[6];
 #pragma unroll
-    for (int k = 0; k < d; ++k) acc[k] = 0.0;
-    if (dpose) {
-#pragma unroll
-      for (int s = 0; s < nk; ++s) {
-        const int id = tp.idx[i * nk + s];
-        const bool ps = kSlotKind[T][s] == 0;
-        const int ds = ps ? 6 : 3;
-        const double* dl = ps ? dpose + 6ll * id : dpt + 3ll * id;
-        const double* blk = rec + d * kColStart[T][s];
-#pragma unroll
-        for (int k = 0; k < d; ++k)
-#pragma unroll
-          for (int c = 0; c < 6; ++c)
-            if (c < ds) acc[k] += blk[k * ds + c] * dl[c];
+  for (int k = 0; k < d; ++k) {
+    const double r = acc[k] - rec[d * cols + k];
+    e += r * r;
+  }
+  return e * 0.5;
+}
+
+// ---- type groups ------------------------------------------------------------
+// One launch covers every factor type of a group (a bit mask over types):
+// block b belongs to the type whose [bstart[T], bstart[T+1]) holds it, so a
+// block is uniform in type and the per-type block numbering, and with it the
+// partial-sum layout, is the same as one launch per type. Types outside the
+// mask span no blocks.
+struct GroupDev {
+  TypeDev t[kNTypes];
+  int bstart[kNTypes + 1];
+  int pbase;   // partial slot of this launch's block 0
+};
+
+// Sum of per-block partials. The last launch of a sum (out != nullptr) folds
+// the final reduction into its last-arriving block: partial stores and loads
+// bypass the non-coherent L2 (sc1, as the backward solve's hand-off does), the
+// arrival counter is reset for the next sum, and the fixed strided order of
+// the old single-block reduction is kept, so the result is deterministic.
+struct SumDev {
+  double* partials = nullptr;
+  unsigned* counter = nullptr;
+  double* out = nullptr;
+  int total = 0;
+};
+
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <unsigned M, int T = 0, class F>
+__device__ __forceinline__ double group_apply(const GroupDev& g, int b, F&& f) {
+  if constexpr (T == kNTypes) {
+    return 0.0;
+  } else {
+    if constexpr (((M >> T) & 1u) != 0u) {
+      if (b < g.bstart[T + 1]) {
+        const int i = (b - g.bstart[T]) * kBlock + static_cast<int>(threadIdx.x);
+        return i < g.t[T].n ? f(std::integral_constant<int, T>{}, i) : 0.0;
       }
     }
-#pragma unroll
-    for (int k = 0; k < d; ++k) {
-      const double r = acc[k] - rec[d * cols + k];
-      e += r * r;
-    }
-    e *= 0.5;
+    return group_apply<M, T + 1>(g, b, f);
   }
+}
+
+__device__ __forceinline__ double sum_strided(const double* __restrict__ p, int n, bool coherent) {
+  double v = 0.0;
+  for (int i = threadIdx.x; i < n; i += kBlock) v += coherent ? ld_sc1(p + i) : p[i];
+  return block_sum(v);
+}
+
+__device__ __forceinline__ void group_finish(double e, const GroupDev& g, const SumDev& sd) {
   const double s = block_sum(e);
-  if (threadIdx.x == 0) partials[blockIdx.x] = s;
+  double* slot = sd.partials + g.pbase + blockIdx.x;
+  if (!sd.out) {
+    if (threadIdx.x == 0) *slot = s;
+    return;
+  }
+  __shared__ int last;
+  if (threadIdx.x == 0) {
+    st_sc1(slot, s);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = __hip_atomic_fetch_add(sd.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = prev == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  const double r = sum_strided(sd.partials, sd.total, true);
+  if (threadIdx.x == 0) {
+    *sd.out = r;
+    __hip_atomic_store(sd.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+template <unsigned M>
+__global__ __launch_bounds__(kBlock) void k_linearize(GroupDev g, const double* __restrict__ pose,
+                                                      const double* __restrict__ pt, double* __restrict__ arena,
+                                                      SumDev sd) {
+  const double e = group_apply<M>(g, blockIdx.x, [&](auto tc, int i) {
+    return linearize_one<decltype(tc)::value>(g.t[decltype(tc)::value], i, pose, pt, arena);
+  });
+  group_finish(e, g, sd);
+}
+
+template <unsigned M>
+__global__ __launch_bounds__(kBlock) void k_error(GroupDev g, const double* __restrict__ pose,
+                                                  const double* __restrict__ pt, SumDev sd) {
+  const double e = group_apply<M>(g, blockIdx.x, [&](auto tc, int i) {
+    return error_one<decltype(tc)::value>(g.t[decltype(tc)::value], i, pose, pt);
+  });
+  group_finish(e, g, sd);
+}
+
+template <unsigned M>
+__global__ __launch_bounds__(kBlock) void k_linerr(GroupDev g, const double* __restrict__ arena,
+                                                   const double* __restrict__ dpose, const double* __restrict__ dpt,
+                                                   SumDev sd) {
+  const double e = group_apply<M>(g, blockIdx.x, [&](auto tc, int i) {
+    return linerr_one<decltype(tc)::value>(g.t[decltype(tc)::value], i, arena, dpose, dpt);
+  });
+  group_finish(e, g, sd);
 }
 
 __global__ __launch_bounds__(kBlock) void k_reduce(const double* __restrict__ partials, int n, double* out) {
-  double v = 0.0;
-  for (int i = threadIdx.x; i < n; i += kBlock) v += partials[i];
-  const double s = block_sum(v);
+  const double s = sum_strided(partials, n, false);
   if (threadIdx.x == 0) *out = s;
 }
 
@@ -850,36 +949,102 @@ __global__ __launch_bounds__(kBlock) void k_retract(int n_pose, int n_pt, const 
 }  // namespace
 
 // ---------------------------------------------------------------- launchers
-#define DH_DISPATCH(type, KERNEL, grid, ...)                                        \
-  switch (type) {                                                                    \
-    case 0: KERNEL<0><<<grid, kBlock, 0, s>>>(__VA_ARGS__); break;                   \
-    case 1: KERNEL<1><<<grid, kBlock, 0, s>>>(__VA_ARGS__); break;                   \
-    case 2: KERNEL<2><<<grid, kBlock, 0, s>>>(__VA_ARGS__); break;                   \
-    case 3: KERNEL<3><<<grid, kBlock, 0, s>>>(__VA_ARGS__); break;                   \
-    case 4: KERNEL<4><<<grid, kBlock, 0, s>>>(__VA_ARGS__); break;                   \
-    default: KERNEL<5><<<grid, kBlock, 0, s>>>(__VA_ARGS__); break;                  \
+// Launch groups: PoseToPoint alone (it dominates the factor count and keeps
+// its own occupancy), the low-count Ternary/Between/Prior together, and the
+// two LLWorld types alone (their register counts would cap the others).
+constexpr unsigned kGroups[] = {1u << 0, (1u << 1) | (1u << 2) | (1u << 3), 1u << 4, 1u << 5};
+constexpr int kNGroups = sizeof(kGroups) / sizeof(kGroups[0]);
+
+#define DH_GROUP_DISPATCH(g, KERNEL, grid, ...)                                   \
+  switch (g) {                                                                     \
+    case 0: KERNEL<kGroups[0]><<<grid, kBlock, 0, s>>>(__VA_ARGS__); break;        \
+    case 1: KERNEL<kGroups[1]><<<grid, kBlock, 0, s>>>(__VA_ARGS__); break;        \
+    case 2: KERNEL<kGroups[2]><<<grid, kBlock, 0, s>>>(__VA_ARGS__); break;        \
+    default: KERNEL<kGroups[3]><<<grid, kBlock, 0, s>>>(__VA_ARGS__); break;       \
   }
 
-void launch_linearize(int type, const TypeDev& t, const double* pose, const double* pt, double* arena, hipStream_t s) {
-  if (t.n == 0) return;
-  DH_DISPATCH(type, k_linearize, nblocks(t.n), t, pose, pt, arena);
+namespace {
+// per-launch block ranges; partial slots follow type order across launches
+struct GroupPlan {
+  GroupDev dev[kNGroups];
+  int blocks[kNGroups];
+  int total = 0, last = -1;
+};
+
+GroupPlan plan_groups(const TypeDev* td) {
+  GroupPlan gp;
+  int tstart[kNTypes + 1];
+  tstart[0] = 0;
+  for (int t = 0; t < kNTypes; ++t) tstart[t + 1] = tstart[t] + nblocks(td[t].n);
+  gp.total = tstart[kNTypes];
+  for (int g = 0; g < kNGroups; ++g) {
+    GroupDev& d = gp.dev[g];
+    int lo = -1, b = 0;
+    for (int t = 0; t < kNTypes; ++t) {
+      d.t[t] = td[t];
+      d.bstart[t] = b;
+      if ((kGroups[g] >> t) & 1u) {
+        if (lo < 0) lo = tstart[t];
+        b += nblocks(td[t].n);
+      } else {
+        d.t[t].n = 0;
+      }
+    }
+    d.bstart[kNTypes] = b;
+    d.pbase = lo < 0 ? 0 : lo;
+    gp.blocks[g] = b;
+    if (b > 0) gp.last = g;
+  }
+  return gp;
 }
 
-int error_blocks(int n) { return nblocks(n); }
+// the types of a group must be contiguous in type order for pbase to hold
+static_assert(kGroups[1] == 0xEu, "group 1 must cover types 1..3 contiguously");
 
-void launch_error(int type, const TypeDev& t, const double* pose, const double* pt, double* partials, hipStream_t s) {
-  if (t.n == 0) return;
-  DH_DISPATCH(type, k_error, nblocks(t.n), t, pose, pt, partials);
+SumDev sum_for(const GroupPlan& gp, int g, double* partials, unsigned* counter, double* out) {
+  SumDev sd;
+  sd.partials = partials;
+  sd.total = gp.total;
+  if (g == gp.last && out) {
+    sd.counter = counter;
+    sd.out = out;
+  }
+  return sd;
+}
+}  // namespace
+
+int error_blocks(const TypeDev* td) { return plan_groups(td).total; }
+
+void launch_linearize(const TypeDev* td, const double* pose, const double* pt, double* arena, double* partials,
+                      unsigned* counter, double* out, hipStream_t s) {
+  const GroupPlan gp = plan_groups(td);
+  for (int g = 0; g < kNGroups; ++g) {
+    if (gp.blocks[g] == 0) continue;
+    DH_GROUP_DISPATCH(g, k_linearize, gp.blocks[g], gp.dev[g], pose, pt, arena,
+                      sum_for(gp, g, partials, counter, out));
+  }
+  if (gp.last < 0 && out) k_reduce<<<1, kBlock, 0, s>>>(partials, 0, out);
 }
 
-void launch_linerr(int type, const TypeDev& t, const double* arena, const double* dpose, const double* dpt,
-                   double* partials, hipStream_t s) {
-  if (t.n == 0) return;
-  DH_DISPATCH(type, k_linerr, nblocks(t.n), t, arena, dpose, dpt, partials);
+void launch_error(const TypeDev* td, const double* pose, const double* pt, double* partials, unsigned* counter,
+                  double* out, hipStream_t s) {
+  const GroupPlan gp = plan_groups(td);
+  for (int g = 0; g < kNGroups; ++g) {
+    if (gp.blocks[g] == 0) continue;
+    DH_GROUP_DISPATCH(g, k_error, gp.blocks[g], gp.dev[g], pose, pt, sum_for(gp, g, partials, counter, out));
+  }
+  if (gp.last < 0) k_reduce<<<1, kBlock, 0, s>>>(partials, 0, out);
 }
 
-void launch_reduce(const double* partials, int n, double* out, hipStream_t s) {
-  k_reduce<<<1, kBlock, 0, s>>>(partials, n, out);
+void launch_linerr(const TypeDev* td, const double* arena, const double* dpose, const double* dpt, double* partials,
+                   unsigned* counter, double* out, hipStream_t s) {
+  const GroupPlan gp = plan_groups(td);
+  for (int g = 0; g < kNGroups; ++g) {
+    if (gp.blocks[g] == 0) continue;
+    DH_GROUP_DISPATCH(g, k_linerr, gp.blocks[g], gp.dev[g], arena, dpose, dpt,
+                      sum_for(gp, g, partials, counter, out));
+  }
+  if (gp.last < 0) k_reduce<<<1, kBlock, 0, s>>>(partials, 0, out);
 }
 
 void launch_gather_3x3(const GatherDev& g, const double* arena, double* dst, hipStream_t s) {

@@ -67,14 +67,17 @@ struct TileSchedDev {
 };
 
 // ---- launchers (all asynchronous on `s`) ----
-void launch_linearize(int type, const TypeDev& t, const double* pose, const double* pt, double* arena, hipStream_t s);
-// per-factor nonlinear error, block partial sums written at partials[0..]
-int error_blocks(int n);
-void launch_error(int type, const TypeDev& t, const double* pose, const double* pt, double* partials, hipStream_t s);
-// 0.5 || J delta - b ||^2 per factor (delta null -> 0.5||b||^2)
-void launch_linerr(int type, const TypeDev& t, const double* arena, const double* dpose, const double* dpt,
-                   double* partials, hipStream_t s);
-void launch_reduce(const double* partials, int n, double* out, hipStream_t s);
+// Factor kernels, one launch per type group. Partials are laid out in type
+// order (error_blocks slots). With out != nullptr the last launch also sums
+// all partials into *out (counter: a zeroed device word, left zeroed);
+// launch_linearize's sum is the linear error at delta = 0.
+int error_blocks(const TypeDev* td);
+void launch_linearize(const TypeDev* td, const double* pose, const double* pt, double* arena, double* partials,
+                      unsigned* counter, double* out, hipStream_t s);
+void launch_error(const TypeDev* td, const double* pose, const double* pt, double* partials, unsigned* counter,
+                  double* out, hipStream_t s);
+void launch_linerr(const TypeDev* td, const double* arena, const double* dpose, const double* dpt, double* partials,
+                   unsigned* counter, double* out, hipStream_t s);
 
 // point-side gathers (thread per target), dst = arena + off
 void launch_gather_3x3(const GatherDev& g, const double* arena, double* dst, hipStream_t s);

@@ -116,6 +116,7 @@ struct dynohip_solver {
   DevBuf<int> arrive;
   DevBuf<unsigned> done;
   DevBuf<double> partials, result;
+  DevBuf<unsigned> sumctr;   // arrival counter of the folded reductions
   int* failp = nullptr;  // inside `result` (doubles [0..3] results, [4] fail flag as int)
   int partial_slots = 0;
   ChainDev cd;
@@ -188,11 +189,13 @@ int upload_plan(dynohip_solver* s) {
     d.meas = s->tb[t].meas.p;
     d.isig = s->tb[t].isig.p;
     d.hk = s->tb[t].hk.p;
-    slots += error_blocks(tp.n);
   }
+  slots = std::max(1, error_blocks(s->td));
   s->partial_slots = slots;
   HIPCHK(s, s->partials.alloc(2ull * slots));
   HIPCHK(s, s->result.alloc(8));
+  HIPCHK(s, s->sumctr.alloc(1));
+  HIPCHK(s, hipMemsetAsync(s->sumctr.p, 0, sizeof(unsigned), st));
   s->failp = reinterpret_cast<int*>(s->result.p + 4);
   if (upload_gather(s, P.gD, s->gD) || upload_gather(s, P.gE, s->gE) || upload_gather(s, P.gGp, s->gGp) ||
       upload_gather(s, P.gW, s->gW) || upload_gather(s, P.gRed, s->gRed) || upload_gather(s, P.gGred, s->gGred))
@@ -270,21 +273,11 @@ int upload_plan(dynohip_solver* s) {
 
 // error at (pose, pt) into result[slot]
 void enqueue_error(dynohip_solver* s, const double* pose, const double* pt, double* partials, double* out) {
-  int off = 0;
-  for (int t = 0; t < kNTypes; ++t) {
-    launch_error(t, s->td[t], pose, pt, partials + off, s->stream);
-    off += error_blocks(s->td[t].n);
-  }
-  launch_reduce(partials, off, out, s->stream);
+  launch_error(s->td, pose, pt, partials, s->sumctr.p, out, s->stream);
 }
 
 void enqueue_linerr(dynohip_solver* s, const double* dpose, const double* dpt, double* partials, double* out) {
-  int off = 0;
-  for (int t = 0; t < kNTypes; ++t) {
-    launch_linerr(t, s->td[t], s->arena.p, dpose, dpt, partials + off, s->stream);
-    off += error_blocks(s->td[t].n);
-  }
-  launch_reduce(partials, off, out, s->stream);
+  launch_linerr(s->td, s->arena.p, dpose, dpt, partials, s->sumctr.p, out, s->stream);
 }
 
 int compute_error(dynohip_solver* s, const double* pose, const double* pt, double* err_out) {
@@ -294,11 +287,12 @@ int compute_error(dynohip_solver* s, const double* pose, const double* pt, doubl
   return 0;
 }
 
-// linearisation + point-side blocks (once per outer iteration)
-void enqueue_linearize(dynohip_solver* s, const double* pose, const double* pt) {
+// linearisation + point-side blocks (once per outer iteration); lin0, when
+// given, receives the linear error at delta = 0 (0.5 ||b||^2)
+void enqueue_linearize(dynohip_solver* s, const double* pose, const double* pt, double* lin0 = nullptr) {
   Plan& P = s->plan;
   double* A = s->arena.p;
-  for (int t = 0; t < kNTypes; ++t) launch_linearize(t, s->td[t], pose, pt, A, s->stream);
+  launch_linearize(s->td, pose, pt, A, s->partials.p, s->sumctr.p, lin0, s->stream);
   launch_gather_3x3(s->gD.dev(P.gD.ntargets()), A, A + P.off_D, s->stream);
   launch_gather_3x3(s->gE.dev(P.gE.ntargets()), A, A + P.off_E, s->stream);
   launch_gather_3x1(s->gGp.dev(P.gGp.ntargets()), A, A + P.off_gp, s->stream);
@@ -409,9 +403,8 @@ int lm_iterate(dynohip_solver* s) {
     have_old = true;
   } else {
     if (s->timing) (void)hipEventRecord(s->ev[0], st);
-    enqueue_linearize(s, s->pose.p, s->pt.p);
+    enqueue_linearize(s, s->pose.p, s->pt.p, s->result.p + 2);
     if (s->timing) (void)hipEventRecord(s->ev[1], st);
-    enqueue_linerr(s, nullptr, nullptr, s->partials.p, s->result.p + 2);
   }
   s->lin_valid = false;
   s->n_lin++;
@@ -431,8 +424,7 @@ int lm_iterate(dynohip_solver* s) {
     }
     enqueue_try(s, s->lambda);
     if (speculate) {
-      enqueue_linearize(s, s->pose_c.p, s->pt_c.p);
-      enqueue_linerr(s, nullptr, nullptr, s->partials.p, s->result.p + 3);
+      enqueue_linearize(s, s->pose_c.p, s->pt_c.p, s->result.p + 3);
     }
     double res[5];
     HIPCHK(s, hipMemcpyAsync(res, s->result.p, 5 * sizeof(double), hipMemcpyDeviceToHost, st));
