@@ -411,6 +411,8 @@ struct SumDev {
   double* partials = nullptr;
   unsigned* counter = nullptr;
   double* out = nullptr;
+  int* fail_src = nullptr;   // optional: moved to *fail_dst and cleared by the finisher
+  int* fail_dst = nullptr;
   int total = 0;
 };
 
@@ -419,6 +421,14 @@ __device__ __forceinline__ double ld_sc1(const double* p) {
 }
 __device__ __forceinline__ void st_sc1(double* p, double v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// hands the solve's accumulated failure bits to the result word and clears
+// them for the next solve (the flag is never memset per solve)
+__device__ __forceinline__ void move_fail(const SumDev& sd) {
+  if (!sd.fail_src) return;
+  *sd.fail_dst = __hip_atomic_load(sd.fail_src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(sd.fail_src, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <unsigned M, int T = 0, class F>
@@ -461,6 +471,7 @@ __device__ __forceinline__ void group_finish(double e, const GroupDev& g, const 
   const double r = sum_strided(sd.partials, sd.total, true);
   if (threadIdx.x == 0) {
     *sd.out = r;
+    move_fail(sd);
     __hip_atomic_store(sd.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -494,9 +505,12 @@ __global__ __launch_bounds__(kBlock) void k_linerr(GroupDev g, const double* __r
   group_finish(e, g, sd);
 }
 
-__global__ __launch_bounds__(kBlock) void k_reduce(const double* __restrict__ partials, int n, double* out) {
-  const double s = sum_strided(partials, n, false);
-  if (threadIdx.x == 0) *out = s;
+__global__ __launch_bounds__(kBlock) void k_reduce(SumDev sd) {
+  const double s = sum_strided(sd.partials, sd.total, false);
+  if (threadIdx.x == 0) {
+    *sd.out = s;
+    move_fail(sd);
+  }
 }
 
 // ---------------------------------------------------------------- gathers
@@ -611,30 +625,37 @@ __device__ __forceinline__ void group_accumulate(const int64_t* __restrict__ sta
 }
 
 template <int R, int CC>
-__global__ __launch_bounds__(kBlock) void k_gather_thread(const int64_t* __restrict__ start,
-                                                          const GEntry* __restrict__ ent, int nt,
-                                                          const double* __restrict__ arena,
-                                                          double* __restrict__ dst) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nt) return;
+__device__ __forceinline__ void gather_thread(const GatherDev& g, int blk, const double* __restrict__ arena,
+                                              double* __restrict__ dst) {
+  const int t = blk * kBlock + static_cast<int>(threadIdx.x);
+  if (t >= g.n) return;
   double acc[R * CC];
-  group_accumulate<R, CC, 1>(start, ent, t, 0, arena, acc);
+  group_accumulate<R, CC, 1>(g.start, g.ent, t, 0, arena, acc);
   double* o = dst + static_cast<int64_t>(t) * R * CC;
 #pragma unroll
   for (int j = 0; j < R * CC; ++j) o[j] = acc[j];
 }
 
+// the point-side blocks of one linearisation in one launch, a thread per
+// target: D (3x3 per point), E (3x3 per chain link), g_p (3 per point) and
+// W (3x6 per point-pose edge), in block ranges of that order
+__global__ __launch_bounds__(kBlock) void k_gather_point(PointGatherDev p, const double* __restrict__ arena) {
+  const int b = blockIdx.x;
+  if (b < p.bstart[1]) gather_thread<3, 3>(p.g[0], b, arena, p.dst[0]);
+  else if (b < p.bstart[2]) gather_thread<3, 3>(p.g[1], b - p.bstart[1], arena, p.dst[1]);
+  else if (b < p.bstart[3]) gather_thread<3, 1>(p.g[2], b - p.bstart[2], arena, p.dst[2]);
+  else gather_thread<3, 6>(p.g[3], b - p.bstart[3], arena, p.dst[3]);
+}
+
 // a wave per 6x6 target
-__global__ __launch_bounds__(kBlock) void k_gather_band(const int64_t* __restrict__ start,
-                                                        const GEntry* __restrict__ ent, int nt,
-                                                        const double* __restrict__ arena,
-                                                        const int32_t* __restrict__ tA,
-                                                        const int32_t* __restrict__ tB, TileDev b, double lambda) {
-  const int t = (xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x) >> 6;
+__device__ __forceinline__ void gather_band(const GatherDev& g, const int32_t* __restrict__ tA,
+                                            const int32_t* __restrict__ tB, int blk,
+                                            const double* __restrict__ arena, const TileDev& b, double lambda) {
+  const int t = (blk * kBlock + static_cast<int>(threadIdx.x)) >> 6;
   const int q = threadIdx.x & 63;
-  if (t >= nt) return;
+  if (t >= g.n) return;
   double acc[36], a18[18], a9[9], a5[5], a3[3], a2[2], a1[1];
-  group_accumulate<6, 6, 64, 1>(start, ent, t, q, arena, acc);
+  group_accumulate<6, 6, 64, 1>(g.start, g.ent, t, q, arena, acc);
   rs_step<36, 32>(acc, a18, q & 32);
   rs_step<18, 16>(a18, a9, q & 16);
   rs_step<9, 8>(a9, a5, q & 8);
@@ -659,14 +680,13 @@ __global__ __launch_bounds__(kBlock) void k_gather_band(const int64_t* __restric
 }
 
 // a wave per pose gradient
-__global__ __launch_bounds__(kBlock) void k_gather_grad(const int64_t* __restrict__ start,
-                                                        const GEntry* __restrict__ ent, int nt,
-                                                        const double* __restrict__ arena, double* __restrict__ gred) {
-  const int t = (xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x) >> 6;
+__device__ __forceinline__ void gather_grad(const GatherDev& g, int blk, const double* __restrict__ arena,
+                                            double* __restrict__ gred) {
+  const int t = (blk * kBlock + static_cast<int>(threadIdx.x)) >> 6;
   const int q = threadIdx.x & 63;
-  if (t >= nt) return;
+  if (t >= g.n) return;
   double acc[6], a3[3], a2[2], a1[1], b1[1], c1[1], d1[1];
-  group_accumulate<6, 1, 64>(start, ent, t, q, arena, acc);
+  group_accumulate<6, 1, 64>(g.start, g.ent, t, q, arena, acc);
   rs_step<6, 32>(acc, a3, q & 32);
   rs_step<3, 16>(a3, a2, q & 16);
   rs_step<2, 8>(a2, a1, q & 8);
@@ -675,6 +695,26 @@ __global__ __launch_bounds__(kBlock) void k_gather_grad(const int64_t* __restric
   rs_step<1, 1>(c1, d1, q & 1);
   const int idx = rs_index<6>(q);
   if (idx >= 0) gred[6 * t + idx] = d1[0];
+}
+
+// the reduced system of one solve in one launch: the 6x6 blocks of
+// S = H_cc - W D^-1 W^T (+ lambda on the diagonal) into their tiles, the
+// reduced gradient, and the identity on the padding rows of the last tile.
+// Each part's blocks are remapped so that consecutive targets share an
+// XCD's L2; the parts start at multiples of 8 blocks (the XCD count), so each
+// part is spread over all XCDs (one remap over the whole grid would leave the
+// light gradient blocks to the last XCDs).
+__global__ __launch_bounds__(kBlock) void k_gather_reduced(ReducedGatherDev r, const double* __restrict__ arena,
+                                                           TileDev b, double lambda) {
+  const int hb = blockIdx.x;
+  if (hb < r.nb_band) {
+    gather_band(r.band, r.tA, r.tB, xcd_block(hb, r.nb_band), arena, b, lambda);
+  } else if (hb < r.nb_band + r.nb_grad) {
+    gather_grad(r.grad, xcd_block(hb - r.nb_band, r.nb_grad), arena, r.gred);
+  } else {
+    const int row = b.n_red + (hb - r.nb_band - r.nb_grad) * kBlock + static_cast<int>(threadIdx.x);
+    if (row < b.NT * kTile) b.slots[tile_index(b, row, row)] = 1.0;
+  }
 }
 
 // ---------------------------------------------------------------- chains
@@ -746,8 +786,23 @@ __device__ __forceinline__ void ldk(const double* __restrict__ src, double (&dst
 //   M_i = E_{i-1} L_{i-1}^-T, L_i L_i^T = D_i + lambda I - M_i M_i^T;
 // then v = C^-1 gp. Thread per chain; the next point's D, g_p and E are
 // fetched while the current point is factored.
+// Blocks past the chains zero the solve's accumulation buffers (the tile
+// slots the reduced gather scatters into, the reduced gradient) in 16-byte
+// stores, in place of separate memsets.
 __global__ __launch_bounds__(kBlock) void k_chain_factor(ChainDev cd, double* __restrict__ arena, double lambda,
-                                                         int* fail) {
+                                                         int* fail, ZeroDev zb) {
+  const int nbc = (cd.n_comp + kBlock - 1) / kBlock;
+  if (static_cast<int>(blockIdx.x) >= nbc) {
+    const int64_t stride = static_cast<int64_t>(gridDim.x - nbc) * kBlock;
+    const int64_t i0 = static_cast<int64_t>(blockIdx.x - nbc) * kBlock + threadIdx.x;
+    const double2 zero = {0.0, 0.0};
+    for (int k = 0; k < 2; ++k) {
+      double2* p = reinterpret_cast<double2*>(k == 0 ? zb.p0 : zb.p1);
+      const int64_t n = (k == 0 ? zb.n0 : zb.n1) / 2;
+      for (int64_t i = i0; i < n; i += stride) p[i] = zero;
+    }
+    return;
+  }
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= cd.n_comp) return;
   const int i0 = cd.comp_start[c], i1 = cd.comp_start[c + 1];
@@ -919,13 +974,6 @@ __global__ __launch_bounds__(kBlock) void k_backsub(ChainDev cd, const double* _
   }
 }
 
-// ---------------------------------------------------------------- band
-__global__ void k_tile_pad(TileDev b) {
-  const int row = b.n_red + blockIdx.x * blockDim.x + threadIdx.x;
-  if (row >= b.NT * kTile) return;
-  b.slots[tile_index(b, row, row)] = 1.0;
-}
-
 // ---------------------------------------------------------------- retract
 __global__ __launch_bounds__(kBlock) void k_retract(int n_pose, int n_pt, const double* __restrict__ pose,
                                                     const double* __restrict__ pt, const double* __restrict__ dpose,
@@ -1011,6 +1059,16 @@ SumDev sum_for(const GroupPlan& gp, int g, double* partials, unsigned* counter, 
   }
   return sd;
 }
+
+// no factors: the sum is 0
+void launch_empty_sum(double* partials, double* out, int* fail_src, int* fail_dst, hipStream_t s) {
+  SumDev sd;
+  sd.partials = partials;
+  sd.out = out;
+  sd.fail_src = fail_src;
+  sd.fail_dst = fail_dst;
+  k_reduce<<<1, kBlock, 0, s>>>(sd);
+}
 }  // namespace
 
 int error_blocks(const TypeDev* td) { return plan_groups(td).total; }
@@ -1023,17 +1081,22 @@ void launch_linearize(const TypeDev* td, const double* pose, const double* pt, d
     DH_GROUP_DISPATCH(g, k_linearize, gp.blocks[g], gp.dev[g], pose, pt, arena,
                       sum_for(gp, g, partials, counter, out));
   }
-  if (gp.last < 0 && out) k_reduce<<<1, kBlock, 0, s>>>(partials, 0, out);
+  if (gp.last < 0 && out) launch_empty_sum(partials, out, nullptr, nullptr, s);
 }
 
 void launch_error(const TypeDev* td, const double* pose, const double* pt, double* partials, unsigned* counter,
-                  double* out, hipStream_t s) {
+                  double* out, int* fail_src, int* fail_dst, hipStream_t s) {
   const GroupPlan gp = plan_groups(td);
   for (int g = 0; g < kNGroups; ++g) {
     if (gp.blocks[g] == 0) continue;
-    DH_GROUP_DISPATCH(g, k_error, gp.blocks[g], gp.dev[g], pose, pt, sum_for(gp, g, partials, counter, out));
+    SumDev sd = sum_for(gp, g, partials, counter, out);
+    if (sd.out) {
+      sd.fail_src = fail_src;
+      sd.fail_dst = fail_dst;
+    }
+    DH_GROUP_DISPATCH(g, k_error, gp.blocks[g], gp.dev[g], pose, pt, sd);
   }
-  if (gp.last < 0) k_reduce<<<1, kBlock, 0, s>>>(partials, 0, out);
+  if (gp.last < 0) launch_empty_sum(partials, out, fail_src, fail_dst, s);
 }
 
 void launch_linerr(const TypeDev* td, const double* arena, const double* dpose, const double* dpt, double* partials,
@@ -1044,35 +1107,43 @@ void launch_linerr(const TypeDev* td, const double* arena, const double* dpose, 
     DH_GROUP_DISPATCH(g, k_linerr, gp.blocks[g], gp.dev[g], arena, dpose, dpt,
                       sum_for(gp, g, partials, counter, out));
   }
-  if (gp.last < 0) k_reduce<<<1, kBlock, 0, s>>>(partials, 0, out);
+  if (gp.last < 0) launch_empty_sum(partials, out, nullptr, nullptr, s);
 }
 
-void launch_gather_3x3(const GatherDev& g, const double* arena, double* dst, hipStream_t s) {
-  if (g.n == 0) return;
-  k_gather_thread<3, 3><<<nblocks(g.n), kBlock, 0, s>>>(g.start, g.ent, g.n, arena, dst);
-}
-void launch_gather_3x1(const GatherDev& g, const double* arena, double* dst, hipStream_t s) {
-  if (g.n == 0) return;
-  k_gather_thread<3, 1><<<nblocks(g.n), kBlock, 0, s>>>(g.start, g.ent, g.n, arena, dst);
-}
-void launch_gather_3x6(const GatherDev& g, const double* arena, double* dst, hipStream_t s) {
-  if (g.n == 0) return;
-  k_gather_thread<3, 6><<<nblocks(g.n), kBlock, 0, s>>>(g.start, g.ent, g.n, arena, dst);
-}
-void launch_gather_band(const GatherDev& g, const double* arena, const int32_t* tA, const int32_t* tB,
-                        const TileDev& b, double lambda, hipStream_t s) {
-  if (g.n == 0) return;
-  k_gather_band<<<nblocks(static_cast<int64_t>(g.n) * 64), kBlock, 0, s>>>(g.start, g.ent, g.n, arena, tA, tB, b,
-                                                                            lambda);
-}
-void launch_gather_grad(const GatherDev& g, const double* arena, double* gred, hipStream_t s) {
-  if (g.n == 0) return;
-  k_gather_grad<<<nblocks(static_cast<int64_t>(g.n) * 64), kBlock, 0, s>>>(g.start, g.ent, g.n, arena, gred);
+void launch_gather_point(const GatherDev (&g)[4], double* const (&dst)[4], const double* arena, hipStream_t s) {
+  PointGatherDev p;
+  p.bstart[0] = 0;
+  for (int k = 0; k < 4; ++k) {
+    p.g[k] = g[k];
+    p.dst[k] = dst[k];
+    p.bstart[k + 1] = p.bstart[k] + nblocks(g[k].n);
+  }
+  if (p.bstart[4] == 0) return;
+  k_gather_point<<<p.bstart[4], kBlock, 0, s>>>(p, arena);
 }
 
-void launch_chain_factor(const ChainDev& c, double* arena, double lambda, int* fail, hipStream_t s) {
-  if (c.n_comp == 0) return;
-  k_chain_factor<<<nblocks(c.n_comp), kBlock, 0, s>>>(c, arena, lambda, fail);
+void launch_gather_reduced(const GatherDev& band, const int32_t* tA, const int32_t* tB, const GatherDev& grad,
+                           double* gred, const double* arena, const TileDev& b, double lambda, hipStream_t s) {
+  ReducedGatherDev r;
+  r.band = band;
+  r.tA = tA;
+  r.tB = tB;
+  r.grad = grad;
+  r.gred = gred;
+  r.nb_band = (nblocks(static_cast<int64_t>(band.n) * 64) + 7) / 8 * 8;
+  r.nb_grad = (nblocks(static_cast<int64_t>(grad.n) * 64) + 7) / 8 * 8;
+  const int nb = r.nb_band + r.nb_grad + nblocks(std::max(0, b.NT * kTile - b.n_red));
+  if (nb == 0) return;
+  k_gather_reduced<<<nb, kBlock, 0, s>>>(r, arena, b, lambda);
+}
+
+void launch_chain_factor(const ChainDev& c, double* arena, double lambda, int* fail, const ZeroDev& z,
+                         hipStream_t s) {
+  const int64_t nz = std::max(z.n0, z.n1) / 2;
+  const int nbz = nz == 0 ? 0 : static_cast<int>(std::min<int64_t>(1024, nblocks(nz)));
+  const int nb = nblocks(c.n_comp) + nbz;
+  if (nb == 0) return;
+  k_chain_factor<<<nb, kBlock, 0, s>>>(c, arena, lambda, fail, z);
 }
 void launch_chain_solve_y(const ChainDev& c, double* arena, hipStream_t s) {
   if (c.n_nb == 0) return;
@@ -1083,12 +1154,6 @@ void launch_backsub(const ChainDev& c, int n_edge, const double* arena, const do
   if (c.n_comp == 0) return;
   if (n_edge > 0) k_wdx<<<nblocks(n_edge), kBlock, 0, s>>>(c, n_edge, arena, dpose, wdx);
   k_backsub<<<nblocks(c.n_comp), kBlock, 0, s>>>(c, arena, wdx, dpt);
-}
-
-void launch_tile_pad(const TileDev& b, hipStream_t s) {
-  const int npad = b.NT * kTile - b.n_red;
-  if (npad <= 0) return;
-  k_tile_pad<<<1, kTile, 0, s>>>(b);
 }
 
 void launch_retract(int n_pose, int n_pt, const double* pose, const double* pt, const double* dpose,

@@ -26,6 +26,30 @@ struct GatherDev {
   const GEntry* ent = nullptr;
 };
 
+// launch_gather_point: D, E, g_p, W targets
+struct PointGatherDev {
+  GatherDev g[4];
+  double* dst[4] = {};
+  int bstart[5] = {};
+};
+
+struct ReducedGatherDev {
+  GatherDev band;              // 6x6 reduced blocks (targets tA[t], tB[t])
+  const int32_t* tA = nullptr;
+  const int32_t* tB = nullptr;
+  GatherDev grad;              // 6-vector reduced gradient per pose
+  double* gred = nullptr;
+  int nb_band = 0, nb_grad = 0;
+};
+
+// two buffers zeroed by the blocks past the chains in k_chain_factor
+struct ZeroDev {
+  double* p0 = nullptr;
+  int64_t n0 = 0;              // doubles, even
+  double* p1 = nullptr;
+  int64_t n1 = 0;
+};
+
 struct ChainDev {
   int n_comp = 0;
   int n_nb = 0;
@@ -74,27 +98,25 @@ struct TileSchedDev {
 int error_blocks(const TypeDev* td);
 void launch_linearize(const TypeDev* td, const double* pose, const double* pt, double* arena, double* partials,
                       unsigned* counter, double* out, hipStream_t s);
+// fail_src (optional): accumulated failure bits, moved to *fail_dst and cleared
 void launch_error(const TypeDev* td, const double* pose, const double* pt, double* partials, unsigned* counter,
-                  double* out, hipStream_t s);
+                  double* out, int* fail_src, int* fail_dst, hipStream_t s);
 void launch_linerr(const TypeDev* td, const double* arena, const double* dpose, const double* dpt, double* partials,
                    unsigned* counter, double* out, hipStream_t s);
 
 // point-side gathers (thread per target), dst = arena + off
-void launch_gather_3x3(const GatherDev& g, const double* arena, double* dst, hipStream_t s);
-void launch_gather_3x1(const GatherDev& g, const double* arena, double* dst, hipStream_t s);
-void launch_gather_3x6(const GatherDev& g, const double* arena, double* dst, hipStream_t s);
-// reduced system (wave per target)
-void launch_gather_band(const GatherDev& g, const double* arena, const int32_t* tA, const int32_t* tB,
-                        const TileDev& b, double lambda, hipStream_t s);
-void launch_gather_grad(const GatherDev& g, const double* arena, double* gred, hipStream_t s);
+void launch_gather_point(const GatherDev (&g)[4], double* const (&dst)[4], const double* arena, hipStream_t s);
+// reduced blocks into their tiles (+ lambda), reduced gradient, identity padding
+void launch_gather_reduced(const GatherDev& band, const int32_t* tA, const int32_t* tB, const GatherDev& grad,
+                           double* gred, const double* arena, const TileDev& b, double lambda, hipStream_t s);
 
-void launch_chain_factor(const ChainDev& c, double* arena, double lambda, int* fail, hipStream_t s);
+void launch_chain_factor(const ChainDev& c, double* arena, double lambda, int* fail, const ZeroDev& z,
+                         hipStream_t s);
 void launch_chain_solve_y(const ChainDev& c, double* arena, hipStream_t s);
 // dpt = C^-1 (gp - W dpose); wdx: scratch of 3 doubles per point-pose edge
 void launch_backsub(const ChainDev& c, int n_edge, const double* arena, const double* dpose, double* wdx, double* dpt,
                     hipStream_t s);
 
-void launch_tile_pad(const TileDev& b, hipStream_t s);
 // factor the tiles and solve (L L^T) x = r (forward substitution fused
 // into the factorisation: contrib holds L(i,k) y_k per stored tile). Linv
 // receives the NT diagonal inverse tiles, y the forward result. One launch

@@ -117,7 +117,9 @@ struct dynohip_solver {
   DevBuf<unsigned> done;
   DevBuf<double> partials, result;
   DevBuf<unsigned> sumctr;   // arrival counter of the folded reductions
-  int* failp = nullptr;  // inside `result` (doubles [0..3] results, [4] fail flag as int)
+  // inside `result`: doubles [0..3] results, [4] the solve's fail flag (int),
+  // [5] the fail bits being accumulated (moved to [4] and cleared by the error sum)
+  int* failp = nullptr;
   int partial_slots = 0;
   ChainDev cd;
   TileDev bd;
@@ -196,7 +198,8 @@ int upload_plan(dynohip_solver* s) {
   HIPCHK(s, s->result.alloc(8));
   HIPCHK(s, s->sumctr.alloc(1));
   HIPCHK(s, hipMemsetAsync(s->sumctr.p, 0, sizeof(unsigned), st));
-  s->failp = reinterpret_cast<int*>(s->result.p + 4);
+  s->failp = reinterpret_cast<int*>(s->result.p + 5);
+  HIPCHK(s, hipMemsetAsync(s->result.p, 0, 8 * sizeof(double), st));
   if (upload_gather(s, P.gD, s->gD) || upload_gather(s, P.gE, s->gE) || upload_gather(s, P.gGp, s->gGp) ||
       upload_gather(s, P.gW, s->gW) || upload_gather(s, P.gRed, s->gRed) || upload_gather(s, P.gGred, s->gGred))
     return DYNOHIP_EHIP;
@@ -273,7 +276,8 @@ int upload_plan(dynohip_solver* s) {
 
 // error at (pose, pt) into result[slot]
 void enqueue_error(dynohip_solver* s, const double* pose, const double* pt, double* partials, double* out) {
-  launch_error(s->td, pose, pt, partials, s->sumctr.p, out, s->stream);
+  launch_error(s->td, pose, pt, partials, s->sumctr.p, out, s->failp, reinterpret_cast<int*>(s->result.p + 4),
+               s->stream);
 }
 
 void enqueue_linerr(dynohip_solver* s, const double* dpose, const double* dpt, double* partials, double* out) {
@@ -293,10 +297,10 @@ void enqueue_linearize(dynohip_solver* s, const double* pose, const double* pt, 
   Plan& P = s->plan;
   double* A = s->arena.p;
   launch_linearize(s->td, pose, pt, A, s->partials.p, s->sumctr.p, lin0, s->stream);
-  launch_gather_3x3(s->gD.dev(P.gD.ntargets()), A, A + P.off_D, s->stream);
-  launch_gather_3x3(s->gE.dev(P.gE.ntargets()), A, A + P.off_E, s->stream);
-  launch_gather_3x1(s->gGp.dev(P.gGp.ntargets()), A, A + P.off_gp, s->stream);
-  launch_gather_3x6(s->gW.dev(P.gW.ntargets()), A, A + P.off_W, s->stream);
+  const GatherDev g[4] = {s->gD.dev(P.gD.ntargets()), s->gE.dev(P.gE.ntargets()), s->gGp.dev(P.gGp.ntargets()),
+                          s->gW.dev(P.gW.ntargets())};
+  double* const dst[4] = {A + P.off_D, A + P.off_E, A + P.off_gp, A + P.off_W};
+  launch_gather_point(g, dst, A, s->stream);
 }
 
 // damped solve + linearised error + retract + error for one lambda.
@@ -308,15 +312,16 @@ void enqueue_try(dynohip_solver* s, double lambda) {
   double* A = s->arena.p;
   const size_t nrp = static_cast<size_t>(P.NT) * kTile;
   if (timed) (void)hipEventRecord(s->ev[2], st);
-  (void)hipMemsetAsync(s->failp, 0, sizeof(double), st);
-  (void)hipMemsetAsync(s->slots.p, 0, static_cast<size_t>(P.n_slots) * kTile * kTile * sizeof(double), st);
-  (void)hipMemsetAsync(s->gred.p, 0, nrp * sizeof(double), st);
-  launch_chain_factor(s->cd, A, lambda, s->failp, st);
+  ZeroDev z;
+  z.p0 = s->slots.p;
+  z.n0 = static_cast<int64_t>(P.n_slots) * kTile * kTile;
+  z.p1 = s->gred.p;
+  z.n1 = static_cast<int64_t>(nrp);
+  launch_chain_factor(s->cd, A, lambda, s->failp, z, st);
   launch_chain_solve_y(s->cd, A, st);
   if (timed) (void)hipEventRecord(s->ev[3], st);
-  launch_gather_band(s->gRed.dev(P.gRed.ntargets()), A, s->redA.p, s->redB.p, s->bd, lambda, st);
-  launch_tile_pad(s->bd, st);
-  launch_gather_grad(s->gGred.dev(P.gGred.ntargets()), A, s->gred.p, st);
+  launch_gather_reduced(s->gRed.dev(P.gRed.ntargets()), s->redA.p, s->redB.p, s->gGred.dev(P.gGred.ntargets()),
+                        s->gred.p, A, s->bd, lambda, st);
   if (timed) (void)hipEventRecord(s->ev[4], st);
   double* y = s->xy.p;
   double* x = s->xy.p + nrp;
