@@ -9,7 +9,9 @@ import os
 
 from . import _abi
 
-LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+# DYNOSAM_AMD_LIB_DIR points the loader at another build of the same
+# libraries (kernel-variant A/B measurements); the default is the in-tree build
+LIB_DIR = os.environ.get("DYNOSAM_AMD_LIB_DIR") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 _libs = {}
 
 
@@ -96,7 +98,7 @@ def _declare(name, lib):
         lib.dynohip_sliding_window_init.restype = None
         lib.dynohip_sliding_window_check.argtypes = [P(_abi.SlidingWindowState), C.c_uint64, P(C.c_uint64), P(C.c_uint64)]
         lib.dynohip_sliding_window_check.restype = C.c_int
-        lib.dynohip_set_exec_options.argtypes = [vp, C.c_int, C.c_int]
+        lib.dynohip_set_exec_options.argtypes = [vp, C.c_int, C.c_int, C.c_int]
         lib.dynohip_set_exec_options.restype = C.c_int
         lib.dynohip_set_tile_ordering.argtypes = [C.c_int]
         lib.dynohip_set_tile_ordering.restype = None

@@ -796,9 +796,10 @@ __global__ __launch_bounds__(kBlock) void k_chain_factor(ChainDev cd, double* __
     const int64_t stride = static_cast<int64_t>(gridDim.x - nbc) * kBlock;
     const int64_t i0 = static_cast<int64_t>(blockIdx.x - nbc) * kBlock + threadIdx.x;
     const double2 zero = {0.0, 0.0};
-    for (int k = 0; k < 2; ++k) {
-      double2* p = reinterpret_cast<double2*>(k == 0 ? zb.p0 : zb.p1);
-      const int64_t n = (k == 0 ? zb.n0 : zb.n1) / 2;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      double2* p = reinterpret_cast<double2*>(zb.p[k]);
+      const int64_t n = zb.n[k] / 2;
       for (int64_t i = i0; i < n; i += stride) p[i] = zero;
     }
     return;
@@ -1139,7 +1140,7 @@ void launch_gather_reduced(const GatherDev& band, const int32_t* tA, const int32
 
 void launch_chain_factor(const ChainDev& c, double* arena, double lambda, int* fail, const ZeroDev& z,
                          hipStream_t s) {
-  const int64_t nz = std::max(z.n0, z.n1) / 2;
+  const int64_t nz = std::max(z.n[0], std::max(z.n[1], z.n[2])) / 2;
   const int nbz = nz == 0 ? 0 : static_cast<int>(std::min<int64_t>(1024, nblocks(nz)));
   const int nb = nblocks(c.n_comp) + nbz;
   if (nb == 0) return;

@@ -42,12 +42,10 @@ struct ReducedGatherDev {
   int nb_band = 0, nb_grad = 0;
 };
 
-// two buffers zeroed by the blocks past the chains in k_chain_factor
+// buffers zeroed by the blocks past the chains in k_chain_factor
 struct ZeroDev {
-  double* p0 = nullptr;
-  int64_t n0 = 0;              // doubles, even
-  double* p1 = nullptr;
-  int64_t n1 = 0;
+  double* p[3] = {};
+  int64_t n[3] = {};           // doubles, even
 };
 
 struct ChainDev {
@@ -86,6 +84,12 @@ struct TileSchedDev {
   int* arrive = nullptr;       // NT arrival counters (zero between launches)
   unsigned* done = nullptr;    // NT column-done stamps of the one-launch backward solve
   unsigned epoch = 0;          // stamp of the current solve (never 0)
+  const int32_t* fdep_start = nullptr;  // dataflow dependencies (Plan::fdep)
+  const int32_t* fdep = nullptr;
+  unsigned* wcnt = nullptr;    // per-slot write counters, zeroed before each solve
+  unsigned* fqueue = nullptr;  // task queue head, zeroed before each solve
+  bool persistent_factor = true;  // one dataflow launch instead of one launch per level
+  int workers = 256;           // its workgroups (one per CU)
   int wide_updates = 256;      // levels with more update tasks use the side-stream kernel
   bool level_backward = false; // force one backward launch per level
 };

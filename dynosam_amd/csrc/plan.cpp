@@ -253,9 +253,15 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
   };
 
   // ---- arena layout ----
+  // every region starts at an even offset (16-byte aligned), so blocks at
+  // even offsets inside it can be read with 16-byte loads
+  auto align2 = [&arena] { arena = (arena + 1) & ~1ull; };
   P.off_D = arena; arena += 9ull * P.n_pt;
+  align2();
   P.off_E = arena; arena += 9ull * P.n_pt;
+  align2();
   P.off_gp = arena; arena += 3ull * P.n_pt;
+  align2();
   P.off_W = arena; arena += 18ull * P.n_edge;
 
   // ---- component neighbour poses and Y layout ----
@@ -288,7 +294,9 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
     P.comp_nb_start.push_back(static_cast<int32_t>(P.nb_pose.size()));
   }
   P.off_v = arena; arena += 3ull * P.n_pt;
+  align2();
   P.off_L = arena; arena += 9ull * P.n_pt;
+  align2();
   P.off_M = arena; arena += 9ull * P.n_pt;
   P.arena_size = arena;
   if (arena >= (1ull << 32)) { err = "graph too large for 32-bit arena offsets"; return DYNOHIP_ESTRUCT; }

@@ -145,6 +145,12 @@ struct Plan {
   std::vector<int32_t> pairs;           // operand pairs (A slot, B slot) of the tasks
   std::vector<int32_t> flevel;          // level l = tasks [flevel[l], flevel[l+1])
   std::vector<int32_t> fpanels;         // panels of level l (they come first within the level)
+  // dataflow form of the same schedule (k_factor_persist): task q may start
+  // once every slot of fdep[fdep_start[q] .. fdep_start[q+1]) (pairs: slot,
+  // count) has received `count` completed writes (update tasks and panels
+  // i != k write their dst slot once each)
+  std::vector<int32_t> fdep_start;
+  std::vector<int32_t> fdep;
   std::vector<BackTask> btask;
   std::vector<int32_t> blevel;
   std::vector<int32_t> bent;            // pairs (slot, row tile)

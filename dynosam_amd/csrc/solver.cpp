@@ -114,6 +114,8 @@ struct dynohip_solver {
   DevBuf<BackPart> bpart;
   DevBuf<double> bpartials;
   DevBuf<int> arrive;
+  DevBuf<int32_t> fdep_start, fdep;
+  DevBuf<unsigned> fsync;   // [0] dataflow task queue head, [4..] per-slot write counters
   DevBuf<unsigned> done;
   DevBuf<double> partials, result;
   DevBuf<unsigned> sumctr;   // arrival counter of the folded reductions
@@ -227,6 +229,10 @@ int upload_plan(dynohip_solver* s) {
   HIPCHK(s, s->bpartials.alloc(static_cast<size_t>(P.n_partials) * kTile + 1));
   HIPCHK(s, s->arrive.alloc(static_cast<size_t>(P.NT) + 1));
   HIPCHK(s, hipMemsetAsync(s->arrive.p, 0, (static_cast<size_t>(P.NT) + 1) * sizeof(int), st));
+  HIPCHK(s, s->fdep_start.upload(P.fdep_start, st));
+  HIPCHK(s, s->fdep.upload(P.fdep, st));
+  HIPCHK(s, s->fsync.alloc((static_cast<size_t>(P.n_slots) + 4 + 3) / 4 * 4));
+  HIPCHK(s, hipMemsetAsync(s->fsync.p, 0, s->fsync.n * sizeof(unsigned), st));
   HIPCHK(s, s->done.alloc(static_cast<size_t>(P.NT) + 1));
   HIPCHK(s, hipMemsetAsync(s->done.p, 0, (static_cast<size_t>(P.NT) + 1) * sizeof(unsigned), st));
   s->sd.epoch = 0;
@@ -270,6 +276,10 @@ int upload_plan(dynohip_solver* s) {
   s->sd.arrive = s->arrive.p;
   s->sd.done = s->done.p;
   s->sd.bent = s->bent.p;
+  s->sd.fdep_start = s->fdep_start.p;
+  s->sd.fdep = s->fdep.p;
+  s->sd.fqueue = s->fsync.p;
+  s->sd.wcnt = s->fsync.p + 4;
   HIPCHK(s, hipStreamSynchronize(st));
   return 0;
 }
@@ -313,10 +323,12 @@ void enqueue_try(dynohip_solver* s, double lambda) {
   const size_t nrp = static_cast<size_t>(P.NT) * kTile;
   if (timed) (void)hipEventRecord(s->ev[2], st);
   ZeroDev z;
-  z.p0 = s->slots.p;
-  z.n0 = static_cast<int64_t>(P.n_slots) * kTile * kTile;
-  z.p1 = s->gred.p;
-  z.n1 = static_cast<int64_t>(nrp);
+  z.p[0] = s->slots.p;
+  z.n[0] = static_cast<int64_t>(P.n_slots) * kTile * kTile;
+  z.p[1] = s->gred.p;
+  z.n[1] = static_cast<int64_t>(nrp);
+  z.p[2] = reinterpret_cast<double*>(s->fsync.p);
+  z.n[2] = static_cast<int64_t>(s->fsync.n) / 2;
   launch_chain_factor(s->cd, A, lambda, s->failp, z, st);
   launch_chain_solve_y(s->cd, A, st);
   if (timed) (void)hipEventRecord(s->ev[3], st);
@@ -455,6 +467,7 @@ int lm_iterate(dynohip_solver* s) {
       }
     }
     if (fail & 2) return set_err(s, DYNOHIP_EHIP, "backward solve: dependency wait timed out");
+    if (fail & 4) return set_err(s, DYNOHIP_EHIP, "factorisation: dependency wait timed out");
     const int solved = fail == 0 && std::isfinite(res[0]);
     te.solved = solved;
     bool step_ok = false, stop = false;
@@ -560,6 +573,10 @@ int dynohip_create(int device_id, dynohip_solver** out) {
   (void)hipEventCreateWithFlags(&s->ev_main, hipEventDisableTiming);
   (void)hipEventCreateWithFlags(&s->ev_side, hipEventDisableTiming);
   for (auto& e : s->ev) (void)hipEventCreate(&e);
+  // the dataflow factorisation keeps one 158 KB-LDS workgroup per CU
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_id) == hipSuccess && cus > 0)
+    s->sd.workers = cus;
   dynohip_lm_params_default(&s->prm);
   *out = s;
   return DYNOHIP_OK;
@@ -822,10 +839,11 @@ int dynohip_get_stats(dynohip_solver* s, dynohip_stats* out) {
   return DYNOHIP_OK;
 }
 
-int dynohip_set_exec_options(dynohip_solver* s, int wide_updates, int level_backward) {
+int dynohip_set_exec_options(dynohip_solver* s, int wide_updates, int level_backward, int level_factor) {
   if (!s || wide_updates < 0) return DYNOHIP_EINVAL;
   s->sd.wide_updates = wide_updates;
   s->sd.level_backward = level_backward != 0;
+  s->sd.persistent_factor = level_factor == 0;
   return DYNOHIP_OK;
 }
 

@@ -277,48 +277,116 @@ __device__ __forceinline__ double lower_gemv4(const double* Li, const double* v,
   return s;
 }
 
+// ---- global memory access of the factorisation --------------------------
+// The level kernels (SC1 = false) read tiles written by earlier launches
+// with plain loads. The one-launch dataflow kernel (SC1 = true) hands tiles
+// between workgroups inside the launch, following cdna_hip_programming.md
+// Guideline 16 R1: every tile element, contribution and pending operand
+// written in the launch is stored write-through (sc1) and drained before the
+// slot's write counter is bumped, and every load of such data is an sc1 load
+// (16-byte buffer loads for whole tiles, 8-byte atomic loads otherwise), so
+// no acquire fence is needed.
+typedef double d2v __attribute__((ext_vector_type(2)));
+
+template <bool SC1>
+__device__ __forceinline__ double gld(const double* p) {
+  if constexpr (SC1) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *p;
+}
+template <bool SC1>
+__device__ __forceinline__ void gst(double* p, double v) {
+  if constexpr (SC1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+
+// a tile base pointer is wave-uniform; make that visible to the compiler so
+// the buffer descriptor lives in SGPRs
+__device__ __forceinline__ const double* uniform_ptr(const double* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
+  return reinterpret_cast<const double*>((static_cast<uint64_t>(hi) << 32) | lo);
+}
+
+template <bool SC1>
+__device__ __forceinline__ void load_tile_lds_t(const double* __restrict__ src, double* dst, int tid) {
+  if constexpr (SC1) {
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(uniform_ptr(src)), 0, T * T * 8, 0x00020000);
+    d2v v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      v[i] = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(rs, (tid + 256 * i) * 16, 0, 16));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int e = tid + 256 * i, rr = (2 * e) / T, cc = (2 * e) % T;
+      dst[rr * LD + cc] = v[i].x;
+      dst[rr * LD + cc + 1] = v[i].y;
+    }
+  } else {
+    load_tile_lds(src, dst, tid, 256);
+  }
+}
+
 // sum over operand pairs [beg, end) of A B^T into acc (operands staged in
 // Qs / Rs; a pair with A == B is loaded once)
+template <bool SC1>
 __device__ __forceinline__ void sum_pairs(const TileDev& b, const int32_t* __restrict__ pairs, int beg, int end,
                                           double* Qs, double* Rs, int tid, int w, int l, v4d acc[2][2]) {
   zero_acc(acc);
   for (int e = beg; e < end; ++e) {
     const int32_t pa = pairs[2 * e], pb = pairs[2 * e + 1];
     __syncthreads();
-    load_tile_lds(slot_ptr(b, pa), Qs, tid, 256);
-    if (pb != pa) load_tile_lds(slot_ptr(b, pb), Rs, tid, 256);
+    load_tile_lds_t<SC1>(slot_ptr(b, pa), Qs, tid);
+    if (pb != pa) load_tile_lds_t<SC1>(slot_ptr(b, pb), Rs, tid);
     __syncthreads();
     mfma_abt_acc(Qs, pb != pa ? Rs : Qs, w, l, acc);
   }
 }
 
 // Issue the loads of up to four 64x64 tiles into LDS before any of the
-// stores, so their latencies overlap (one round trip instead of four).
-__device__ __forceinline__ void load_tiles_lds(const double* const (&src)[4], double* const (&dst)[4], int n,
+// stores, so their latencies overlap (one round trip instead of four). A
+// null source skips its tile. (Fixed operand positions, no pointer arrays:
+// those would go through scratch and turn the LDS stores into flat stores.)
+template <bool SC1>
+__device__ __forceinline__ void load_tiles_lds(const double* s0, double* d0, const double* s1, double* d1,
+                                               const double* s2, double* d2, const double* s3, double* d3,
                                                int tid) {
-  double2 v[4][8];
+  const double* const src[4] = {s0, s1, s2, s3};
+  d2v v[4][8];
 #pragma unroll
   for (int t = 0; t < 4; ++t)
-    if (t < n) {
-      const double2* s2 = reinterpret_cast<const double2*>(src[t]);
+    if (src[t]) {
+      if constexpr (SC1) {
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(uniform_ptr(src[t])), 0, T * T * 8, 0x00020000);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[t][i] = s2[tid + 256 * i];
-    }
+        for (int i = 0; i < 8; ++i)
+          v[t][i] = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(rs, (tid + 256 * i) * 16, 0, 16));
+      } else {
+        const d2v* s2v = reinterpret_cast<const d2v*>(src[t]);
 #pragma unroll
-  for (int t = 0; t < 4; ++t)
-    if (t < n) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int e = tid + 256 * i, rr = (2 * e) / T, cc = (2 * e) % T;
-        dst[t][rr * LD + cc] = v[t][i].x;
-        dst[t][rr * LD + cc + 1] = v[t][i].y;
+        for (int i = 0; i < 8; ++i) v[t][i] = s2v[tid + 256 * i];
       }
     }
+  auto put = [&](int t, double* d) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int e = tid + 256 * i, rr = (2 * e) / T, cc = (2 * e) % T;
+      d[rr * LD + cc] = v[t][i].x;
+      d[rr * LD + cc + 1] = v[t][i].y;
+    }
+  };
+  if (s0) put(0, d0);
+  if (s1) put(1, d1);
+  if (s2) put(2, d2);
+  if (s3) put(3, d3);
 }
 
 // dst -= sum over the task's pairs of A B^T: the destination and the first
 // pair's operands are fetched in one round trip; further pairs (rare) one
 // by one
+template <bool SC1>
 __device__ __forceinline__ void run_update(const TileDev& b, const TileTask& tk, const int32_t* __restrict__ pairs,
                                            double* Qs, double* Rs, int tid, int w, int l) {
   double* dst = slot_ptr(b, tk.dst);
@@ -328,15 +396,14 @@ __device__ __forceinline__ void run_update(const TileDev& b, const TileTask& tk,
 #pragma unroll
     for (int tj = 0; tj < 2; ++tj)
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) old[ti][tj][rr] = dst[MFMA_ROW(w, l, ti, rr) * T + MFMA_COL(w, l, tj)];
+      for (int rr = 0; rr < 4; ++rr) old[ti][tj][rr] = gld<SC1>(dst + MFMA_ROW(w, l, ti, rr) * T + MFMA_COL(w, l, tj));
   v4d acc[2][2];
   zero_acc(acc);
   for (int e = tk.po_beg; e < tk.po_end; ++e) {
     const int32_t pa = pairs[2 * e], pb = pairs[2 * e + 1];
     if (e > tk.po_beg) __syncthreads();
-    const double* src[4] = {slot_ptr(b, pa), slot_ptr(b, pb), nullptr, nullptr};
-    double* dsts[4] = {Qs, Rs, nullptr, nullptr};
-    load_tiles_lds(src, dsts, pb != pa ? 2 : 1, tid);
+    load_tiles_lds<SC1>(slot_ptr(b, pa), Qs, pb != pa ? slot_ptr(b, pb) : nullptr, Rs, nullptr, nullptr, nullptr,
+                        nullptr, tid);
     __syncthreads();
     mfma_abt_acc(Qs, pb != pa ? Rs : Qs, w, l, acc);
   }
@@ -346,7 +413,7 @@ __device__ __forceinline__ void run_update(const TileDev& b, const TileTask& tk,
     for (int tj = 0; tj < 2; ++tj)
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr)
-        dst[MFMA_ROW(w, l, ti, rr) * T + MFMA_COL(w, l, tj)] = old[ti][tj][rr] - acc[ti][tj][rr];
+        gst<SC1>(dst + MFMA_ROW(w, l, ti, rr) * T + MFMA_COL(w, l, tj), old[ti][tj][rr] - acc[ti][tj][rr]);
 }
 
 // A_kk -= L(k,c) L(k,c)^T on this wave's upper blocks (w, TJ >= w), K = 64
@@ -373,25 +440,27 @@ __device__ __forceinline__ void own_pending_quadrant(double* As, const double* Q
       for (int rr = 0; rr < 4; ++rr) As[MFMA_ROW(w, l, ti, rr) * LD + MFMA_COL(w, l, tj)] -= acc[ti][tj][rr];
 }
 
-__global__ __launch_bounds__(256) void k_tasks(TileDev b, const TileTask* __restrict__ tasks,
-                                               const int32_t* __restrict__ pairs, double* __restrict__ Linv,
-                                               const double* __restrict__ r, double* __restrict__ contrib,
-                                               double* __restrict__ y, int* fail) {
-  __shared__ double Ps[T * LD];   // pending diagonal operand L(k, c) -> later L_kk^-1
-  __shared__ double Qs[T * LD];   // pair operand A
-  __shared__ double Rs[T * LD];   // pair operand B
-  __shared__ double As[T * LD];   // own tile (i, k)
-  __shared__ double Xch[2 * 4 * 256];
-  __shared__ double rpart[4][T];
-  __shared__ double vv[T];
-  const TileTask tk = tasks[blockIdx.x];
+struct TaskLds {
+  double Ps[T * LD];   // pending diagonal operand L(k, c) -> later L_kk^-1
+  double Qs[T * LD];   // pair operand A
+  double Rs[T * LD];   // pair operand B
+  double As[T * LD];   // own tile (i, k)
+  double Xch[2 * 4 * 256];
+  double rpart[4][T];
+  double vv[T];
+};
+
+template <bool SC1>
+__device__ __forceinline__ void panel_task(const TileDev& b, const TileTask& tk, const int32_t* __restrict__ pairs,
+                                           double* __restrict__ Linv, const double* __restrict__ r,
+                                           double* __restrict__ contrib, double* __restrict__ y, int* fail,
+                                           TaskLds& S) {
+  double* const Ps = S.Ps;
+  double* const Qs = S.Qs;
+  double* const Rs = S.Rs;
+  double* const As = S.As;
   const int tid = threadIdx.x;
   const int w = tid >> 6, l = tid & 63;
-  if (tk.kind == 1) {
-    run_update(b, tk, pairs, Qs, Rs, tid, w, l);
-    return;
-  }
-  // ---- panel
   const bool own = tk.i != tk.k;
   const int npd = tk.pd_end - tk.pd_beg, npo = own ? tk.po_end - tk.po_beg : 0;
   const bool fast = npd <= 1 && npo <= 1;
@@ -405,33 +474,26 @@ __global__ __launch_bounds__(256) void k_tasks(TileDev b, const TileTask* __rest
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
       const int row = ACC_ROW(w, l, rr), col = ACC_COL(TJ, l);
-      accA[TJ][rr] = TJ >= w ? diag[row * T + col] : 0.0;
+      accA[TJ][rr] = TJ >= w ? gld<SC1>(diag + row * T + col) : 0.0;
       accX[TJ][rr] = row == col ? 1.0 : 0.0;
     }
   {
     double sacc = 0.0;
     for (int e = b.row_start[tk.k] + w; e < b.row_start[tk.k + 1]; e += 4)
-      if (b.row_col[e] != tk.k) sacc += contrib[static_cast<int64_t>(b.row_slot[e]) * T + l];
-    rpart[w][l] = sacc;
+      if (b.row_col[e] != tk.k) sacc += gld<SC1>(contrib + static_cast<int64_t>(b.row_slot[e]) * T + l);
+    S.rpart[w][l] = sacc;
   }
   if (fast) {
-    const double* src[4] = {nullptr, nullptr, nullptr, nullptr};
-    double* dst[4] = {nullptr, nullptr, nullptr, nullptr};
-    int n = 0;
-    if (npd) { src[n] = slot_ptr(b, pairs[2 * tk.pd_beg]); dst[n++] = Ps; }
-    if (own) { src[n] = slot_ptr(b, tk.dst); dst[n++] = As; }
-    if (npo) {
-      src[n] = slot_ptr(b, pairs[2 * tk.po_beg]); dst[n++] = Qs;
-      src[n] = slot_ptr(b, pairs[2 * tk.po_beg + 1]); dst[n++] = Rs;
-    }
-    load_tiles_lds(src, dst, n, tid);
+    load_tiles_lds<SC1>(npd ? slot_ptr(b, pairs[2 * tk.pd_beg]) : nullptr, Ps, own ? slot_ptr(b, tk.dst) : nullptr, As,
+                        npo ? slot_ptr(b, pairs[2 * tk.po_beg]) : nullptr, Qs,
+                        npo ? slot_ptr(b, pairs[2 * tk.po_beg + 1]) : nullptr, Rs, tid);
   } else {
     // several pending pairs (rare): apply them one by one before the factor
     if (own) {
-      load_tile_lds(slot_ptr(b, tk.dst), As, tid, 256);
+      load_tile_lds_t<SC1>(slot_ptr(b, tk.dst), As, tid);
       if (npo) {
         v4d acc[2][2];
-        sum_pairs(b, pairs, tk.po_beg, tk.po_end, Qs, Rs, tid, w, l, acc);
+        sum_pairs<SC1>(b, pairs, tk.po_beg, tk.po_end, Qs, Rs, tid, w, l, acc);
 #pragma unroll
         for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
@@ -442,13 +504,15 @@ __global__ __launch_bounds__(256) void k_tasks(TileDev b, const TileTask* __rest
     }
     for (int e = tk.pd_beg; e < tk.pd_end; ++e) {
       __syncthreads();
-      load_tile_lds(slot_ptr(b, pairs[2 * e]), Ps, tid, 256);
+      load_tile_lds_t<SC1>(slot_ptr(b, pairs[2 * e]), Ps, tid);
       __syncthreads();
       diag_pending(accA, Ps, w, l);
     }
   }
   __syncthreads();
-  if (tid < T) vv[tid] = r[static_cast<int64_t>(tk.k) * T + tid] - ((rpart[0][tid] + rpart[1][tid]) + (rpart[2][tid] + rpart[3][tid]));
+  if (tid < T)
+    S.vv[tid] = r[static_cast<int64_t>(tk.k) * T + tid] -
+                ((S.rpart[0][tid] + S.rpart[1][tid]) + (S.rpart[2][tid] + S.rpart[3][tid]));
   // (2) pending updates: wave 0's diagonal blocks before the factorisation;
   // waves 1-3 apply theirs, plus their quadrant of the own tile's update,
   // while wave 0 factors block 0; wave 0 does its quadrant during step 1
@@ -461,7 +525,7 @@ __global__ __launch_bounds__(256) void k_tasks(TileDev b, const TileTask* __rest
   auto idle1 = [&]() {
     if (op) own_pending_quadrant(As, Qs, Rs, w, l);
   };
-  const bool ok = factor_tile_blk(accA, accX, w, l, Xch, idle0, idle1);
+  const bool ok = factor_tile_blk(accA, accX, w, l, S.Xch, idle0, idle1);
   if (!ok && !own && tid == 0) *fail = 1;
   // L_kk^-1 -> Ps (full square; upper part is exactly zero)
 #pragma unroll
@@ -477,10 +541,10 @@ __global__ __launch_bounds__(256) void k_tasks(TileDev b, const TileTask* __rest
   }
   __syncthreads();
   // y_k = L_kk^-1 r_k
-  const double yrow = lower_gemv4(Ps, vv, tid);
+  const double yrow = lower_gemv4(Ps, S.vv, tid);
   __syncthreads();
   if ((tid & 3) == 0) {
-    vv[tid >> 2] = yrow;
+    S.vv[tid >> 2] = yrow;
     if (!own) y[static_cast<int64_t>(tk.k) * T + (tid >> 2)] = yrow;
   }
   if (!own) return;
@@ -496,7 +560,7 @@ __global__ __launch_bounds__(256) void k_tasks(TileDev b, const TileTask* __rest
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int row = MFMA_ROW(w, l, ti, rr), col = MFMA_COL(w, l, tj);
-        dst[row * T + col] = acc[ti][tj][rr];
+        gst<SC1>(dst + row * T + col, acc[ti][tj][rr]);
         As[row * LD + col] = acc[ti][tj][rr];
       }
   __syncthreads();
@@ -504,11 +568,25 @@ __global__ __launch_bounds__(256) void k_tasks(TileDev b, const TileTask* __rest
   {
     const int row = tid >> 2, part = tid & 3;
     double s = 0.0;
-    for (int m = part; m < T; m += 4) s += As[row * LD + m] * vv[m];
+    for (int m = part; m < T; m += 4) s += As[row * LD + m] * S.vv[m];
     s += __shfl_xor(s, 1);
     s += __shfl_xor(s, 2);
-    if (part == 0) contrib[static_cast<int64_t>(tk.dst) * T + row] = s;
+    if (part == 0) gst<SC1>(contrib + static_cast<int64_t>(tk.dst) * T + row, s);
   }
+}
+
+__global__ __launch_bounds__(256) void k_tasks(TileDev b, const TileTask* __restrict__ tasks,
+                                               const int32_t* __restrict__ pairs, double* __restrict__ Linv,
+                                               const double* __restrict__ r, double* __restrict__ contrib,
+                                               double* __restrict__ y, int* fail) {
+  __shared__ TaskLds S;
+  const TileTask tk = tasks[blockIdx.x];
+  const int tid = threadIdx.x;
+  if (tk.kind == 1) {
+    run_update<false>(b, tk, pairs, S.Qs, S.Rs, tid, tid >> 6, tid & 63);
+    return;
+  }
+  panel_task<false>(b, tk, pairs, Linv, r, contrib, y, fail, S);
 }
 
 // update tasks of a wide level: dst -= sum A B^T, with only the two
@@ -519,7 +597,59 @@ __global__ __launch_bounds__(256) void k_updates(TileDev b, const TileTask* __re
   __shared__ double Rs[T * LD];
   const TileTask tk = tasks[blockIdx.x];
   const int tid = threadIdx.x;
-  run_update(b, tk, pairs, Qs, Rs, tid, tid >> 6, tid & 63);
+  run_update<false>(b, tk, pairs, Qs, Rs, tid, tid >> 6, tid & 63);
+}
+
+// The whole factorisation (and forward substitution) in one launch, as a
+// dataflow over the same tasks: one resident workgroup per CU takes tasks in
+// schedule order from a global queue, waits until every slot the task reads
+// or writes has received the writes the level schedule puts before it
+// (per-slot write counters, Plan::fdep), runs it, and publishes its slot
+// (sc1 stores drained, then the counter bumped). A task only waits for
+// tasks earlier in the queue, which were taken by running workgroups, so
+// the launch cannot deadlock whatever the residency. Waits are bounded: a
+// timeout sets bit 2 of *fail and the task still publishes, so the grid
+// drains and the step is rejected.
+constexpr int kSpinLimitF = 1 << 22;
+
+__global__ __launch_bounds__(256) void k_factor_persist(TileDev b, const TileTask* __restrict__ tasks, int ntasks,
+                                                        const int32_t* __restrict__ pairs,
+                                                        const int32_t* __restrict__ dep_start,
+                                                        const int32_t* __restrict__ dep, unsigned* wcnt,
+                                                        unsigned* queue, double* __restrict__ Linv,
+                                                        const double* __restrict__ r, double* __restrict__ contrib,
+                                                        double* __restrict__ y, int* fail) {
+  __shared__ TaskLds S;
+  __shared__ int s_q;
+  const int tid = threadIdx.x;
+  const int w = tid >> 6, l = tid & 63;
+  for (;;) {
+    if (tid == 0) s_q = static_cast<int>(__hip_atomic_fetch_add(queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    __syncthreads();
+    const int q = __builtin_amdgcn_readfirstlane(s_q);
+    if (q >= ntasks) break;
+    const TileTask tk = tasks[q];
+    if (w == 0) {
+      bool ok = true;
+      for (int j = dep_start[q] + l; j < dep_start[q + 1]; j += 64) {
+        const unsigned* c = wcnt + dep[2 * j];
+        const unsigned need = static_cast<unsigned>(dep[2 * j + 1]);
+        int spins = 0;
+        while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+          if (++spins > kSpinLimitF) { ok = false; break; }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      if (!ok) atomicOr(fail, 4);
+    }
+    __syncthreads();
+    if (tk.kind == 1) run_update<true>(b, tk, pairs, S.Qs, S.Rs, tid, w, l);
+    else panel_task<true>(b, tk, pairs, Linv, r, contrib, y, fail, S);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0 && (tk.kind == 1 || tk.i != tk.k))
+      __hip_atomic_fetch_add(wcnt + tk.dst, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // one level of the backward substitution,
@@ -732,7 +862,12 @@ void launch_tile_cholesky_solve(const TileDev& b, const TileSchedDev& sd, const 
   // a level is "wide" when its update tasks alone need more than one
   // round of the CUs (sd.wide_updates, default 256): they then run as
   // k_updates on the side stream
-  for (size_t lv = 0; lv + 1 < flevel.size(); ++lv) {
+  const int ntasks = flevel.empty() ? 0 : flevel.back();
+  if (sd.persistent_factor && ntasks > 0) {
+    k_factor_persist<<<std::min(ntasks, sd.workers), 256, 0, s>>>(b, sd.ftask, ntasks, sd.pairs, sd.fdep_start, sd.fdep,
+                                                                  sd.wcnt, sd.fqueue, Linv, r, contrib, y, fail);
+  }
+  for (size_t lv = 0; lv + 1 < flevel.size() && !sd.persistent_factor; ++lv) {
     const int n = flevel[lv + 1] - flevel[lv];
     const int np = fpanels[lv], nu = n - np;
     if (nu > 0 && nu > sd.wide_updates && side) {

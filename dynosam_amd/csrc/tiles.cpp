@@ -263,6 +263,53 @@ void schedule(int NT, const std::vector<std::vector<int32_t>>& adj, const std::v
 
 int g_leaf_override = -1;
 
+// Per task, the slots it reads or writes and how many writes each must have
+// received first: the writes of earlier levels (the level schedule is a valid
+// order, so this reproduces it exactly, including the fixed order in which a
+// tile receives its updates). Slots only written before the factorisation
+// (count 0) are left out.
+void build_dataflow_deps(Plan& P) {
+  std::vector<int32_t> written(P.n_slots, 0);
+  P.fdep_start.assign(1, 0);
+  P.fdep.clear();
+  std::vector<int32_t> touch;
+  const int nlev = static_cast<int>(P.flevel.size()) - 1;
+  for (int l = 0; l < nlev; ++l) {
+    for (int32_t q = P.flevel[l]; q < P.flevel[l + 1]; ++q) {
+      const TileTask& t = P.ftask[q];
+      touch.clear();
+      auto add_pairs = [&](int32_t beg, int32_t end) {
+        for (int32_t e = beg; e < end; ++e) {
+          touch.push_back(P.pairs[2 * e]);
+          touch.push_back(P.pairs[2 * e + 1]);
+        }
+      };
+      add_pairs(t.po_beg, t.po_end);
+      if (t.kind == 1) {
+        touch.push_back(t.dst);
+      } else {
+        touch.push_back(t.diag);
+        add_pairs(t.pd_beg, t.pd_end);
+        if (t.i != t.k) touch.push_back(t.dst);
+        for (int32_t e = P.row_start[t.k]; e < P.row_start[t.k + 1]; ++e)
+          if (P.row_col[e] != t.k) touch.push_back(P.row_slot[e]);
+      }
+      std::sort(touch.begin(), touch.end());
+      touch.erase(std::unique(touch.begin(), touch.end()), touch.end());
+      for (int32_t sl : touch)
+        if (written[sl] > 0) {
+          P.fdep.push_back(sl);
+          P.fdep.push_back(written[sl]);
+        }
+      P.fdep_start.push_back(static_cast<int32_t>(P.fdep.size() / 2));
+    }
+    for (int32_t q = P.flevel[l]; q < P.flevel[l + 1]; ++q) {
+      const TileTask& t = P.ftask[q];
+      if (t.kind == 1 || t.i != t.k) written[t.dst]++;
+    }
+  }
+}
+
 }  // namespace
 
 void build_tile_schedule(Plan& P) {
@@ -350,6 +397,7 @@ void build_tile_schedule(Plan& P) {
     }
     P.row_start[t + 1] = static_cast<int32_t>(P.row_col.size());
   }
+  build_dataflow_deps(P);
 }
 
 }  // namespace dynohip

@@ -61,11 +61,13 @@ class Solver:
             self.h, keys.ctypes.data_as(C.POINTER(C.c_uint64)), kinds.ctypes.data_as(C.POINTER(C.c_uint8)),
             data.ctypes.data_as(C.POINTER(C.c_double)), keys.shape[0]))
 
-    def set_exec_options(self, wide_updates=256, level_backward=False):
-        """Execution paths (dynohip_set_exec_options): concurrent update kernel
-        for levels with more than `wide_updates` update tasks; level-launched
-        backward substitution."""
-        _check(self.lib, self.h, self.lib.dynohip_set_exec_options(self.h, int(wide_updates), int(bool(level_backward))))
+    def set_exec_options(self, wide_updates=256, level_backward=False, level_factor=False):
+        """Execution paths (dynohip_set_exec_options): level-launched
+        factorisation instead of the one-launch dataflow, and on that path a
+        concurrent update kernel for levels with more than `wide_updates`
+        update tasks; level-launched backward substitution."""
+        _check(self.lib, self.h, self.lib.dynohip_set_exec_options(
+            self.h, int(wide_updates), int(bool(level_backward)), int(bool(level_factor))))
 
     def values_data(self):
         n = self._values.data.shape[0]

@@ -234,13 +234,15 @@ typedef struct {
   int64_t n_pose, n_tiles, n_slots, n_ftask, n_pairs, n_flevel, n_btask, n_blevel, n_bent, n_red_blocks, nd_leaf;
 } dynohip_schedule_info;
 
-/* Execution-path options of a handle (tests / tuning). A factorisation
+/* Execution-path options of a handle (tests / tuning). By default the
+   factorisation runs as one dataflow launch (per-slot write counters);
+   level_factor = 1 runs it as one launch per level instead. On that path a
    level whose update tasks outnumber `wide_updates` (default 256; 0 = every
    level with updates) runs them as a separate kernel on a second stream,
    concurrently with its panels. level_backward = 1 runs the backward
    substitution as one launch per level instead of the default single
-   launch. */
-int dynohip_set_exec_options(dynohip_solver* s, int wide_updates, int level_backward);
+   launch. All paths give bit-identical results. */
+int dynohip_set_exec_options(dynohip_solver* s, int wide_updates, int level_backward, int level_factor);
 
 /* Tile ordering of the reduced system for plans built after the call
    (process-wide): -1 = automatic (cost model, default), 0 = frame order

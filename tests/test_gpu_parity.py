@@ -116,11 +116,14 @@ def test_cliques_fixture_matches_golden(gpu_available):
 
 @pytest.mark.parametrize("name", ["C1", "C2"])
 def test_execution_paths_agree(gpu_available, name):
-    """The concurrent update kernel (every level split) and the level-launched
-    backward substitution give the same LM iterates as the default paths:
-    the same per-task arithmetic in the same order, bit for bit."""
+    """The level-launched factorisation (with and without the concurrent
+    update kernel on every level) and the level-launched backward
+    substitution give the same LM iterates as the default one-launch
+    dataflow paths: the same per-task arithmetic in the same order, bit for
+    bit."""
     results = []
-    for opts in ({}, {"wide_updates": 0}, {"level_backward": True}, {"wide_updates": 0, "level_backward": True}):
+    for opts in ({}, {"level_factor": True}, {"level_factor": True, "wide_updates": 0}, {"level_backward": True},
+                 {"level_factor": True, "wide_updates": 0, "level_backward": True}):
         g, v, _, s = make(name)
         s.set_exec_options(**opts)
         for _ in range(3):
