@@ -106,6 +106,13 @@ def _declare(name, lib):
         lib.dynohip_plan_schedule.argtypes = [P(_abi.GraphView), P(C.c_uint64), P(C.c_uint8), C.c_size_t,
                                               P(_abi.ScheduleInfo)] + [I32] * 12
         lib.dynohip_plan_schedule.restype = C.c_int
+        lib.dynohip_plan_export.argtypes = [P(_abi.GraphView), P(C.c_uint64), P(C.c_uint8), C.c_size_t, C.c_int,
+                                            C.c_int, C.c_char_p, I32, C.c_size_t, P(C.c_size_t)]
+        lib.dynohip_plan_export.restype = C.c_int
+        lib.dynohip_set_partition.argtypes = [vp, C.c_int, C.c_int, _abi.ALLREDUCE_FN, vp]
+        lib.dynohip_set_partition.restype = C.c_int
+        lib.dynohip_value_owner.argtypes = [vp, I32, C.c_size_t, P(C.c_int64)]
+        lib.dynohip_value_owner.restype = C.c_int
         lib.dynohip_full_batch_trigger.argtypes = [C.c_int64, C.c_uint64]
         lib.dynohip_full_batch_trigger.restype = C.c_int
         for fn, args, res in [

@@ -650,7 +650,8 @@ __global__ __launch_bounds__(kBlock) void k_gather_point(PointGatherDev p, const
 // a wave per 6x6 target
 __device__ __forceinline__ void gather_band(const GatherDev& g, const int32_t* __restrict__ tA,
                                             const int32_t* __restrict__ tB, int blk,
-                                            const double* __restrict__ arena, const TileDev& b, double lambda) {
+                                            const double* __restrict__ arena, const TileDev& b, double lambda,
+                                            const uint8_t* __restrict__ damp) {
   const int t = (blk * kBlock + static_cast<int>(threadIdx.x)) >> 6;
   const int q = threadIdx.x & 63;
   if (t >= g.n) return;
@@ -668,7 +669,7 @@ __device__ __forceinline__ void gather_band(const GatherDev& g, const int32_t* _
   const int r = idx / 6, c = idx % 6;
   if (A == B && r < c) return;
   const int row = 6 * A + r, col = 6 * B + c;
-  const double val = a1[0] + (A == B && r == c ? lambda : 0.0);
+  const double val = a1[0] + (A == B && r == c && (!damp || damp[row]) ? lambda : 0.0);
   const int64_t at = tile_index(b, row, col);
   b.slots[at] = val;
   // diagonal tiles are stored full (symmetric), so the factorisation reads
@@ -708,7 +709,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_reduced(ReducedGatherDev r, c
                                                            TileDev b, double lambda) {
   const int hb = blockIdx.x;
   if (hb < r.nb_band) {
-    gather_band(r.band, r.tA, r.tB, xcd_block(hb, r.nb_band), arena, b, lambda);
+    gather_band(r.band, r.tA, r.tB, xcd_block(hb, r.nb_band), arena, b, lambda, r.damp);
   } else if (hb < r.nb_band + r.nb_grad) {
     gather_grad(r.grad, xcd_block(hb - r.nb_band, r.nb_grad), arena, r.gred);
   } else {
@@ -1124,8 +1125,10 @@ void launch_gather_point(const GatherDev (&g)[4], double* const (&dst)[4], const
 }
 
 void launch_gather_reduced(const GatherDev& band, const int32_t* tA, const int32_t* tB, const GatherDev& grad,
-                           double* gred, const double* arena, const TileDev& b, double lambda, hipStream_t s) {
+                           double* gred, const double* arena, const TileDev& b, double lambda, hipStream_t s,
+                           const uint8_t* damp) {
   ReducedGatherDev r;
+  r.damp = damp;
   r.band = band;
   r.tA = tA;
   r.tB = tB;
@@ -1136,6 +1139,25 @@ void launch_gather_reduced(const GatherDev& band, const int32_t* tA, const int32
   const int nb = r.nb_band + r.nb_grad + nblocks(std::max(0, b.NT * kTile - b.n_red));
   if (nb == 0) return;
   k_gather_reduced<<<nb, kBlock, 0, s>>>(r, arena, b, lambda);
+}
+
+// a 64-thread workgroup per separator tile: lane l owns row 64 s + l
+__global__ __launch_bounds__(64) void k_sep_rhs(const int32_t* __restrict__ tile, const int32_t* __restrict__ start,
+                                                const int32_t* __restrict__ slot, double* __restrict__ r,
+                                                double* __restrict__ contrib) {
+  const int q = blockIdx.x, l = threadIdx.x;
+  double acc = 0.0;
+  for (int e = start[q]; e < start[q + 1]; ++e) {
+    double* c = contrib + static_cast<int64_t>(slot[e]) * kTile + l;
+    acc += *c;
+    *c = 0.0;
+  }
+  r[static_cast<int64_t>(tile[q]) * kTile + l] -= acc;
+}
+
+void launch_sep_rhs(int n_sep_tiles, const int32_t* tile, const int32_t* start, const int32_t* slot, double* r,
+                    double* contrib, hipStream_t s) {
+  if (n_sep_tiles > 0) k_sep_rhs<<<n_sep_tiles, 64, 0, s>>>(tile, start, slot, r, contrib);
 }
 
 void launch_chain_factor(const ChainDev& c, double* arena, double lambda, int* fail, const ZeroDev& z,

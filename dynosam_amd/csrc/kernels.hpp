@@ -40,6 +40,7 @@ struct ReducedGatherDev {
   GatherDev grad;              // 6-vector reduced gradient per pose
   double* gred = nullptr;
   int nb_band = 0, nb_grad = 0;
+  const uint8_t* damp = nullptr;  // partitioned: per reduced row, 1 = this rank adds lambda (null: every row)
 };
 
 // buffers zeroed by the blocks past the chains in k_chain_factor
@@ -112,7 +113,12 @@ void launch_linerr(const TypeDev* td, const double* arena, const double* dpose, 
 void launch_gather_point(const GatherDev (&g)[4], double* const (&dst)[4], const double* arena, hipStream_t s);
 // reduced blocks into their tiles (+ lambda), reduced gradient, identity padding
 void launch_gather_reduced(const GatherDev& band, const int32_t* tA, const int32_t* tB, const GatherDev& grad,
-                           double* gred, const double* arena, const TileDev& b, double lambda, hipStream_t s);
+                           double* gred, const double* arena, const TileDev& b, double lambda, hipStream_t s,
+                           const uint8_t* damp = nullptr);
+// partitioned: r[rows of separator tile] -= sum of this rank's contributions
+// L(s,c) y_c (c interior), which are then zeroed; CSR over separator tiles
+void launch_sep_rhs(int n_sep_tiles, const int32_t* tile, const int32_t* start, const int32_t* slot, double* r,
+                    double* contrib, hipStream_t s);
 
 void launch_chain_factor(const ChainDev& c, double* arena, double lambda, int* fail, const ZeroDev& z,
                          hipStream_t s);
@@ -128,6 +134,14 @@ void launch_backsub(const ChainDev& c, int n_edge, const double* arena, const do
 // Wide levels (many update tasks) run their updates as a separate
 // small-LDS kernel on `side`, concurrently with the level's panels on `s`
 // (joined through ev_main / ev_side).
+// the two halves of launch_tile_cholesky_solve (the partitioned solve runs
+// the forward tasks in two phases around the exchange)
+void launch_tile_forward(const TileDev& b, const TileSchedDev& sd, const std::vector<int32_t>& flevel,
+                         const std::vector<int32_t>& fpanels, double* Linv, const double* r, double* contrib,
+                         double* y, int* fail, hipStream_t s, hipStream_t side, hipEvent_t ev_main,
+                         hipEvent_t ev_side);
+void launch_tile_backward(const TileDev& b, const TileSchedDev& sd, const std::vector<int32_t>& blevel,
+                          const double* Linv, const double* y, double* x, int* fail, hipStream_t s);
 void launch_tile_cholesky_solve(const TileDev& b, const TileSchedDev& sd, const std::vector<int32_t>& flevel,
                                 const std::vector<int32_t>& fpanels, const std::vector<int32_t>& blevel,
                                 double* Linv, const double* r, double* contrib, double* y, double* x, int* fail,

@@ -1,0 +1,251 @@
+// partition.cpp — the full-batch graph split over ranks for the partitioned
+// Schur solve (BASELINE configs[4]: "landmark-block
+// partitioned Schur with RCCL reduce of reduced system").
+//
+// The reference solves the whole graph in one GTSAM process
+// (RGBDBackendModule.cc:207-231). Here the nested dissection of the reduced
+// pose system (tiles.cpp) is forced to split its top log2(nranks) levels, so
+// rank r owns one time-contiguous subtree of tiles (its interior) and the
+// separators above the subtrees belong to no rank. A factor that touches an
+// interior tile of r, and every factor of a landmark chain that does, is
+// linearised and Schur-eliminated on r only; the separators' dissection
+// guarantees no factor or chain touches two interiors. Factors touching only
+// separator tiles go to rank 0. Every rank holds all poses (the reduced
+// system keeps global numbering) and only its own landmarks.
+//
+// Per LM solve each rank eliminates its landmarks and its interior columns
+// locally; the separator tiles and right-hand side rows then hold that rank's
+// partial Schur complement, which the ranks sum (one all-reduce), and every
+// rank factors the small separator system redundantly (solver.cpp).
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "plan.hpp"
+
+namespace dynohip {
+
+dynohip_graph_view GraphStore::view() const {
+  dynohip_graph_view g;
+  std::memset(&g, 0, sizeof(g));
+  dynohip_factor_block* b[kNTypes] = {&g.pose_to_point, &g.landmark_motion_ternary, &g.between,
+                                      &g.prior, &g.landmark_motion_pose, &g.landmark_pose_smoothing};
+  for (int t = 0; t < kNTypes; ++t) {
+    b[t]->n = n[t];
+    b[t]->keys = keys[t].empty() ? nullptr : keys[t].data();
+    b[t]->measured = meas[t].empty() ? nullptr : meas[t].data();
+    b[t]->sigmas = sig[t].empty() ? nullptr : sig[t].data();
+    b[t]->huber_k = hub[t].empty() ? nullptr : hub[t].data();
+  }
+  return g;
+}
+
+namespace {
+
+// owner merge: -1 = no interior seen yet; -2 = conflict
+int32_t merge_owner(int32_t a, int32_t b) {
+  if (a == -2 || b == -2) return -2;
+  if (a < 0) return b;
+  if (b < 0) return a;
+  return a == b ? a : -2;
+}
+
+}  // namespace
+
+int build_partitioned_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t* kind, size_t n,
+                           int nranks, int rank, Plan& L, Partition& part, GraphStore& lg, std::string& err) {
+  if (nranks < 2 || (nranks & (nranks - 1)) != 0 || rank < 0 || rank >= nranks) {
+    err = "partitioned solve needs a power-of-two rank count >= 2 and 0 <= rank < nranks";
+    return DYNOHIP_EINVAL;
+  }
+  Plan G;
+  int rc = build_plan(g, keys, kind, n, G, err, nranks, rank, true);
+  if (rc) return rc;
+  part = Partition();
+  part.nranks = nranks;
+  part.rank = rank;
+  auto pose_owner = [&](int32_t p) {
+    int32_t o = -1;
+    for (int t = (6 * p) / kTile; t <= (6 * p + 5) / kTile; ++t) o = merge_owner(o, G.tile_owner[t]);
+    return o;
+  };
+  std::vector<int32_t> comp_of(G.n_pt);
+  for (int c = 0; c < G.n_comp; ++c)
+    for (int32_t i = G.comp_start[c]; i < G.comp_start[c + 1]; ++i) comp_of[i] = c;
+  // pass 1: landmark chains take the union of their factors' pose owners
+  std::vector<int32_t> comp_own(G.n_comp, -1);
+  std::vector<int32_t> fown[kNTypes];
+  for (int t = 0; t < kNTypes; ++t) {
+    const TypePlan& tp = G.types[t];
+    const int nk = kNKeys[t];
+    fown[t].assign(tp.n, -1);
+    for (int i = 0; i < tp.n; ++i) {
+      int32_t o = -1;
+      for (int sl = 0; sl < nk; ++sl)
+        if (kSlotKind[t][sl] == 0) o = merge_owner(o, pose_owner(tp.idx[i * nk + sl]));
+      fown[t][i] = o;
+      for (int sl = 0; sl < nk; ++sl)
+        if (kSlotKind[t][sl] == 1) {
+          const int c = comp_of[tp.idx[i * nk + sl]];
+          comp_own[c] = merge_owner(comp_own[c], o);
+        }
+    }
+  }
+  for (int c = 0; c < G.n_comp; ++c) {
+    if (comp_own[c] == -2) {
+      err = "internal: a landmark chain spans two partitions";
+      return DYNOHIP_ESTRUCT;
+    }
+    if (comp_own[c] < 0) comp_own[c] = 0;  // separator-only chains: rank 0
+  }
+  // pass 2: factor owners, the local graph in the global factor order
+  const dynohip_factor_block* gb[kNTypes] = {&g.pose_to_point, &g.landmark_motion_ternary, &g.between,
+                                             &g.prior, &g.landmark_motion_pose, &g.landmark_pose_smoothing};
+  lg = GraphStore();
+  for (int t = 0; t < kNTypes; ++t) {
+    const TypePlan& tp = G.types[t];
+    const int nk = kNKeys[t];
+    for (int i = 0; i < tp.n; ++i) {
+      int32_t o = fown[t][i];
+      for (int sl = 0; sl < nk; ++sl)
+        if (kSlotKind[t][sl] == 1) o = merge_owner(o, comp_own[comp_of[tp.idx[i * nk + sl]]]);
+      if (o == -2) {
+        err = "internal: a factor spans two partitions";
+        return DYNOHIP_ESTRUCT;
+      }
+      if (o < 0) o = 0;
+      part.factors_total++;
+      if (o != rank) continue;
+      part.factors_local++;
+      lg.n[t]++;
+      lg.keys[t].insert(lg.keys[t].end(), gb[t]->keys + static_cast<size_t>(i) * nk,
+                        gb[t]->keys + static_cast<size_t>(i + 1) * nk);
+      if (kMeasDim[t])
+        lg.meas[t].insert(lg.meas[t].end(), gb[t]->measured + static_cast<size_t>(i) * kMeasDim[t],
+                          gb[t]->measured + static_cast<size_t>(i + 1) * kMeasDim[t]);
+      lg.sig[t].insert(lg.sig[t].end(), gb[t]->sigmas + static_cast<size_t>(i) * kDim[t],
+                       gb[t]->sigmas + static_cast<size_t>(i + 1) * kDim[t]);
+      lg.hub[t].push_back(gb[t]->huber_k ? gb[t]->huber_k[i] : 0.0);
+    }
+  }
+  // values: every pose, this rank's landmarks
+  part.value_owner.assign(n, -1);
+  part.local_of.assign(n, -1);
+  for (size_t v = 0; v < n; ++v) {
+    const int32_t li = G.user_idx[v];
+    const int32_t o = kind[v] == DYNOHIP_POSE3 ? pose_owner(li) : comp_own[comp_of[li]];
+    part.value_owner[v] = o;
+    if (kind[v] == DYNOHIP_POSE3 || o == rank) {
+      part.local_of[v] = static_cast<int32_t>(part.keys.size());
+      part.keys.push_back(keys[v]);
+      part.kind.push_back(kind[v]);
+      part.global_of.push_back(static_cast<int32_t>(v));
+    }
+  }
+  const dynohip_graph_view lv = lg.view();
+  rc = build_plan(lv, part.keys.data(), part.kind.data(), part.keys.size(), L, err, nranks, rank, false);
+  if (rc) return rc;
+  if (L.n_pose != G.n_pose || L.NT != G.NT || L.pose_key != G.pose_key) {
+    err = "internal: local pose numbering differs from the global one";
+    return DYNOHIP_ESTRUCT;
+  }
+  // the global partitioned schedule
+  L.nd_leaf = G.nd_leaf;
+  L.tile_pos = std::move(G.tile_pos);
+  L.n_slots = G.n_slots;
+  L.row_start = std::move(G.row_start);
+  L.row_col = std::move(G.row_col);
+  L.row_slot = std::move(G.row_slot);
+  L.ftask = std::move(G.ftask);
+  L.pairs = std::move(G.pairs);
+  L.flevel = std::move(G.flevel);
+  L.fpanels = std::move(G.fpanels);
+  L.fdep_start = std::move(G.fdep_start);
+  L.fdep = std::move(G.fdep);
+  L.btask = std::move(G.btask);
+  L.blevel = std::move(G.blevel);
+  L.bent = std::move(G.bent);
+  L.back_part_tiles = G.back_part_tiles;
+  L.bpart = std::move(G.bpart);
+  L.bplevel = std::move(G.bplevel);
+  L.n_partials = G.n_partials;
+  L.tile_flops = G.tile_flops;
+  L.tile_owner = std::move(G.tile_owner);
+  L.ftask1 = std::move(G.ftask1);
+  L.flevel1 = std::move(G.flevel1);
+  L.fpanels1 = std::move(G.fpanels1);
+  L.fdep_start1 = std::move(G.fdep_start1);
+  L.fdep1 = std::move(G.fdep1);
+  L.sep_slot_ranges = std::move(G.sep_slot_ranges);
+  L.sep_tile_ranges = std::move(G.sep_tile_ranges);
+  L.band_D = std::move(G.band_D);
+  L.max_D = G.max_D;
+  // damping: interior rows by their owner, separator rows by rank 0 (the
+  // ranks' diagonals are summed in the exchange)
+  part.damp_row.assign(static_cast<size_t>(L.n_red), 0);
+  for (int q = 0; q < L.n_red; ++q) {
+    const int32_t o = L.tile_owner[q / kTile];
+    part.damp_row[q] = (o == rank || (o < 0 && rank == 0)) ? 1 : 0;
+  }
+  return DYNOHIP_OK;
+}
+
+}  // namespace dynohip
+
+// Host-only introspection of the partitioned plan (tests/test_partition.py
+// replays it in numpy): one named int32 array of rank `rank`'s plan.
+extern "C" int dynohip_plan_export(const dynohip_graph_view* g, const uint64_t* keys, const uint8_t* kind, size_t n,
+                                   int nranks, int rank, const char* name, int32_t* out, size_t cap,
+                                   size_t* n_out) {
+  using namespace dynohip;
+  if (!g || !name || !n_out || (n && (!keys || !kind))) return DYNOHIP_EINVAL;
+  Plan P;
+  Partition part;
+  GraphStore lg;
+  std::string err;
+  const int rc = nranks > 1 ? build_partitioned_plan(*g, keys, kind, n, nranks, rank, P, part, lg, err)
+                            : build_plan(*g, keys, kind, n, P, err);
+  if (rc) return rc;
+  const std::string nm(name);
+  std::vector<int32_t> tmp;
+  const int32_t* src = nullptr;
+  size_t cnt = 0;
+  auto vec = [&](const std::vector<int32_t>& v) {
+    src = v.data();
+    cnt = v.size();
+  };
+  auto raw = [&](const void* p, size_t bytes) {
+    src = static_cast<const int32_t*>(p);
+    cnt = bytes / 4;
+  };
+  if (nm == "info") {
+    tmp = {P.n_pose, P.NT, P.n_slots, P.nd_leaf, P.n_pt, static_cast<int32_t>(part.factors_local),
+           static_cast<int32_t>(part.factors_total)};
+    vec(tmp);
+  } else if (nm == "tile_pos") vec(P.tile_pos);
+  else if (nm == "tile_owner") vec(P.tile_owner);
+  else if (nm == "row_start") vec(P.row_start);
+  else if (nm == "row_col") vec(P.row_col);
+  else if (nm == "row_slot") vec(P.row_slot);
+  else if (nm == "pairs") vec(P.pairs);
+  else if (nm == "ftask") raw(P.ftask.data(), P.ftask.size() * sizeof(TileTask));
+  else if (nm == "flevel") vec(P.flevel);
+  else if (nm == "ftask1") raw(P.ftask1.data(), P.ftask1.size() * sizeof(TileTask));
+  else if (nm == "flevel1") vec(P.flevel1);
+  else if (nm == "bpart") raw(P.bpart.data(), P.bpart.size() * sizeof(BackPart));
+  else if (nm == "bplevel") vec(P.bplevel);
+  else if (nm == "bent") vec(P.bent);
+  else if (nm == "sep_slot_ranges") vec(P.sep_slot_ranges);
+  else if (nm == "sep_tile_ranges") vec(P.sep_tile_ranges);
+  else if (nm == "red_a") vec(P.red_A);
+  else if (nm == "red_b") vec(P.red_B);
+  else if (nm == "value_owner") vec(part.value_owner);
+  else if (nm == "damp_row") {
+    tmp.assign(part.damp_row.begin(), part.damp_row.end());
+    vec(tmp);
+  } else return DYNOHIP_EINVAL;
+  *n_out = cnt;
+  if (out && cnt) std::memcpy(out, src, std::min(cap, cnt) * 4);
+  return DYNOHIP_OK;
+}

@@ -60,8 +60,10 @@ void to_csr(size_t ntargets, std::vector<std::pair<int32_t, GEntry>>& pairs, Gat
 }  // namespace
 
 int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t* kind, size_t n, Plan& P,
-               std::string& err) {
+               std::string& err, int nranks, int rank, bool with_schedule) {
   P = Plan();
+  P.nranks = nranks;
+  P.rank = rank;
   // ---- values: key lookup ----
   std::unordered_map<uint64_t, int32_t> key_to_user;
   key_to_user.reserve(n * 2 + 1);
@@ -421,7 +423,10 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
     P.band_D[j] = rlow[j] - j;
     P.max_D = std::max(P.max_D, P.band_D[j]);
   }
-  build_tile_schedule(P);
+  if (with_schedule && !build_tile_schedule(P)) {
+    err = "graph too short in time for " + std::to_string(nranks) + " partitions";
+    return DYNOHIP_ESTRUCT;
+  }
   return DYNOHIP_OK;
 }
 

@@ -159,14 +159,54 @@ struct Plan {
   std::vector<int32_t> bplevel;         // level l = bpart [bplevel[l], bplevel[l+1])
   int32_t n_partials = 0;
   double tile_flops = 0.0;              // tile-level factorisation flops (incl. fill)
+  // partitioned full-batch solve. nranks > 1: the
+  // lists above hold this rank's phase-0 tasks and its backward parts
+  // (separator columns first); the *1 lists the separator tasks run after
+  // the exchange
+  int nranks = 1, rank = 0;
+  std::vector<int32_t> tile_owner;      // per tile: owning rank, -1 = top separator
+  std::vector<TileTask> ftask1;
+  std::vector<int32_t> flevel1, fpanels1, fdep_start1, fdep1;
+  std::vector<int32_t> sep_slot_ranges; // [beg, end) slot ranges of the separator columns
+  std::vector<int32_t> sep_tile_ranges; // [beg, end) tile ranges (natural order) of the separators
 };
 
 // Orders the tiles (nested dissection over frame order), computes the
-// tile-level fill and the task DAG with its level schedule.
-void build_tile_schedule(Plan& P);
+// tile-level fill and the task DAG with its level schedule. With
+// P.nranks > 1 the top of the dissection is split into rank subtrees; false
+// when the graph is too short for that many.
+bool build_tile_schedule(Plan& P);
 
-// returns DYNOHIP_OK or an error code with `err` filled
+// returns DYNOHIP_OK or an error code with `err` filled. nranks > 1 builds
+// the partitioned tile schedule of `rank` (the graph is the global one);
+// with_schedule = false stops after the reduced-system structure.
 int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t* kind, size_t n, Plan& plan,
-               std::string& err);
+               std::string& err, int nranks = 1, int rank = 0, bool with_schedule = true);
+
+// Partitioned full-batch solve: what one rank holds (partition.cpp).
+struct Partition {
+  int nranks = 1, rank = 0;
+  std::vector<int32_t> value_owner;     // per global value: owning rank, -1 = replicated (separator pose)
+  std::vector<int32_t> local_of;        // per global value: index in the local value list, -1 = not held
+  std::vector<uint64_t> keys;           // local value list (all poses + this rank's points)
+  std::vector<uint8_t> kind;
+  std::vector<int32_t> global_of;       // per local value: global index
+  std::vector<uint8_t> damp_row;        // per reduced row: this rank adds lambda
+  size_t factors_local = 0, factors_total = 0;
+};
+
+// Splits the global graph over nranks time-contiguous subtrees of the
+// nested dissection; builds this rank's local plan (its factors, all poses,
+// its points) carrying the global partitioned tile schedule. `local_graph`
+// receives the storage the local plan's graph view points into.
+struct GraphStore {
+  std::vector<uint64_t> keys[kNTypes];
+  std::vector<double> meas[kNTypes], sig[kNTypes], hub[kNTypes];
+  size_t n[kNTypes] = {};
+  dynohip_graph_view view() const;
+};
+int build_partitioned_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t* kind, size_t n,
+                           int nranks, int rank, Plan& local, Partition& part, GraphStore& local_graph,
+                           std::string& err);
 
 }  // namespace dynohip

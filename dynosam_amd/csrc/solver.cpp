@@ -144,6 +144,20 @@ struct dynohip_solver {
   double phase_ms[7] = {};   // accumulated: lin, schur, assembly, chol, solve, backsub+linerr, retract+error
   int64_t n_lin = 0, n_solves = 0;
   dynohip_stats base_stats{};
+  // partitioned full-batch solve (partition.cpp): this handle is rank
+  // `rank` of `nranks`; `comm` sums over ranks
+  int nranks = 1, rank = 0;
+  dynohip_allreduce_fn comm = nullptr;
+  void* comm_ctx = nullptr;
+  Partition part;
+  GraphStore local_graph;
+  std::vector<uint8_t> value_kind;   // global value kinds
+  DevBuf<uint8_t> damp;
+  DevBuf<TileTask> ftask1;
+  DevBuf<int32_t> fdep_start1, fdep1, seprhs_tile, seprhs_start, seprhs_slot;
+  DevBuf<double> xbuf;
+  TileSchedDev sd1;
+  int n_seprhs = 0;
 };
 
 namespace {
@@ -284,6 +298,74 @@ int upload_plan(dynohip_solver* s) {
   return 0;
 }
 
+int upload_partition(dynohip_solver* s) {
+  Plan& P = s->plan;
+  hipStream_t st = s->stream;
+  HIPCHK(s, s->damp.upload(s->part.damp_row, st));
+  HIPCHK(s, s->ftask1.upload(P.ftask1, st));
+  HIPCHK(s, s->fdep_start1.upload(P.fdep_start1, st));
+  HIPCHK(s, s->fdep1.upload(P.fdep1, st));
+  s->sd1 = s->sd;
+  s->sd1.ftask = s->ftask1.p;
+  s->sd1.fdep_start = s->fdep_start1.p;
+  s->sd1.fdep = s->fdep1.p;
+  // separator right-hand-side rows: this rank's interior contributions
+  std::vector<int32_t> tl, ts(1, 0), sl;
+  for (size_t r = 0; r + 1 < P.sep_tile_ranges.size(); r += 2)
+    for (int32_t t = P.sep_tile_ranges[r]; t < P.sep_tile_ranges[r + 1]; ++t) {
+      tl.push_back(t);
+      for (int32_t e = P.row_start[t]; e < P.row_start[t + 1]; ++e)
+        if (P.tile_owner[P.row_col[e]] == s->rank) sl.push_back(P.row_slot[e]);
+      ts.push_back(static_cast<int32_t>(sl.size()));
+    }
+  s->n_seprhs = static_cast<int>(tl.size());
+  HIPCHK(s, s->seprhs_tile.upload(tl, st));
+  HIPCHK(s, s->seprhs_start.upload(ts, st));
+  HIPCHK(s, s->seprhs_slot.upload(sl, st));
+  size_t nx = 0;
+  for (size_t r = 0; r + 1 < P.sep_slot_ranges.size(); r += 2)
+    nx += static_cast<size_t>(P.sep_slot_ranges[r + 1] - P.sep_slot_ranges[r]) * kTile * kTile;
+  for (size_t r = 0; r + 1 < P.sep_tile_ranges.size(); r += 2)
+    nx += static_cast<size_t>(P.sep_tile_ranges[r + 1] - P.sep_tile_ranges[r]) * kTile;
+  HIPCHK(s, s->xbuf.alloc(nx));
+  // rows and contributions of other ranks' interiors are never written
+  // here: keep them zero (their poses then retract by zero)
+  HIPCHK(s, hipMemsetAsync(s->contrib.p, 0, s->contrib.n * sizeof(double), st));
+  HIPCHK(s, hipMemsetAsync(s->xy.p, 0, s->xy.n * sizeof(double), st));
+  HIPCHK(s, hipStreamSynchronize(st));
+  return 0;
+}
+
+// sum over ranks (partitioned); no-op on an ordinary handle
+int comm_sum(dynohip_solver* s, double* buf, size_t n, int on_device) {
+  if (s->nranks <= 1 || n == 0) return 0;
+  if (!s->comm || s->comm(s->comm_ctx, buf, n, on_device) != 0)
+    return set_err(s, DYNOHIP_EHIP, "partition exchange (all-reduce of %zu doubles) failed", n);
+  return 0;
+}
+
+// copies the separator tiles and RHS rows into / out of the exchange buffer
+int sep_copy(dynohip_solver* s, bool pack) {
+  Plan& P = s->plan;
+  size_t o = 0;
+  auto cp = [&](double* dev, size_t cnt) -> int {
+    double* a = pack ? s->xbuf.p + o : dev;
+    const double* b = pack ? dev : s->xbuf.p + o;
+    HIPCHK(s, hipMemcpyAsync(a, b, cnt * sizeof(double), hipMemcpyDeviceToDevice, s->stream));
+    o += cnt;
+    return 0;
+  };
+  for (size_t r = 0; r + 1 < P.sep_slot_ranges.size(); r += 2)
+    if (cp(s->slots.p + static_cast<size_t>(P.sep_slot_ranges[r]) * kTile * kTile,
+           static_cast<size_t>(P.sep_slot_ranges[r + 1] - P.sep_slot_ranges[r]) * kTile * kTile))
+      return DYNOHIP_EHIP;
+  for (size_t r = 0; r + 1 < P.sep_tile_ranges.size(); r += 2)
+    if (cp(s->gred.p + static_cast<size_t>(P.sep_tile_ranges[r]) * kTile,
+           static_cast<size_t>(P.sep_tile_ranges[r + 1] - P.sep_tile_ranges[r]) * kTile))
+      return DYNOHIP_EHIP;
+  return 0;
+}
+
 // error at (pose, pt) into result[slot]
 void enqueue_error(dynohip_solver* s, const double* pose, const double* pt, double* partials, double* out) {
   launch_error(s->td, pose, pt, partials, s->sumctr.p, out, s->failp, reinterpret_cast<int*>(s->result.p + 4),
@@ -298,7 +380,7 @@ int compute_error(dynohip_solver* s, const double* pose, const double* pt, doubl
   enqueue_error(s, pose, pt, s->partials.p, s->result.p);
   HIPCHK(s, hipMemcpyAsync(err_out, s->result.p, sizeof(double), hipMemcpyDeviceToHost, s->stream));
   HIPCHK(s, hipStreamSynchronize(s->stream));
-  return 0;
+  return comm_sum(s, err_out, 1, 0);
 }
 
 // linearisation + point-side blocks (once per outer iteration); lin0, when
@@ -315,7 +397,7 @@ void enqueue_linearize(dynohip_solver* s, const double* pose, const double* pt, 
 
 // damped solve + linearised error + retract + error for one lambda.
 // result[0] = new linear error, result[1] = new nonlinear error; fail flag.
-void enqueue_try(dynohip_solver* s, double lambda) {
+int enqueue_try(dynohip_solver* s, double lambda) {
   const bool timed = s->timing;
   Plan& P = s->plan;
   hipStream_t st = s->stream;
@@ -333,13 +415,34 @@ void enqueue_try(dynohip_solver* s, double lambda) {
   launch_chain_solve_y(s->cd, A, st);
   if (timed) (void)hipEventRecord(s->ev[3], st);
   launch_gather_reduced(s->gRed.dev(P.gRed.ntargets()), s->redA.p, s->redB.p, s->gGred.dev(P.gGred.ntargets()),
-                        s->gred.p, A, s->bd, lambda, st);
+                        s->gred.p, A, s->bd, lambda, st, s->nranks > 1 ? s->damp.p : nullptr);
   if (timed) (void)hipEventRecord(s->ev[4], st);
   double* y = s->xy.p;
   double* x = s->xy.p + nrp;
   if (++s->sd.epoch == 0) s->sd.epoch = 1;  // stamps of earlier solves never match
-  launch_tile_cholesky_solve(s->bd, s->sd, P.flevel, P.fpanels, P.bplevel, s->linv.p, s->gred.p, s->contrib.p, y,
-                             x, s->failp, st, s->side, s->ev_main, s->ev_side);
+  if (s->nranks > 1) {
+    // phase 0: this rank's subtree and its updates of the separator tiles;
+    // its interior contributions leave the separator RHS rows
+    launch_tile_forward(s->bd, s->sd, P.flevel, P.fpanels, s->linv.p, s->gred.p, s->contrib.p, y, s->failp, st,
+                        s->side, s->ev_main, s->ev_side);
+    launch_sep_rhs(s->n_seprhs, s->seprhs_tile.p, s->seprhs_start.p, s->seprhs_slot.p, s->gred.p, s->contrib.p, st);
+    // exchange: the separator system summed over ranks
+    if (sep_copy(s, true)) return DYNOHIP_EHIP;
+    HIPCHK(s, hipStreamSynchronize(st));
+    int rc = comm_sum(s, s->xbuf.p, s->xbuf.n, 1);
+    if (rc) return rc;
+    if (sep_copy(s, false)) return DYNOHIP_EHIP;
+    HIPCHK(s, hipMemsetAsync(s->fsync.p, 0, s->fsync.n * sizeof(unsigned), st));
+    // phase 1 (every rank, identical inputs): the separator columns, then
+    // the backward substitution of the separators and this rank's interior
+    s->sd1.epoch = s->sd.epoch;
+    launch_tile_forward(s->bd, s->sd1, P.flevel1, P.fpanels1, s->linv.p, s->gred.p, s->contrib.p, y, s->failp, st,
+                        s->side, s->ev_main, s->ev_side);
+    launch_tile_backward(s->bd, s->sd, P.bplevel, s->linv.p, y, x, s->failp, st);
+  } else {
+    launch_tile_cholesky_solve(s->bd, s->sd, P.flevel, P.fpanels, P.bplevel, s->linv.p, s->gred.p, s->contrib.p, y,
+                               x, s->failp, st, s->side, s->ev_main, s->ev_side);
+  }
   if (timed) (void)hipEventRecord(s->ev[5], st);
   if (timed) (void)hipEventRecord(s->ev[6], st);
   // pose deltas are x[0 .. 6 n_pose) in pose-index order
@@ -349,6 +452,7 @@ void enqueue_try(dynohip_solver* s, double lambda) {
   launch_retract(P.n_pose, P.n_pt, s->pose.p, s->pt.p, x, s->dpt.p, s->pose_c.p, s->pt_c.p, st);
   enqueue_error(s, s->pose_c.p, s->pt_c.p, s->partials.p + s->partial_slots, s->result.p + 1);
   if (timed) (void)hipEventRecord(s->ev[8], st);
+  return 0;
 }
 
 void push_trace(dynohip_solver* s, const dynohip_trace_entry& e) { s->trace.push_back(e); }
@@ -439,7 +543,8 @@ int lm_iterate(dynohip_solver* s) {
       s->n_lin++;
       relinearize = false;
     }
-    enqueue_try(s, s->lambda);
+    int trc = enqueue_try(s, s->lambda);
+    if (trc) return trc;
     if (speculate) {
       enqueue_linearize(s, s->pose_c.p, s->pt_c.p, s->result.p + 3);
     }
@@ -448,6 +553,15 @@ int lm_iterate(dynohip_solver* s) {
     HIPCHK(s, hipStreamSynchronize(st));
     int fail = 0;
     std::memcpy(&fail, &res[4], sizeof(int));
+    if (s->nranks > 1) {
+      // errors are sums over the ranks' factors; fail bits are OR-ed
+      double red[8] = {res[0], res[1], res[2], res[3], (fail & 1) ? 1.0 : 0.0, (fail & 2) ? 1.0 : 0.0,
+                       (fail & 4) ? 1.0 : 0.0, 0.0};
+      int rc = comm_sum(s, red, 8, 0);
+      if (rc) return rc;
+      for (int k = 0; k < 4; ++k) res[k] = red[k];
+      fail = (red[4] > 0 ? 1 : 0) | (red[5] > 0 ? 2 : 0) | (red[6] > 0 ? 4 : 0);
+    }
     if (!have_old) {
       oldLin = res[2];
       te.old_linear_error = oldLin;
@@ -632,11 +746,18 @@ int dynohip_set_values(dynohip_solver* s, const uint64_t* keys, const uint8_t* k
   if (!same) {
     s->has_plan = false;
     dynohip_graph_view g = s->graph.view();
-    int rc = build_plan(g, keys, kind, n, s->plan, s->err);
+    int rc = s->nranks > 1 ? build_partitioned_plan(g, keys, kind, n, s->nranks, s->rank, s->plan, s->part,
+                                                    s->local_graph, s->err)
+                           : build_plan(g, keys, kind, n, s->plan, s->err);
     if (rc) return rc;
     rc = upload_plan(s);
     if (rc) return rc;
+    if (s->nranks > 1) {
+      rc = upload_partition(s);
+      if (rc) return rc;
+    }
     s->value_keys.assign(keys, keys + n);
+    s->value_kind.assign(kind, kind + n);
     s->has_plan = true;
     compute_base_stats(s);
   }
@@ -644,12 +765,18 @@ int dynohip_set_values(dynohip_solver* s, const uint64_t* keys, const uint8_t* k
   Plan& P = s->plan;
   std::vector<double> hp(12ull * P.n_pose), hq(3ull * P.n_pt);
   size_t off = 0;
+  const bool parted = s->nranks > 1;
   for (size_t i = 0; i < n; ++i) {
-    if (kind[i] != P.user_kind[i]) return set_err(s, DYNOHIP_EINVAL, "value kind changed for key %zu", i);
+    if (kind[i] != s->value_kind[i]) return set_err(s, DYNOHIP_EINVAL, "value kind changed for key %zu", i);
     const int sz = kind[i] == DYNOHIP_POSE3 ? 12 : 3;
     for (int k = 0; k < sz; ++k)
       if (!std::isfinite(data[off + k])) return set_err(s, DYNOHIP_ENONFINITE, "non-finite value");
-    double* dst = kind[i] == DYNOHIP_POSE3 ? &hp[12ull * P.user_idx[i]] : &hq[3ull * P.user_idx[i]];
+    const int32_t u = parted ? s->part.local_of[i] : static_cast<int32_t>(i);
+    if (u < 0) {  // another rank's landmark
+      off += sz;
+      continue;
+    }
+    double* dst = kind[i] == DYNOHIP_POSE3 ? &hp[12ull * P.user_idx[u]] : &hq[3ull * P.user_idx[u]];
     std::memcpy(dst, data + off, sz * sizeof(double));
     off += sz;
   }
@@ -669,12 +796,19 @@ int dynohip_get_values(dynohip_solver* s, double* out, size_t n_doubles) {
   if (!hp.empty()) HIPCHK(s, hipMemcpyAsync(hp.data(), s->pose.p, hp.size() * sizeof(double), hipMemcpyDeviceToHost, s->stream));
   if (!hq.empty()) HIPCHK(s, hipMemcpyAsync(hq.data(), s->pt.p, hq.size() * sizeof(double), hipMemcpyDeviceToHost, s->stream));
   HIPCHK(s, hipStreamSynchronize(s->stream));
-  size_t need = 12ull * P.n_pose + 3ull * P.n_pt;
+  size_t need = 0;
+  for (uint8_t k : s->value_kind) need += k == DYNOHIP_POSE3 ? 12 : 3;
   if (n_doubles < need) return set_err(s, DYNOHIP_EINVAL, "output buffer too small (%zu < %zu)", n_doubles, need);
   size_t off = 0;
-  for (size_t i = 0; i < P.user_kind.size(); ++i) {
-    const int sz = P.user_kind[i] == DYNOHIP_POSE3 ? 12 : 3;
-    const double* src = P.user_kind[i] == DYNOHIP_POSE3 ? &hp[12ull * P.user_idx[i]] : &hq[3ull * P.user_idx[i]];
+  const bool parted = s->nranks > 1;
+  for (size_t i = 0; i < s->value_kind.size(); ++i) {
+    const int sz = s->value_kind[i] == DYNOHIP_POSE3 ? 12 : 3;
+    const int32_t u = parted ? s->part.local_of[i] : static_cast<int32_t>(i);
+    if (u < 0) {
+      off += sz;
+      continue;
+    }
+    const double* src = s->value_kind[i] == DYNOHIP_POSE3 ? &hp[12ull * P.user_idx[u]] : &hq[3ull * P.user_idx[u]];
     std::memcpy(out + off, src, sz * sizeof(double));
     off += sz;
   }
@@ -844,6 +978,29 @@ int dynohip_set_exec_options(dynohip_solver* s, int wide_updates, int level_back
   s->sd.wide_updates = wide_updates;
   s->sd.level_backward = level_backward != 0;
   s->sd.persistent_factor = level_factor == 0;
+  return DYNOHIP_OK;
+}
+
+int dynohip_set_partition(dynohip_solver* s, int nranks, int rank, dynohip_allreduce_fn allreduce, void* ctx) {
+  if (!s || nranks < 1 || rank < 0 || rank >= nranks) return DYNOHIP_EINVAL;
+  if (nranks > 1 && ((nranks & (nranks - 1)) != 0 || !allreduce))
+    return set_err(s, DYNOHIP_EINVAL, "partitioned solve needs a power-of-two rank count and an all-reduce");
+  s->nranks = nranks;
+  s->rank = rank;
+  s->comm = allreduce;
+  s->comm_ctx = ctx;
+  s->has_plan = false;
+  s->has_values = false;
+  s->lin_valid = false;
+  return DYNOHIP_OK;
+}
+
+int dynohip_value_owner(dynohip_solver* s, int32_t* owner_out, size_t n, int64_t* exchange_doubles) {
+  int rc = ready(s);
+  if (rc) return rc;
+  if (n != s->value_kind.size() || (n && !owner_out)) return set_err(s, DYNOHIP_EINVAL, "owner buffer size");
+  for (size_t i = 0; i < n; ++i) owner_out[i] = s->nranks > 1 ? s->part.value_owner[i] : 0;
+  if (exchange_doubles) *exchange_doubles = s->nranks > 1 ? static_cast<int64_t>(s->xbuf.n) : 0;
   return DYNOHIP_OK;
 }
 

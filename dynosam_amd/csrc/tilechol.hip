@@ -855,10 +855,10 @@ __global__ __launch_bounds__(kBackThreads) void k_back_persist(TileDev b, const 
 
 }  // namespace
 
-void launch_tile_cholesky_solve(const TileDev& b, const TileSchedDev& sd, const std::vector<int32_t>& flevel,
-                                const std::vector<int32_t>& fpanels, const std::vector<int32_t>& blevel,
-                                double* Linv, const double* r, double* contrib, double* y, double* x, int* fail,
-                                hipStream_t s, hipStream_t side, hipEvent_t ev_main, hipEvent_t ev_side) {
+void launch_tile_forward(const TileDev& b, const TileSchedDev& sd, const std::vector<int32_t>& flevel,
+                         const std::vector<int32_t>& fpanels, double* Linv, const double* r, double* contrib,
+                         double* y, int* fail, hipStream_t s, hipStream_t side, hipEvent_t ev_main,
+                         hipEvent_t ev_side) {
   // a level is "wide" when its update tasks alone need more than one
   // round of the CUs (sd.wide_updates, default 256): they then run as
   // k_updates on the side stream
@@ -881,6 +881,10 @@ void launch_tile_cholesky_solve(const TileDev& b, const TileSchedDev& sd, const 
       k_tasks<<<n, 256, 0, s>>>(b, sd.ftask + flevel[lv], sd.pairs, Linv, r, contrib, y, fail);
     }
   }
+}
+
+void launch_tile_backward(const TileDev& b, const TileSchedDev& sd, const std::vector<int32_t>& blevel,
+                          const double* Linv, const double* y, double* x, int* fail, hipStream_t s) {
   const int nparts = blevel.empty() ? 0 : blevel.back();
   if (nparts > 0 && nparts <= kBackPersistMax && !sd.level_backward) {
     k_back_persist<<<nparts, kBackThreads, 0, s>>>(b, sd.bpart, sd.bent, Linv, y, x, sd.partials, sd.arrive, sd.done,
@@ -891,6 +895,14 @@ void launch_tile_cholesky_solve(const TileDev& b, const TileSchedDev& sd, const 
     const int n = blevel[lv + 1] - blevel[lv];
     if (n > 0) k_back<<<n, kBackThreads, 0, s>>>(b, sd.bpart + blevel[lv], sd.bent, Linv, y, x, sd.partials, sd.arrive);
   }
+}
+
+void launch_tile_cholesky_solve(const TileDev& b, const TileSchedDev& sd, const std::vector<int32_t>& flevel,
+                                const std::vector<int32_t>& fpanels, const std::vector<int32_t>& blevel,
+                                double* Linv, const double* r, double* contrib, double* y, double* x, int* fail,
+                                hipStream_t s, hipStream_t side, hipEvent_t ev_main, hipEvent_t ev_side) {
+  launch_tile_forward(b, sd, flevel, fpanels, Linv, r, contrib, y, fail, s, side, ev_main, ev_side);
+  launch_tile_backward(b, sd, blevel, Linv, y, x, fail, s);
 }
 
 }  // namespace dynohip

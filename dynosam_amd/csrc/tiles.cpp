@@ -41,6 +41,9 @@ struct Sched {
   int leaf = 0;
   std::vector<int32_t> order;               // tile at position p
   std::vector<int32_t> pos;                 // position of tile t
+  std::vector<int32_t> owner;               // per position: rank subtree, -1 = top separator (partitioned)
+  std::vector<int32_t> task_owner;          // per forward task: rank that runs it, -1 = after the exchange
+  bool ok = true;                           // partitioned: every top split succeeded
   std::vector<std::vector<int32_t>> st;     // per column position: row positions (sorted, incl. itself)
   std::vector<int32_t> slot_base;           // per column position
   int32_t n_slots = 0;
@@ -81,11 +84,49 @@ void nd_order(int lo, int hi, int leaf, const std::vector<int32_t>& maxnb, std::
   for (int t = m; t < s_end; ++t) out.push_back(t);
 }
 
+// Partitioned form: the top log2(nranks) levels of
+// the dissection always split, and rank r owns the r-th leaf subtree in time
+// order (its interior); the separators above them are owned by no rank (-1).
+// Fails (returns false) when a required split is impossible: the graph is
+// too short in time for that many ranks.
+bool nd_order_part(int lo, int hi, int leaf, const std::vector<int32_t>& maxnb, int nr, int r0,
+                   std::vector<int32_t>& out, std::vector<int32_t>& owner) {
+  if (nr == 1) {
+    const size_t b = out.size();
+    nd_order(lo, hi, leaf, maxnb, out);
+    owner.resize(out.size(), r0);
+    (void)b;
+    return true;
+  }
+  const int n = hi - lo;
+  if (n < 3) return false;
+  const int m = lo + n / 2;
+  int reach = m - 1;
+  for (int t = lo; t < m; ++t) reach = std::max(reach, std::min(maxnb[t], hi - 1));
+  const int s_end = reach + 1;
+  if (hi - s_end < 1 || s_end <= m) return false;
+  const int nl = nr / 2;
+  if (!nd_order_part(lo, m, leaf, maxnb, nl, r0, out, owner)) return false;
+  if (!nd_order_part(s_end, hi, leaf, maxnb, nr - nl, r0 + nl, out, owner)) return false;
+  for (int t = m; t < s_end; ++t) {
+    out.push_back(t);
+    owner.push_back(-1);
+  }
+  return true;
+}
+
 void schedule(int NT, const std::vector<std::vector<int32_t>>& adj, const std::vector<int32_t>& maxnb, int leaf,
-              Sched& S) {
+              Sched& S, int nranks = 1) {
   S.leaf = leaf;
   S.order.clear();
-  nd_order(0, NT, leaf, maxnb, S.order);
+  S.owner.clear();
+  if (nranks > 1) {
+    S.ok = nd_order_part(0, NT, leaf, maxnb, nranks, 0, S.order, S.owner);
+    if (!S.ok) return;
+  } else {
+    nd_order(0, NT, leaf, maxnb, S.order);
+    S.owner.assign(NT, 0);
+  }
   S.pos.assign(NT, 0);
   for (int p = 0; p < NT; ++p) S.pos[S.order[p]] = p;
   // ---- symbolic factorisation (elimination tree merge) in position space
@@ -123,6 +164,7 @@ void schedule(int NT, const std::vector<std::vector<int32_t>>& adj, const std::v
   // columns.
   struct Contrib {
     int32_t R, a, b;  // ready level, operand slots (A B^T)
+    int32_t own;      // owner of the source column
   };
   std::vector<std::vector<Contrib>> contrib(ns);
   std::vector<int32_t> lvlP(ns, 0);
@@ -130,19 +172,52 @@ void schedule(int NT, const std::vector<std::vector<int32_t>>& adj, const std::v
     int32_t lvl;
     TileTask t;
     std::vector<int32_t> pd, po;  // pairs
+    int32_t own = 0;              // rank running the task (-1: after the exchange)
   };
   std::vector<LT> tasks;
   const double T3 = static_cast<double>(kTile) * kTile * kTile;
   double flops = 0.0;
   // split contributions (sorted by R) into update tasks finishing before
   // level P and the pairs the panel at level P absorbs
-  auto plan_tile = [&](int32_t sl, int32_t P, std::vector<int32_t>& absorbed) {
-    auto& cs = contrib[sl];
-    std::sort(cs.begin(), cs.end(), [](const Contrib& x, const Contrib& y) { return x.R < y.R; });
+  // Partitioned: a separator tile (target owner -1) takes the contributions
+  // of interior columns as update tasks of their rank, never absorbed by its
+  // panel, so that the tile leaves phase 0 as that rank's partial Schur
+  // complement.
+  auto plan_tile = [&](int32_t sl, int32_t P, std::vector<int32_t>& absorbed, int32_t town) {
+    auto& all = contrib[sl];
+    std::sort(all.begin(), all.end(), [](const Contrib& x, const Contrib& y) { return x.R < y.R; });
+    std::vector<Contrib> cs;
+    if (town < 0) {
+      std::vector<int32_t> owners;
+      for (const Contrib& c : all)
+        if (c.own >= 0) owners.push_back(c.own);
+      std::sort(owners.begin(), owners.end());
+      owners.erase(std::unique(owners.begin(), owners.end()), owners.end());
+      for (int32_t o : owners) {
+        size_t q = 0;
+        std::vector<Contrib> mine;
+        for (const Contrib& c : all)
+          if (c.own == o) mine.push_back(c);
+        while (q < mine.size()) {
+          const int32_t t = mine[q].R + 1;
+          LT u{t, TileTask{1, -1, -1, sl, -1, 0, 0, 0, 0, 0}, {}, {}, o};
+          while (q < mine.size() && mine[q].R <= t - 1) {
+            u.po.push_back(mine[q].a);
+            u.po.push_back(mine[q].b);
+            ++q;
+          }
+          tasks.push_back(std::move(u));
+        }
+      }
+      for (const Contrib& c : all)
+        if (c.own < 0) cs.push_back(c);
+    } else {
+      cs = all;
+    }
     size_t q = 0;
     while (q < cs.size() && cs[q].R <= P - 2) {
       const int32_t t = cs[q].R + 1;
-      LT u{t, TileTask{1, -1, -1, sl, -1, 0, 0, 0, 0, 0}, {}, {}};
+      LT u{t, TileTask{1, -1, -1, sl, -1, 0, 0, 0, 0, 0}, {}, {}, town};
       while (q < cs.size() && cs[q].R <= t - 1) {
         u.po.push_back(cs[q].a);
         u.po.push_back(cs[q].b);
@@ -161,17 +236,18 @@ void schedule(int NT, const std::vector<std::vector<int32_t>>& adj, const std::v
     int32_t Rd = 0;
     for (const Contrib& c : contrib[dslot]) Rd = std::max(Rd, c.R);
     const int32_t Pd = Rd + 1;
+    const int32_t cown = S.owner[cp];
     std::vector<int32_t> pd;
-    plan_tile(dslot, Pd, pd);
+    plan_tile(dslot, Pd, pd, cown);
     flops += T3 / 3.0;
     for (int32_t rp : s) {
       const int32_t sl = S.slot(rp, cp);
-      LT t{Pd, TileTask{0, S.order[cp], S.order[rp], sl, dslot, 0, 0, 0, 0, 0}, pd, {}};
+      LT t{Pd, TileTask{0, S.order[cp], S.order[rp], sl, dslot, 0, 0, 0, 0, 0}, pd, {}, cown};
       if (rp != cp) {
         int32_t Ro = 0;
         for (const Contrib& c : contrib[sl]) Ro = std::max(Ro, c.R);
         t.lvl = std::max(Pd, Ro + 1);
-        plan_tile(sl, t.lvl, t.po);
+        plan_tile(sl, t.lvl, t.po, cown);
         flops += T3;
       }
       lvlP[sl] = t.lvl;
@@ -180,7 +256,7 @@ void schedule(int NT, const std::vector<std::vector<int32_t>>& adj, const std::v
     for (size_t x = 1; x < s.size(); ++x)
       for (size_t y = 1; y <= x; ++y) {
         const int32_t sa = S.slot(s[x], cp), sb = S.slot(s[y], cp);
-        contrib[S.slot(s[x], s[y])].push_back({std::max(lvlP[sa], lvlP[sb]), sa, sb});
+        contrib[S.slot(s[x], s[y])].push_back({std::max(lvlP[sa], lvlP[sb]), sa, sb, cown});
         flops += 2.0 * T3;
       }
   }
@@ -193,6 +269,7 @@ void schedule(int NT, const std::vector<std::vector<int32_t>>& adj, const std::v
   S.ftask.clear();
   S.flevel.clear();
   S.pairs.clear();
+  S.task_owner.clear();
   int cur = 0;
   for (LT& t : tasks) {
     while (cur < t.lvl) {
@@ -207,6 +284,7 @@ void schedule(int NT, const std::vector<std::vector<int32_t>>& adj, const std::v
     put(t.pd, t.t.pd_beg, t.t.pd_end);
     put(t.po, t.t.po_beg, t.t.po_end);
     S.ftask.push_back(t.t);
+    S.task_owner.push_back(t.own);
   }
   S.flevel.push_back(static_cast<int32_t>(S.ftask.size()));
   S.fpanels.assign(S.flevel.size() - 1, 0);
@@ -268,15 +346,16 @@ int g_leaf_override = -1;
 // order, so this reproduces it exactly, including the fixed order in which a
 // tile receives its updates). Slots only written before the factorisation
 // (count 0) are left out.
-void build_dataflow_deps(Plan& P) {
+void build_dataflow_deps(const Plan& P, const std::vector<TileTask>& ftask, const std::vector<int32_t>& flevel,
+                         std::vector<int32_t>& fdep_start, std::vector<int32_t>& fdep) {
   std::vector<int32_t> written(P.n_slots, 0);
-  P.fdep_start.assign(1, 0);
-  P.fdep.clear();
+  fdep_start.assign(1, 0);
+  fdep.clear();
   std::vector<int32_t> touch;
-  const int nlev = static_cast<int>(P.flevel.size()) - 1;
+  const int nlev = static_cast<int>(flevel.size()) - 1;
   for (int l = 0; l < nlev; ++l) {
-    for (int32_t q = P.flevel[l]; q < P.flevel[l + 1]; ++q) {
-      const TileTask& t = P.ftask[q];
+    for (int32_t q = flevel[l]; q < flevel[l + 1]; ++q) {
+      const TileTask& t = ftask[q];
       touch.clear();
       auto add_pairs = [&](int32_t beg, int32_t end) {
         for (int32_t e = beg; e < end; ++e) {
@@ -298,21 +377,43 @@ void build_dataflow_deps(Plan& P) {
       touch.erase(std::unique(touch.begin(), touch.end()), touch.end());
       for (int32_t sl : touch)
         if (written[sl] > 0) {
-          P.fdep.push_back(sl);
-          P.fdep.push_back(written[sl]);
+          fdep.push_back(sl);
+          fdep.push_back(written[sl]);
         }
-      P.fdep_start.push_back(static_cast<int32_t>(P.fdep.size() / 2));
+      fdep_start.push_back(static_cast<int32_t>(fdep.size() / 2));
     }
-    for (int32_t q = P.flevel[l]; q < P.flevel[l + 1]; ++q) {
-      const TileTask& t = P.ftask[q];
+    for (int32_t q = flevel[l]; q < flevel[l + 1]; ++q) {
+      const TileTask& t = ftask[q];
       if (t.kind == 1 || t.i != t.k) written[t.dst]++;
+    }
+  }
+}
+
+// keep the tasks whose owner is `who`, in schedule order, with their levels
+// renumbered densely (empty levels dropped)
+void filter_tasks(const std::vector<TileTask>& all, const std::vector<int32_t>& lev,
+                  const std::vector<int32_t>& owner, int32_t who, std::vector<TileTask>& ftask,
+                  std::vector<int32_t>& flevel, std::vector<int32_t>& fpanels) {
+  ftask.clear();
+  flevel.assign(1, 0);
+  fpanels.clear();
+  for (size_t l = 0; l + 1 < lev.size(); ++l) {
+    int np = 0;
+    for (int32_t q = lev[l]; q < lev[l + 1]; ++q)
+      if (owner[q] == who) {
+        ftask.push_back(all[q]);
+        np += all[q].kind == 0;
+      }
+    if (static_cast<int32_t>(ftask.size()) != flevel.back()) {
+      flevel.push_back(static_cast<int32_t>(ftask.size()));
+      fpanels.push_back(np);
     }
   }
 }
 
 }  // namespace
 
-void build_tile_schedule(Plan& P) {
+bool build_tile_schedule(Plan& P) {
   const int NT = P.NT;
   std::vector<std::vector<int32_t>> adj(NT);
   std::vector<int32_t> maxnb(NT);
@@ -332,14 +433,16 @@ void build_tile_schedule(Plan& P) {
     std::sort(v.begin(), v.end());
     v.erase(std::unique(v.begin(), v.end()), v.end());
   }
+  const int nr = std::max(1, P.nranks);
   Sched best;
-  schedule(NT, adj, maxnb, g_leaf_override > 0 ? g_leaf_override : 0, best);
+  schedule(NT, adj, maxnb, g_leaf_override > 0 ? g_leaf_override : 0, best, nr);
+  if (!best.ok) return false;
   if (g_leaf_override < 0) {
     for (int leaf : {4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128, 192, 256}) {
-      if (leaf >= NT) break;
+      if (leaf * nr >= NT) break;
       Sched cand;
-      schedule(NT, adj, maxnb, leaf, cand);
-      if (cand.cost < best.cost) best = std::move(cand);
+      schedule(NT, adj, maxnb, leaf, cand, nr);
+      if (cand.ok && cand.cost < best.cost) best = std::move(cand);
     }
   }
   P.nd_leaf = best.leaf;
@@ -397,7 +500,60 @@ void build_tile_schedule(Plan& P) {
     }
     P.row_start[t + 1] = static_cast<int32_t>(P.row_col.size());
   }
-  build_dataflow_deps(P);
+  // ---- partitioned: this rank's phase-0 tasks (its subtree, and its
+  // interior columns' updates of separator tiles), then the separator tasks
+  // every rank runs after the exchange
+  P.tile_owner.assign(NT, 0);
+  for (int cp = 0; cp < NT; ++cp) P.tile_owner[best.order[cp]] = best.owner[cp];
+  P.sep_slot_ranges.clear();
+  P.sep_tile_ranges.clear();
+  P.ftask1.clear();
+  P.flevel1.assign(1, 0);
+  P.fpanels1.clear();
+  P.fdep_start1.assign(1, 0);
+  P.fdep1.clear();
+  if (nr > 1) {
+    const std::vector<TileTask> all = P.ftask;
+    const std::vector<int32_t> lev = P.flevel;
+    filter_tasks(all, lev, best.task_owner, P.rank, P.ftask, P.flevel, P.fpanels);
+    filter_tasks(all, lev, best.task_owner, -1, P.ftask1, P.flevel1, P.fpanels1);
+    build_dataflow_deps(P, P.ftask1, P.flevel1, P.fdep_start1, P.fdep1);
+    // backward: separator columns first (they are the top of the tree), then
+    // this rank's interior, in the global level order
+    std::vector<BackPart> keep;
+    std::vector<int32_t> klev(1, 0);
+    for (int pass = 0; pass < 2; ++pass) {
+      const int32_t who = pass == 0 ? -1 : P.rank;
+      for (size_t l = 0; l + 1 < P.bplevel.size(); ++l) {
+        for (int32_t q = P.bplevel[l]; q < P.bplevel[l + 1]; ++q)
+          if (P.tile_owner[P.bpart[q].k] == who) keep.push_back(P.bpart[q]);
+        if (static_cast<int32_t>(keep.size()) != klev.back()) klev.push_back(static_cast<int32_t>(keep.size()));
+      }
+    }
+    P.bpart = std::move(keep);
+    P.bplevel = std::move(klev);
+    // exchanged data: every stored tile of the separator columns (contiguous
+    // slots per column position), and the separator rows of the RHS
+    for (int cp = 0; cp < NT; ++cp) {
+      if (best.owner[cp] >= 0) continue;
+      const int32_t b = best.slot_base[cp], e = b + static_cast<int32_t>(best.st[cp].size());
+      if (!P.sep_slot_ranges.empty() && P.sep_slot_ranges.back() == b) P.sep_slot_ranges.back() = e;
+      else {
+        P.sep_slot_ranges.push_back(b);
+        P.sep_slot_ranges.push_back(e);
+      }
+    }
+    for (int t = 0; t < NT; ++t) {
+      if (P.tile_owner[t] >= 0) continue;
+      if (!P.sep_tile_ranges.empty() && P.sep_tile_ranges.back() == t) P.sep_tile_ranges.back() = t + 1;
+      else {
+        P.sep_tile_ranges.push_back(t);
+        P.sep_tile_ranges.push_back(t + 1);
+      }
+    }
+  }
+  build_dataflow_deps(P, P.ftask, P.flevel, P.fdep_start, P.fdep);
+  return true;
 }
 
 }  // namespace dynohip

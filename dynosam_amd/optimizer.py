@@ -193,3 +193,30 @@ def plan_schedule(graph, values):
     out = {k: getattr(info, k) for k, _ in _abi.ScheduleInfo._fields_}
     out.update(arrs)
     return out
+
+
+def plan_export(graph, values, name, nranks=1, rank=0):
+    """Host-only: one named int32 array of the (partitioned) plan of `rank`
+    (dynohip_plan_export). Structs come back flattened: ftask / ftask1 10
+    ints per task, bpart 8 ints per part."""
+    lib = _native.load("libdynohip.so")
+    gv = graph.view()
+    keys = np.ascontiguousarray(values.keys, dtype=np.uint64)
+    kinds = np.ascontiguousarray(values.kinds, dtype=np.uint8)
+    kp = keys.ctypes.data_as(C.POINTER(C.c_uint64))
+    kk = kinds.ctypes.data_as(C.POINTER(C.c_uint8))
+    n = C.c_size_t()
+    rc = lib.dynohip_plan_export(C.byref(gv), kp, kk, keys.shape[0], int(nranks), int(rank), name.encode(), None, 0,
+                                 C.byref(n))
+    _check(lib, None, rc)
+    out = np.zeros(n.value, dtype=np.int32)
+    rc = lib.dynohip_plan_export(C.byref(gv), kp, kk, keys.shape[0], int(nranks), int(rank), name.encode(),
+                                 out.ctypes.data_as(C.POINTER(C.c_int32)), n.value, C.byref(n))
+    _check(lib, None, rc)
+    if name in ("ftask", "ftask1"):
+        return out.reshape(-1, 10)
+    if name == "bpart":
+        return out.reshape(-1, 8)
+    if name == "pairs":
+        return out.reshape(-1, 2)
+    return out

@@ -256,6 +256,44 @@ int dynohip_plan_schedule(const dynohip_graph_view* g, const uint64_t* keys, con
                           int32_t* row_slot, int32_t* red_a, int32_t* red_b);
 
 /* ------------------------------------------------------------------ */
+/* Partitioned full-batch solve over several GPUs (SURVEY.md §8(e) 2,  */
+/* BASELINE configs[4]). One handle per rank, one rank per GPU.         */
+/* ------------------------------------------------------------------ */
+/* Sums `n` doubles over all ranks, in place, identically on every rank
+   (an all-reduce). on_device = 1: `buf` is device memory of the handle's
+   device and its producers have completed; the function must return only
+   once the result is in `buf`. on_device = 0: host memory. Returns 0 on
+   success. Typically torch.distributed.all_reduce over RCCL. */
+typedef int (*dynohip_allreduce_fn)(void* ctx, double* buf, size_t n, int on_device);
+
+/* Marks the handle as rank `rank` of `nranks` (a power of two >= 2; 1 =
+   ordinary single-GPU handle). Call before dynohip_set_values; every rank
+   then passes the same GLOBAL graph and values. The reduced pose system is
+   split along its nested dissection into nranks time-contiguous subtrees:
+   a rank linearises and Schur-eliminates only the factors and landmark
+   chains touching its subtree, then the ranks sum the separator system (one
+   all-reduce of its tiles and right-hand side per linear solve, plus one of
+   8 scalars per LM inner iteration) and every rank factors it. LM decisions
+   are identical on all ranks. All ranks must make the same calls in the
+   same order (set_values, optimize, iterate, graph_error are collective).
+   Replaces the single-process solve of RGBDBackendModule.cc:207-231. */
+int dynohip_set_partition(dynohip_solver* s, int nranks, int rank, dynohip_allreduce_fn allreduce, void* ctx);
+
+/* After set_values on a partitioned handle: per global value, the rank
+   whose dynohip_get_values output is authoritative for it (-1: every rank
+   holds it identically). get_values fills only the values this rank holds
+   and leaves the others untouched in `data_out`. `exchange_doubles` (may be
+   null) receives the size of the per-solve separator all-reduce. */
+int dynohip_value_owner(dynohip_solver* s, int32_t* owner_out, size_t n, int64_t* exchange_doubles);
+
+/* Host-only introspection: one named int32 array of rank `rank`'s plan
+   (nranks = 1: the ordinary plan), e.g. "ftask", "ftask1", "bpart",
+   "tile_owner", "sep_slot_ranges", "value_owner". *n_out = its length;
+   at most `cap` entries are copied to `out` (may be null). */
+int dynohip_plan_export(const dynohip_graph_view* g, const uint64_t* keys, const uint8_t* kind, size_t n,
+                        int nranks, int rank, const char* name, int32_t* out, size_t cap, size_t* n_out);
+
+/* ------------------------------------------------------------------ */
 /* Window / batch drivers (integer, bit-exact)                          */
 /* ------------------------------------------------------------------ */
 /* RGBDBackendModule::SlidingWindow (RGBDBackendModule.hpp:87-145) */

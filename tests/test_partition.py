@@ -1,0 +1,296 @@
+"""Partitioned full-batch solve, host side, no GPU.
+
+The plan of every rank (dynohip_plan_export with nranks > 1) is replayed in
+numpy with the semantics of the kernels it drives (k_tasks / k_back in
+csrc/tilechol.hip, k_sep_rhs in csrc/kernels.hip, the separator all-reduce
+of solver.cpp):
+  * each rank gets a share of a random SPD matrix and right-hand side whose
+    support lies in its interior tiles and the separators (separator-only
+    entries split at random between the ranks, as factors touching only
+    separators may sit on any rank);
+  * phase 0: the rank's own tasks, then its interior contributions leave
+    the separator RHS rows;
+  * the separator tiles and rows are summed over ranks (the all-reduce);
+  * phase 1 and the backward substitution on every rank;
+and the rows every rank owns (its interior and the separators) must match
+numpy.linalg.solve of the whole matrix. Also checks the factor ownership:
+every factor and landmark chain lands on exactly one rank, and the ranks'
+factor counts add up to the graph.
+"""
+import numpy as np
+import pytest
+
+from dynosam_amd import synth
+from dynosam_amd.optimizer import plan_export, plan_schedule
+
+T = 64
+NAMES = ("info", "tile_pos", "tile_owner", "row_start", "row_col", "row_slot", "pairs", "ftask", "flevel",
+         "ftask1", "flevel1", "bpart", "bplevel", "bent", "sep_slot_ranges", "sep_tile_ranges", "value_owner",
+         "damp_row")
+
+
+def export_all(graph, values, nranks, rank):
+    return {k: plan_export(graph, values, k, nranks, rank) for k in NAMES}
+
+
+def random_spd(n_pose, NT, red_a, red_b, rng):
+    n_red = 6 * n_pose
+    M = np.zeros((NT * T, NT * T))
+    for a, b in zip(red_a, red_b):
+        blk = rng.standard_normal((6, 6)) * 0.3
+        if a == b:
+            blk = blk @ blk.T
+        M[6 * a:6 * a + 6, 6 * b:6 * b + 6] = blk
+        if a != b:
+            M[6 * b:6 * b + 6, 6 * a:6 * a + 6] = blk.T
+    d = np.abs(M).sum(axis=1) + 1.0
+    M[np.arange(n_red), np.arange(n_red)] = d[:n_red]
+    M[np.arange(n_red, NT * T), np.arange(n_red, NT * T)] = 1.0
+    return M
+
+
+def split(M, rhs, owner, nranks, rng):
+    """Per-rank shares: entry (i, j) belongs to the rank owning tile(i) or
+    tile(j); separator-only entries are split at random (symmetrically)."""
+    NT = len(owner)
+    Ms = [np.zeros_like(M) for _ in range(nranks)]
+    rs = [np.zeros_like(rhs) for _ in range(nranks)]
+    for ti in range(NT):
+        for tj in range(NT):
+            blk = M[ti * T:(ti + 1) * T, tj * T:(tj + 1) * T]
+            if not blk.any():
+                continue
+            oi, oj = owner[ti], owner[tj]
+            assert not (oi >= 0 and oj >= 0 and oi != oj), f"tiles {ti},{tj} couple two interiors"
+            o = max(oi, oj)
+            if o >= 0:
+                Ms[o][ti * T:(ti + 1) * T, tj * T:(tj + 1) * T] = blk
+            elif tj <= ti:
+                w = rng.dirichlet(np.ones(nranks))
+                for r in range(nranks):
+                    Ms[r][ti * T:(ti + 1) * T, tj * T:(tj + 1) * T] = w[r] * blk
+                    if ti != tj:
+                        Ms[r][tj * T:(tj + 1) * T, ti * T:(ti + 1) * T] = w[r] * blk.T
+    for ti in range(NT):
+        seg = rhs[ti * T:(ti + 1) * T]
+        if owner[ti] >= 0:
+            rs[owner[ti]][ti * T:(ti + 1) * T] = seg
+        else:
+            w = rng.dirichlet(np.ones(nranks))
+            for r in range(nranks):
+                rs[r][ti * T:(ti + 1) * T] = w[r] * seg
+    return Ms, rs
+
+
+class RankState:
+    def __init__(self, plan, M, rhs):
+        self.p = plan
+        NT = len(plan["tile_pos"])
+        self.NT = NT
+        self.slots = np.zeros((plan["info"][2], T, T))
+        pos = plan["tile_pos"]
+        for ti in range(NT):
+            for tj in range(ti + 1):
+                blk = M[ti * T:(ti + 1) * T, tj * T:(tj + 1) * T]
+                if not blk.any():
+                    continue
+                if ti == tj:
+                    self.slots[self.slot_of(ti, ti)] += blk
+                elif pos[ti] >= pos[tj]:
+                    self.slots[self.slot_of(ti, tj)] += blk
+                else:
+                    self.slots[self.slot_of(tj, ti)] += blk.T
+        self.r = rhs.reshape(NT, T).copy()
+        self.contrib = np.zeros((len(self.slots), T))
+        self.y = np.full((NT, T), np.nan)
+        self.Linv = np.full((NT, T, T), np.nan)
+        self.x = np.full((NT, T), np.nan)
+
+    def slot_of(self, i, j):
+        p = self.p
+        lo, hi = p["row_start"][i], p["row_start"][i + 1]
+        cols = p["row_col"][lo:hi]
+        k = np.searchsorted(cols, j)
+        assert k < len(cols) and cols[k] == j, f"no slot for tile ({i}, {j})"
+        return int(p["row_slot"][lo + k])
+
+    def forward(self, ft, fl):
+        p, slots, pairs = self.p, self.slots, self.p["pairs"]
+        rs, rc, rsl = p["row_start"], p["row_col"], p["row_slot"]
+
+        def psum(beg, end):
+            return sum((slots[pairs[e][0]] @ slots[pairs[e][1]].T for e in range(beg, end)), np.zeros((T, T)))
+
+        def pslots(beg, end):
+            return {("s", int(v)) for e in range(beg, end) for v in pairs[e]}
+
+        for lv in range(len(fl) - 1):
+            reads, writes = [], []
+            for q in range(fl[lv], fl[lv + 1]):
+                kind, k, i, dst, diag, pdb, pde, pob, poe, _ = (int(v) for v in ft[q])
+                if kind == 1:
+                    reads.append(pslots(pob, poe) | {("s", dst)})
+                    writes.append({("s", dst)})
+                    continue
+                rd = {("s", diag)} | pslots(pdb, pde)
+                rd |= {("c", int(rsl[e])) for e in range(rs[k], rs[k + 1]) if rc[e] != k}
+                if i != k:
+                    rd |= {("s", dst)} | pslots(pob, poe)
+                    writes.append({("s", dst), ("c", dst)})
+                else:
+                    writes.append({("L", k), ("y", k)})
+                reads.append(rd)
+            for a in range(len(writes)):
+                for b in range(len(writes)):
+                    if a != b:
+                        bad = writes[a] & (reads[b] | writes[b])
+                        assert not bad, f"level {lv}: conflict {bad}"
+            for q in range(fl[lv], fl[lv + 1]):
+                kind, k, i, dst, diag, pdb, pde, pob, poe, _ = (int(v) for v in ft[q])
+                if kind == 1:
+                    slots[dst] -= psum(pob, poe)
+                    continue
+                A = slots[diag] - psum(pdb, pde)
+                Li = np.linalg.inv(np.linalg.cholesky(A))
+                rk = self.r[k] - sum((self.contrib[rsl[e]] for e in range(rs[k], rs[k + 1]) if rc[e] != k),
+                                     np.zeros(T))
+                yk = Li @ rk
+                if i == k:
+                    self.Linv[k] = Li
+                    self.y[k] = yk
+                else:
+                    L = (slots[dst] - psum(pob, poe)) @ Li.T
+                    slots[dst] = L
+                    self.contrib[dst] = L @ yk
+
+    def sep_rhs(self, rank):
+        p = self.p
+        owner = p["tile_owner"]
+        for b, e in p["sep_tile_ranges"].reshape(-1, 2):
+            for s in range(b, e):
+                for q in range(p["row_start"][s], p["row_start"][s + 1]):
+                    if owner[p["row_col"][q]] == rank:
+                        sl = p["row_slot"][q]
+                        self.r[s] -= self.contrib[sl]
+                        self.contrib[sl] = 0.0
+
+    def backward(self):
+        bp, bl, be = self.p["bpart"], self.p["bplevel"], self.p["bent"].reshape(-1, 2)
+        acc = {}
+        for q in range(bl[-1]):
+            k, beg, end, nparts, part, _pbase, _, _ = (int(v) for v in bp[q])
+            s = acc.setdefault(k, np.zeros(T))
+            for e in range(beg, end):
+                sl, row = int(be[e][0]), int(be[e][1])
+                assert np.isfinite(self.x[row]).all(), "backward reads an unsolved tile"
+                s -= self.slots[sl].T @ self.x[row]
+            if part == nparts - 1:
+                self.x[k] = self.Linv[k].T @ (self.y[k] + s)
+
+
+def replay_partitioned(name, nranks, seed=5, **kw):
+    graph, values, _ = synth.generate(name, **kw)
+    glob = plan_schedule(graph, values)
+    plans = [export_all(graph, values, nranks, r) for r in range(nranks)]
+    owner = plans[0]["tile_owner"]
+    for p in plans[1:]:
+        assert np.array_equal(p["tile_owner"], owner)
+        assert np.array_equal(p["ftask1"], plans[0]["ftask1"])
+    rng = np.random.default_rng(seed)
+    M = random_spd(glob["n_pose"], glob["n_tiles"], glob["red_a"], glob["red_b"], rng)
+    rhs = rng.standard_normal(M.shape[0])
+    Ms, rs = split(M, rhs, owner, nranks, rng)
+    states = [RankState(plans[r], Ms[r], rs[r]) for r in range(nranks)]
+    for r, st in enumerate(states):
+        st.forward(st.p["ftask"], st.p["flevel"])
+        st.sep_rhs(r)
+    # the all-reduce of the separator tiles and right-hand side rows
+    ssr, str_ = plans[0]["sep_slot_ranges"].reshape(-1, 2), plans[0]["sep_tile_ranges"].reshape(-1, 2)
+    for b, e in ssr:
+        tot = sum(st.slots[b:e] for st in states)
+        for st in states:
+            st.slots[b:e] = tot
+    for b, e in str_:
+        tot = sum(st.r[b:e] for st in states)
+        for st in states:
+            st.r[b:e] = tot
+    ref = np.linalg.solve(M, rhs).reshape(-1, T)
+    for r, st in enumerate(states):
+        st.forward(st.p["ftask1"], st.p["flevel1"])
+        st.backward()
+        mine = [t for t in range(st.NT) if owner[t] in (-1, r)]
+        assert np.allclose(st.x[mine], ref[mine], rtol=1e-9, atol=1e-10), f"rank {r}"
+    return plans, graph, values
+
+
+@pytest.mark.parametrize("name,nranks", [("C1", 2), ("C2", 2), ("C2", 4)])
+def test_partitioned_replay_solves(name, nranks):
+    replay_partitioned(name, nranks)
+
+
+def test_partitioned_replay_eight_ranks():
+    replay_partitioned("C2", 8, seed=11)
+
+
+def test_partition_ownership():
+    graph, values, _ = synth.generate("C2")
+    nranks = 4
+    infos = [plan_export(graph, values, "info", nranks, r) for r in range(nranks)]
+    total = sum(int(i[5]) for i in infos)
+    assert total == int(infos[0][6])
+    vo = plan_export(graph, values, "value_owner", nranks, 0)
+    kinds = np.asarray(values.kinds)
+    # every landmark has exactly one owning rank, poses are owned or replicated
+    assert (vo[kinds == 1] >= 0).all() and (vo[kinds == 1] < nranks).all()
+    assert (vo >= -1).all()
+    # ranks hold disjoint landmark sets that cover the graph
+    n_pts = [int(plan_export(graph, values, "info", nranks, r)[4]) for r in range(nranks)]
+    assert sum(n_pts) == int((kinds == 1).sum())
+    # damping: every reduced row damped by exactly one rank
+    damp = sum(plan_export(graph, values, "damp_row", nranks, r).astype(int) for r in range(nranks))
+    assert (damp == 1).all()
+
+
+def test_partition_too_short_fails():
+    graph, values, _ = synth.generate("C1")
+    with pytest.raises(RuntimeError):
+        plan_export(graph, values, "info", 8, 0)
+
+
+def _allreduce_worker(rank, world, port, out_path):
+    import ctypes as C
+    import os
+
+    import torch.distributed as dist
+
+    from dynosam_amd.partitioned import TorchAllReduce
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ar = TorchAllReduce("cpu")
+    buf = np.arange(8, dtype=np.float64) * (rank + 1)
+    rc = ar.fn(None, buf.ctypes.data_as(C.POINTER(C.c_double)), buf.shape[0], 0)
+    res = [None] * world
+    dist.all_gather_object(res, (rc, buf.tolist(), ar.calls, ar.doubles))
+    if rank == 0:
+        np.save(out_path, np.array([[r[0]] + r[1] + [r[2], r[3]] for r in res]))
+    dist.destroy_process_group()
+
+
+def test_allreduce_callback_gloo(tmp_path):
+    """The C-ABI all-reduce callback (dynohip_allreduce_fn) over gloo, world
+    size 2, host buffers: in place, identical on every rank."""
+    import os
+
+    import torch.multiprocessing as mp
+
+    out = str(tmp_path / "ar.npy")
+    port = 29700 + os.getpid() % 1000
+    mp.spawn(_allreduce_worker, args=(2, port, out), nprocs=2, join=True)
+    got = np.load(out)
+    want = np.arange(8) * 3.0
+    for row in got:
+        assert row[0] == 0
+        assert np.array_equal(row[1:9], want)
+        assert row[9] == 1 and row[10] == 8
