@@ -294,3 +294,29 @@ def test_allreduce_callback_gloo(tmp_path):
         assert row[0] == 0
         assert np.array_equal(row[1:9], want)
         assert row[9] == 1 and row[10] == 8
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_partitioned_lm_matches_single_gpu(tmp_path, nranks):
+    """The partitioned solve on `nranks` processes sharing the GPU (gloo
+    exchange) reproduces the single-handle solve of the same C2 graph: same
+    iteration count and accept sequence, values within the north-star 1e-6
+    relative Frobenius (tools/partition_check.py does the comparison)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "part.json"
+    port = 29800 + nranks + os.getpid() % 100
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(nranks),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "tools", "partition_check.py"),
+           "--config", "C2", "--backend", "gloo", "--out", str(out)]
+    r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    res = json.loads(out.read_text())
+    assert res["ok"] and res["ranks"] == nranks
+    assert res["iterations"][0] == res["iterations"][1]
+    assert res["values_rel_frobenius"] < 1e-6
