@@ -783,30 +783,41 @@ __device__ __forceinline__ void ldk(const double* __restrict__ src, double (&dst
   for (int k = 0; k < K; ++k) dst[k] = src[k];
 }
 
-// block Cholesky of each point chain C = tridiag(D_i + lambda I, E_i):
-//   M_i = E_{i-1} L_{i-1}^-T, L_i L_i^T = D_i + lambda I - M_i M_i^T;
-// then v = C^-1 gp. Thread per chain; the next point's D, g_p and E are
-// fetched while the current point is factored.
-// Blocks past the chains zero the solve's accumulation buffers (the tile
-// slots the reduced gather scatters into, the reduced gradient) in 16-byte
-// stores, in place of separate memsets.
-__global__ __launch_bounds__(kBlock) void k_chain_factor(ChainDev cd, double* __restrict__ arena, double lambda,
-                                                         int* fail, ZeroDev zb) {
-  const int nbc = (cd.n_comp + kBlock - 1) / kBlock;
-  if (static_cast<int>(blockIdx.x) >= nbc) {
-    const int64_t stride = static_cast<int64_t>(gridDim.x - nbc) * kBlock;
-    const int64_t i0 = static_cast<int64_t>(blockIdx.x - nbc) * kBlock + threadIdx.x;
-    const double2 zero = {0.0, 0.0};
+// ---- point chains C = tridiag(D_i + lambda I, E_i) (block Cholesky):
+//   M_i = E_{i-1} L_{i-1}^-T, L_i L_i^T = D_i + lambda I - M_i M_i^T,
+// forward z_i = L_i^-1 (b_i - M_i z_{i-1}), backward
+// x_i = L_i^-T (z_i - M_{i+1}^T x_{i+1}).
+// Singleton chains (static landmarks) run a thread per chain. Chains of
+// two or more points (dynamic tracklets) run a 16-lane group per chain:
+// lane j holds point s0 + j of the current 16-point segment in registers
+// and the recurrence moves lane to lane by shuffles, so a step costs its
+// arithmetic instead of a dependent memory round trip. Both forms do the
+// same operations in the same order (the compiler's FMA contraction may
+// still differ between them in the last bit).
+constexpr int kGrp = 16;
+
+template <int K>
+__device__ __forceinline__ void grp_bcast(const double (&src)[K], double (&dst)[K], int lane_src) {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      double2* p = reinterpret_cast<double2*>(zb.p[k]);
-      const int64_t n = zb.n[k] / 2;
-      for (int64_t i = i0; i < n; i += stride) p[i] = zero;
-    }
-    return;
-  }
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= cd.n_comp) return;
+  for (int k = 0; k < K; ++k) dst[k] = __shfl(src[k], lane_src, kGrp);
+}
+// t = M^T X (the subtrahend of sub_mtx, same association)
+template <int N>
+__device__ __forceinline__ void mtx(const double* M, const double* X, double* t) {
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < N; ++c) t[r * N + c] = M[r] * X[c] + M[3 + r] * X[N + c] + M[6 + r] * X[2 * N + c];
+}
+template <int K>
+__device__ __forceinline__ void sub_k(const double* t, double* B) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) B[k] -= t[k];
+}
+
+// one chain, one thread; the next point's D, g_p and E are fetched while
+// the current point is factored
+__device__ void chain_factor_thread(const ChainDev& cd, double* __restrict__ arena, double lambda, int* fail, int c) {
   const int i0 = cd.comp_start[c], i1 = cd.comp_start[c + 1];
   double Lp[9], z[3];
   double Dn[9], gn[3], En[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -870,11 +881,118 @@ __global__ __launch_bounds__(kBlock) void k_chain_factor(ChainDev cd, double* __
   }
 }
 
+// one chain of >= 2 points, one 16-lane group
+__device__ void chain_factor_group(const ChainDev& cd, double* __restrict__ arena, double lambda, int* fail, int c,
+                                   int lane) {
+  const int i0 = cd.comp_start[c], n = cd.comp_start[c + 1] - i0;
+  double Lp[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, zp[3] = {0, 0, 0};
+  double L[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, g[3] = {0, 0, 0}, M[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  int last = 0;
+  for (int s0 = 0; s0 < n; s0 += kGrp) {
+    const int i = s0 + lane;
+    double Dm[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, E[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (i < n) {
+      ldk(arena + cd.off_D + 9ll * (i0 + i), Dm);
+      ldk(arena + cd.off_gp + 3ll * (i0 + i), g);
+      if (i > 0) ldk(arena + cd.off_E + 9ll * (i0 + i - 1), E);
+    }
+    const int steps = min(kGrp, n - s0);
+    for (int k = 0; k < steps; ++k) {
+      if (lane == k) {
+        Dm[0] += lambda; Dm[4] += lambda; Dm[8] += lambda;
+        if (i > 0) {
+          double Mt[9];
+#pragma unroll
+          for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int q = 0; q < 3; ++q) Mt[3 * r + q] = E[3 * q + r];
+          lsolve<3>(Lp, Mt);
+#pragma unroll
+          for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int q = 0; q < 3; ++q) M[3 * r + q] = Mt[3 * q + r];
+          double* Mo = arena + cd.off_M + 9ll * (i0 + i);
+#pragma unroll
+          for (int q = 0; q < 9; ++q) Mo[q] = M[q];
+#pragma unroll
+          for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int q = 0; q < 3; ++q) Dm[3 * r + q] -= M[3 * r] * M[3 * q] + M[3 * r + 1] * M[3 * q + 1] + M[3 * r + 2] * M[3 * q + 2];
+          sub_mx<1>(M, zp, g);
+        }
+        if (!chol3(Dm, L)) {
+          *fail = 1;
+#pragma unroll
+          for (int q = 0; q < 9; ++q) L[q] = (q % 4 == 0) ? 1.0 : 0.0;
+        }
+        lsolve<1>(L, g);
+        double* Lo = arena + cd.off_L + 9ll * (i0 + i);
+#pragma unroll
+        for (int q = 0; q < 9; ++q) Lo[q] = L[q];
+        double* vo = arena + cd.off_v + 3ll * (i0 + i);
+        vo[0] = g[0]; vo[1] = g[1]; vo[2] = g[2];
+      }
+      grp_bcast(L, Lp, k);
+      grp_bcast(g, zp, k);
+    }
+    last = s0;
+  }
+  // backward: lane i+1 hands t = M_{i+1}^T v_{i+1} to lane i
+  double t[3] = {0, 0, 0};
+  for (int s0 = last; s0 >= 0; s0 -= kGrp) {
+    const int i = s0 + lane;
+    if (s0 != last && i < n) {  // the last segment is still in registers
+      ldk(arena + cd.off_L + 9ll * (i0 + i), L);
+      ldk(arena + cd.off_v + 3ll * (i0 + i), g);
+      if (i > 0) ldk(arena + cd.off_M + 9ll * (i0 + i), M);
+    }
+    const int steps = min(kGrp, n - s0);
+    for (int k = steps - 1; k >= 0; --k) {
+      double tn[3] = {0, 0, 0};
+      if (lane == k) {
+        double x[3] = {g[0], g[1], g[2]};
+        if (i < n - 1) sub_k<3>(t, x);
+        ltsolve<1>(L, x);
+        double* vo = arena + cd.off_v + 3ll * (i0 + i);
+        vo[0] = x[0]; vo[1] = x[1]; vo[2] = x[2];
+        if (i > 0) mtx<1>(M, x, tn);
+      }
+      grp_bcast(tn, t, k);
+    }
+  }
+}
+
+// Blocks: [0, nbg) 16-lane groups over the chains of >= 2 points,
+// [nbg, nbg + nbs) a thread per singleton chain, then blocks that zero the
+// solve's accumulation buffers (the tile slots the reduced gather scatters
+// into, the reduced gradient) in 16-byte stores, in place of memsets.
+__global__ __launch_bounds__(kBlock) void k_chain_factor(ChainDev cd, double* __restrict__ arena, double lambda,
+                                                         int* fail, ZeroDev zb, int nbg, int nbs) {
+  const int blk = blockIdx.x;
+  if (blk < nbg) {
+    const int c = (blk * kBlock + static_cast<int>(threadIdx.x)) / kGrp;
+    if (c < cd.n_long) chain_factor_group(cd, arena, lambda, fail, c, threadIdx.x % kGrp);
+    return;
+  }
+  if (blk < nbg + nbs) {
+    const int c = cd.n_long + (blk - nbg) * kBlock + static_cast<int>(threadIdx.x);
+    if (c < cd.n_comp) chain_factor_thread(cd, arena, lambda, fail, c);
+    return;
+  }
+  const int64_t stride = static_cast<int64_t>(gridDim.x - nbg - nbs) * kBlock;
+  const int64_t i0 = static_cast<int64_t>(blk - nbg - nbs) * kBlock + threadIdx.x;
+  const double2 zero = {0.0, 0.0};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    double2* p = reinterpret_cast<double2*>(zb.p[k]);
+    const int64_t n = zb.n[k] / 2;
+    for (int64_t i = i0; i < n; i += stride) p[i] = zero;
+  }
+}
+
 // Y = C^-1 W for one (chain, neighbour pose) pair: thread per pair, the
 // next point's L, M and W prefetched in the forward sweep.
-__global__ __launch_bounds__(kBlock) void k_chain_solve_y(ChainDev cd, double* __restrict__ arena) {
-  const int q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= cd.n_nb) return;
+__device__ void chain_solve_y_thread(const ChainDev& cd, double* __restrict__ arena, int q) {
   const int c = cd.nb_comp[q];
   const int nb0 = cd.comp_nb_start[c];
   const int m = cd.comp_nb_start[c + 1] - nb0;
@@ -883,11 +1001,36 @@ __global__ __launch_bounds__(kBlock) void k_chain_solve_y(ChainDev cd, double* _
   double* Y = arena + cd.comp_y_base[c];
   int ep = cd.nbedge_start[q];
   const int ep1 = cd.nbedge_start[q + 1];
+  // the pair's edge list (point, W offset) in registers when it is short,
+  // so fetching a point's W is one load, not an index load and then a W load
+  constexpr int kCache = 12;
+  int cpt[kCache];
+  uint32_t cw[kCache];
+  const bool cached = ep1 - ep <= kCache;
+  if (cached) {
+#pragma unroll
+    for (int k = 0; k < kCache; ++k) {
+      cpt[k] = ep + k < ep1 ? cd.nbedge_pt[ep + k] : -1;
+      cw[k] = ep + k < ep1 ? cd.nbedge_w[ep + k] : 0u;
+    }
+  }
+  int ci = 0;
   // rhs of point i: W of edge (i, b) if the point sees pose b, else 0
   auto load_rhs = [&](int i, double (&rhs)[18]) {
-    if (ep < ep1 && cd.nbedge_pt[ep] == i) {
-      ldk(arena + cd.nbedge_w[ep], rhs);
+    int pt = -1;
+    uint32_t w = 0;
+    if (cached) {
+#pragma unroll
+      for (int k = 0; k < kCache; ++k)
+        if (k == ci) { pt = cpt[k]; w = cw[k]; }
+    } else if (ep < ep1) {
+      pt = cd.nbedge_pt[ep];
+      w = cd.nbedge_w[ep];
+    }
+    if (pt == i) {
+      ldk(arena + w, rhs);
       ++ep;
+      ++ci;
     } else {
 #pragma unroll
       for (int k = 0; k < 18; ++k) rhs[k] = 0.0;
@@ -913,22 +1056,41 @@ __global__ __launch_bounds__(kBlock) void k_chain_solve_y(ChainDev cd, double* _
 #pragma unroll
     for (int k = 0; k < 18; ++k) { yo[k] = rhs[k]; Z[k] = rhs[k]; }
   }
-  // backward (Z holds Y_{n-1} after the forward sweep)
-  double Yn[18];
+  // backward (Z holds Y_{n-1} after the forward sweep); point i-1's Y, L
+  // and M_i are fetched before point i's result is stored, so the loads
+  // overlap the arithmetic instead of following the store
+  double Yn[18], Lb[9], Mb[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, Yb[18];
+  ldk(arena + cd.off_L + 9ll * (i0 + n - 1), Lb);
   for (int i = n - 1; i >= 0; --i) {
     double* yo = Y + 18ll * (static_cast<int64_t>(i) * m + b);
-    double x[18];
+    double x[18], L[9], M[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) { L[k] = Lb[k]; M[k] = Mb[k]; }
     if (i == n - 1) {
 #pragma unroll
       for (int k = 0; k < 18; ++k) x[k] = Z[k];
     } else {
-      ldk(yo, x);
-      sub_mtx<6>(arena + cd.off_M + 9ll * (i0 + i + 1), Yn, x);
+#pragma unroll
+      for (int k = 0; k < 18; ++k) x[k] = Yb[k];
     }
-    ltsolve<6>(arena + cd.off_L + 9ll * (i0 + i), x);
+    if (i > 0) {
+      ldk(Y + 18ll * (static_cast<int64_t>(i - 1) * m + b), Yb);
+      ldk(arena + cd.off_L + 9ll * (i0 + i - 1), Lb);
+      ldk(arena + cd.off_M + 9ll * (i0 + i), Mb);
+    }
+    if (i < n - 1) sub_mtx<6>(M, Yn, x);
+    ltsolve<6>(L, x);
 #pragma unroll
     for (int k = 0; k < 18; ++k) { yo[k] = x[k]; Yn[k] = x[k]; }
   }
+}
+
+// thread per (chain, neighbour pose) pair: with 18 right-hand-side columns
+// a step has enough arithmetic to cover the prefetched loads, and a 16-lane
+// group per pair would leave 15 lanes idle per step
+__global__ __launch_bounds__(kBlock) void k_chain_solve_y(ChainDev cd, double* __restrict__ arena) {
+  const int q = blockIdx.x * kBlock + static_cast<int>(threadIdx.x);
+  if (q < cd.n_nb) chain_solve_y_thread(cd, arena, q);
 }
 
 // t_e = W_e dX_pose(e) for every point-pose edge (edge-parallel)
@@ -949,10 +1111,8 @@ __global__ __launch_bounds__(kBlock) void k_wdx(ChainDev cd, int n_edge, const d
 }
 
 // dp = C^-1 (gp - W dX), the W dX products from k_wdx
-__global__ __launch_bounds__(kBlock) void k_backsub(ChainDev cd, const double* __restrict__ arena,
-                                                    const double* __restrict__ t, double* __restrict__ dpt) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= cd.n_comp) return;
+__device__ void backsub_thread(const ChainDev& cd, const double* __restrict__ arena, const double* __restrict__ t,
+                               double* __restrict__ dpt, int c) {
   const int i0 = cd.comp_start[c], i1 = cd.comp_start[c + 1];
   double z[3];
   for (int i = i0; i < i1; ++i) {
@@ -974,6 +1134,70 @@ __global__ __launch_bounds__(kBlock) void k_backsub(ChainDev cd, const double* _
     dpt[3ll * i] = x[0]; dpt[3ll * i + 1] = x[1]; dpt[3ll * i + 2] = x[2];
     xn[0] = x[0]; xn[1] = x[1]; xn[2] = x[2];
   }
+}
+
+__device__ void backsub_group(const ChainDev& cd, const double* __restrict__ arena, const double* __restrict__ t,
+                              double* __restrict__ dpt, int c, int lane) {
+  const int i0 = cd.comp_start[c], n = cd.comp_start[c + 1] - i0;
+  double zp[3] = {0, 0, 0}, g[3] = {0, 0, 0};
+  double L[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, M[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  int last = 0;
+  for (int s0 = 0; s0 < n; s0 += kGrp) {
+    const int i = s0 + lane;
+    if (i < n) {
+      ldk(arena + cd.off_gp + 3ll * (i0 + i), g);
+      for (int e = cd.pt_edge_start[i0 + i]; e < cd.pt_edge_start[i0 + i + 1]; ++e) {
+        g[0] -= t[3ll * e]; g[1] -= t[3ll * e + 1]; g[2] -= t[3ll * e + 2];
+      }
+      ldk(arena + cd.off_L + 9ll * (i0 + i), L);
+      if (i > 0) ldk(arena + cd.off_M + 9ll * (i0 + i), M);
+    }
+    const int steps = min(kGrp, n - s0);
+    for (int k = 0; k < steps; ++k) {
+      if (lane == k) {
+        if (i > 0) sub_mx<1>(M, zp, g);
+        lsolve<1>(L, g);
+        double* d = dpt + 3ll * (i0 + i);
+        d[0] = g[0]; d[1] = g[1]; d[2] = g[2];
+      }
+      grp_bcast(g, zp, k);
+    }
+    last = s0;
+  }
+  double tt[3] = {0, 0, 0};
+  for (int s0 = last; s0 >= 0; s0 -= kGrp) {
+    const int i = s0 + lane;
+    if (s0 != last && i < n) {
+      ldk(dpt + 3ll * (i0 + i), g);
+      ldk(arena + cd.off_L + 9ll * (i0 + i), L);
+      if (i > 0) ldk(arena + cd.off_M + 9ll * (i0 + i), M);
+    }
+    const int steps = min(kGrp, n - s0);
+    for (int k = steps - 1; k >= 0; --k) {
+      double tn[3] = {0, 0, 0};
+      if (lane == k) {
+        double x[3] = {g[0], g[1], g[2]};
+        if (i < n - 1) sub_k<3>(tt, x);
+        ltsolve<1>(L, x);
+        double* d = dpt + 3ll * (i0 + i);
+        d[0] = x[0]; d[1] = x[1]; d[2] = x[2];
+        if (i > 0) mtx<1>(M, x, tn);
+      }
+      grp_bcast(tn, tt, k);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_backsub(ChainDev cd, const double* __restrict__ arena,
+                                                    const double* __restrict__ t, double* __restrict__ dpt, int nbg) {
+  const int blk = blockIdx.x;
+  if (blk < nbg) {
+    const int c = (blk * kBlock + static_cast<int>(threadIdx.x)) / kGrp;
+    if (c < cd.n_long) backsub_group(cd, arena, t, dpt, c, threadIdx.x % kGrp);
+    return;
+  }
+  const int c = cd.n_long + (blk - nbg) * kBlock + static_cast<int>(threadIdx.x);
+  if (c < cd.n_comp) backsub_thread(cd, arena, t, dpt, c);
 }
 
 // ---------------------------------------------------------------- retract
@@ -1164,9 +1388,11 @@ void launch_chain_factor(const ChainDev& c, double* arena, double lambda, int* f
                          hipStream_t s) {
   const int64_t nz = std::max(z.n[0], std::max(z.n[1], z.n[2])) / 2;
   const int nbz = nz == 0 ? 0 : static_cast<int>(std::min<int64_t>(1024, nblocks(nz)));
-  const int nb = nblocks(c.n_comp) + nbz;
+  const int nbg = nblocks(static_cast<int64_t>(c.n_long) * kGrp);
+  const int nbs = nblocks(c.n_comp - c.n_long);
+  const int nb = nbg + nbs + nbz;
   if (nb == 0) return;
-  k_chain_factor<<<nb, kBlock, 0, s>>>(c, arena, lambda, fail, z);
+  k_chain_factor<<<nb, kBlock, 0, s>>>(c, arena, lambda, fail, z, nbg, nbs);
 }
 void launch_chain_solve_y(const ChainDev& c, double* arena, hipStream_t s) {
   if (c.n_nb == 0) return;
@@ -1176,7 +1402,8 @@ void launch_backsub(const ChainDev& c, int n_edge, const double* arena, const do
                     hipStream_t s) {
   if (c.n_comp == 0) return;
   if (n_edge > 0) k_wdx<<<nblocks(n_edge), kBlock, 0, s>>>(c, n_edge, arena, dpose, wdx);
-  k_backsub<<<nblocks(c.n_comp), kBlock, 0, s>>>(c, arena, wdx, dpt);
+  const int nbg = nblocks(static_cast<int64_t>(c.n_long) * kGrp);
+  k_backsub<<<nbg + nblocks(c.n_comp - c.n_long), kBlock, 0, s>>>(c, arena, wdx, dpt, nbg);
 }
 
 void launch_retract(int n_pose, int n_pt, const double* pose, const double* pt, const double* dpose,

@@ -52,6 +52,8 @@ struct ZeroDev {
 struct ChainDev {
   int n_comp = 0;
   int n_nb = 0;
+  int n_long = 0;      // chains of >= 2 points: comps [0, n_long) (longest first)
+  int n_nb_long = 0;   // their (chain, neighbour pose) pairs: [0, n_nb_long)
   const int32_t* comp_start = nullptr;
   const int32_t* comp_nb_start = nullptr;
   const int32_t* nb_comp = nullptr;

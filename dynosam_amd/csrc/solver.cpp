@@ -259,6 +259,9 @@ int upload_plan(dynohip_solver* s) {
   ChainDev& c = s->cd;
   c.n_comp = P.n_comp;
   c.n_nb = static_cast<int>(P.nb_pose.size());
+  c.n_long = 0;
+  while (c.n_long < P.n_comp && P.comp_start[c.n_long + 1] - P.comp_start[c.n_long] >= 2) ++c.n_long;
+  c.n_nb_long = P.comp_nb_start.empty() ? 0 : P.comp_nb_start[c.n_long];
   c.comp_start = s->comp_start.p;
   c.comp_nb_start = s->comp_nb_start.p;
   c.nb_comp = s->nb_comp.p;
