@@ -170,3 +170,80 @@ def trace_to_dicts(entries):
 class ScheduleInfo(C.Structure):
     _fields_ = [(n, C.c_int64) for n in ("n_pose", "n_tiles", "n_slots", "n_ftask", "n_pairs", "n_flevel", "n_btask",
                                           "n_blevel", "n_bent", "n_red_blocks", "nd_leaf")]
+
+
+# ---- include/dynobackend.h -------------------------------------------------
+class Measurement(C.Structure):
+    """dynob_measurement: one tracked landmark measurement (camera frame)."""
+    _fields_ = [
+        ("tracklet_id", C.c_int64),
+        ("object_id", C.c_int32),
+        ("reserved", C.c_int32),
+        ("frame_id", C.c_uint64),
+        ("landmark", C.c_double * 3),
+    ]
+
+
+MEASUREMENT_DTYPE = None  # numpy structured dtype with the same layout (set lazily by backend.py)
+
+
+class BackendParams(C.Structure):
+    _fields_ = [
+        ("formulation", C.c_int),
+        ("min_static_observations", C.c_int),
+        ("min_dynamic_observations", C.c_int),
+        ("use_smoothing_factor", C.c_int),
+        ("init_H_with_identity", C.c_int),
+        ("use_robust_kernels", C.c_int),
+        ("k_huber_3d_points", C.c_double),
+        ("static_point_sigma", C.c_double),
+        ("dynamic_point_sigma", C.c_double),
+        ("motion_ternary_sigma", C.c_double),
+        ("odometry_sigmas", C.c_double * 6),
+        ("smoothing_sigmas", C.c_double * 6),
+        ("initial_pose_prior_sigma", C.c_double),
+    ]
+
+
+class InputPacket(C.Structure):
+    _fields_ = [
+        ("frame_id", C.c_uint64),
+        ("timestamp", C.c_double),
+        ("T_world_camera", C.c_double * 12),
+        ("static_measurements", C.c_void_p),
+        ("n_static", C.c_size_t),
+        ("dynamic_measurements", C.c_void_p),
+        ("n_dynamic", C.c_size_t),
+        ("motion_object_ids", C.POINTER(C.c_int32)),
+        ("motions12", C.POINTER(C.c_double)),
+        ("n_motions", C.c_size_t),
+    ]
+
+
+class ModuleParams(C.Structure):
+    _fields_ = [
+        ("use_full_batch_opt", C.c_int),
+        ("full_batch_frame", C.c_int64),
+        ("opt_window_size", C.c_int),
+        ("opt_window_overlap", C.c_int),
+        ("optimize", C.c_int),
+        ("device_id", C.c_int),
+        ("post_update", C.c_int),
+        ("reserved", C.c_int),
+        ("lm", LMParams),
+    ]
+
+
+class SpinResult(C.Structure):
+    _fields_ = [
+        ("optimized", C.c_int),
+        ("iterations", C.c_int),
+        ("inner_iterations", C.c_int),
+        ("reserved", C.c_int),
+        ("window_start", C.c_uint64),
+        ("window_end", C.c_uint64),
+        ("error_before", C.c_double),
+        ("error_after", C.c_double),
+        ("ms_construct", C.c_double),
+        ("ms_optimize", C.c_double),
+    ]

@@ -115,6 +115,49 @@ def _declare(name, lib):
         lib.dynohip_value_owner.restype = C.c_int
         lib.dynohip_full_batch_trigger.argtypes = [C.c_int64, C.c_uint64]
         lib.dynohip_full_batch_trigger.restype = C.c_int
+        vp_ = C.c_void_p
+        U64, I64, I32_, D, U8 = P(C.c_uint64), P(C.c_int64), P(C.c_int32), P(C.c_double), P(C.c_uint8)
+        SZ = P(C.c_size_t)
+        for fn, args, res in [
+            ("dynob_map_create", [P(vp_)], C.c_int),
+            ("dynob_map_destroy", [vp_], None),
+            ("dynob_map_last_error", [vp_], C.c_char_p),
+            ("dynob_map_update_observations", [vp_, vp_, C.c_size_t], C.c_int),
+            ("dynob_map_update_sensor_pose", [vp_, C.c_uint64, D], C.c_int),
+            ("dynob_map_update_object_motions", [vp_, C.c_uint64, I32_, D, C.c_size_t], C.c_int),
+            ("dynob_map_query", [vp_, C.c_int, C.c_int64, C.c_int64, I64, C.c_size_t, SZ], C.c_int64),
+            ("dynob_params_default", [P(_abi.BackendParams), C.c_int], None),
+            ("dynob_formulation_create", [vp_, P(_abi.BackendParams), P(vp_)], C.c_int),
+            ("dynob_formulation_destroy", [vp_], None),
+            ("dynob_formulation_last_error", [vp_], C.c_char_p),
+            ("dynob_set_initial_pose", [vp_, C.c_uint64, D], C.c_int),
+            ("dynob_set_initial_pose_prior", [vp_, C.c_uint64, D], C.c_int),
+            ("dynob_add_odometry", [vp_, C.c_uint64, D], C.c_int),
+            ("dynob_update_static_observations", [vp_, C.c_uint64, C.c_int], C.c_int),
+            ("dynob_update_dynamic_observations", [vp_, C.c_uint64, C.c_int], C.c_int),
+            ("dynob_update_theta", [vp_, U64, U8, D, C.c_size_t], C.c_int),
+            ("dynob_formulation_graph", [vp_, P(_abi.GraphView)], C.c_int),
+            ("dynob_formulation_values", [vp_, P(U64), P(U8), P(D), SZ, SZ], C.c_int),
+            ("dynob_formulation_factor_types", [vp_, U8, C.c_size_t, SZ], C.c_int),
+            ("dynob_get_sensor_pose", [vp_, C.c_uint64, D], C.c_int),
+            ("dynob_get_object_motions", [vp_, C.c_uint64, I32_, D, C.c_size_t, SZ], C.c_int),
+            ("dynob_get_dynamic_landmarks", [vp_, C.c_uint64, I64, I32_, D, C.c_size_t, SZ], C.c_int),
+            ("dynob_get_static_landmarks", [vp_, C.c_uint64, I64, D, C.c_size_t, SZ], C.c_int),
+            ("dynob_object_centroid", [vp_, C.c_uint64, C.c_int32, D], C.c_int),
+            ("dynob_post_update", [vp_], C.c_int),
+            ("dynob_get_object_poses", [vp_, I32_, U64, D, C.c_size_t, SZ], C.c_int),
+            ("dynob_module_params_default", [P(_abi.ModuleParams)], None),
+            ("dynob_module_create", [P(_abi.BackendParams), P(_abi.ModuleParams), P(vp_)], C.c_int),
+            ("dynob_module_destroy", [vp_], None),
+            ("dynob_module_last_error", [vp_], C.c_char_p),
+            ("dynob_module_spin", [vp_, P(_abi.InputPacket), P(_abi.SpinResult)], C.c_int),
+            ("dynob_module_map", [vp_], vp_),
+            ("dynob_module_formulation", [vp_], vp_),
+            ("dynob_module_last_problem", [vp_, P(_abi.GraphView), P(U64), P(U8), P(D), P(D), SZ, SZ], C.c_int),
+        ]:
+            f = getattr(lib, fn)
+            f.argtypes = args
+            f.restype = res
         for fn, args, res in [
             ("dynohip_symbol", [C.c_ubyte, C.c_uint64], C.c_uint64),
             ("dynohip_labeled_symbol", [C.c_ubyte, C.c_ubyte, C.c_uint64], C.c_uint64),

@@ -1,0 +1,1437 @@
+// backend.cpp — host-side mirror of the reference backend module around the
+// LM call sites (include/dynobackend.h): Map, the WorldMotion / WorldPose
+// formulations, the accessor queries and RGBDBackendModule's spin. The LM
+// solves go through the HIP path (dynohip_*).
+//
+// Integer bookkeeping (which factors, which keys, which values and in which
+// order) follows the reference line by line; every function names the
+// reference lines it restates. Node sets are ordered by id exactly like
+// FastMapNodeSet (MapNodes.hpp:44-52), theta_ is ordered by key like
+// gtsam::Values, factors_ keeps insertion order like NonlinearFactorGraph.
+#include <array>
+#include <chrono>
+#include <iterator>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/dynobackend.h"
+#include "se3.hpp"
+
+namespace dynob {
+
+using dynohip::P3;
+
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+#define DB_CHECK(cond, code, msg)                                                   \
+  do {                                                                              \
+    if (!(cond)) throw Error((code), std::string(msg) + " [" #cond "]");            \
+  } while (0)
+
+constexpr unsigned char kBackgroundLabel = 0;
+
+P3 pose_from(const double* d) {
+  P3 T;
+  std::memcpy(T.R, d, 9 * sizeof(double));
+  std::memcpy(T.t, d + 9, 3 * sizeof(double));
+  return T;
+}
+void pose_to(const P3& T, double* d) {
+  std::memcpy(d, T.R, 9 * sizeof(double));
+  std::memcpy(d + 9, T.t, 3 * sizeof(double));
+}
+P3 pose_identity() {
+  P3 T;
+  std::memset(&T, 0, sizeof(T));
+  T.R[0] = T.R[4] = T.R[8] = 1.0;
+  return T;
+}
+// gtsam::Pose3 * Point3 (transformFrom: R p + t)
+void transform_from(const P3& T, const double* p, double* o) { dynohip::transform_from(T, p, o); }
+
+// gtsam keys (BackendDefinitions.hpp:57-88; keys.cpp)
+uint64_t camera_pose_key(uint64_t frame) { return dynohip_camera_pose_key(frame); }
+uint64_t static_key(int64_t trk) { return dynohip_static_landmark_key(trk); }
+uint64_t dynamic_key(uint64_t frame, int64_t trk) {
+  uint64_t k = 0;
+  DB_CHECK(dynohip_dynamic_landmark_key(frame, trk, &k) == DYNOHIP_OK, DYNOHIP_EINVAL, "invalid tracklet id");
+  return k;
+}
+uint64_t motion_key(int obj, uint64_t frame) { return dynohip_object_motion_key(obj, frame); }
+uint64_t object_pose_key(int obj, uint64_t frame) { return dynohip_object_pose_key(obj, frame); }
+
+// ---------------------------------------------------------------------------
+// Map (Map.hpp:112-444, MapNodes-inl.hpp:37-262)
+// ---------------------------------------------------------------------------
+struct LandmarkNode {
+  int64_t tracklet_id = 0;
+  int32_t object_id = 0;
+  // frames_seen_ and measurements_ (one entry per seen frame), ordered by
+  // frame id (FrameNodePtrSet / FastMap<FrameNodePtr>)
+  std::map<uint64_t, std::array<double, 3>> measurements;
+  bool is_static() const { return object_id == kBackgroundLabel; }
+  size_t num_observations() const { return measurements.size(); }
+  bool seen_at(uint64_t f) const { return measurements.count(f) != 0; }
+  const double* measurement(uint64_t f) const {
+    auto it = measurements.find(f);
+    DB_CHECK(it != measurements.end(), DYNOHIP_ESTATE,
+             "Missing measurement in landmark node with id " + std::to_string(tracklet_id) + " at frame " +
+                 std::to_string(f));
+    return it->second.data();
+  }
+};
+
+struct FrameNode {
+  uint64_t frame_id = 0;
+  std::set<int64_t> dynamic_landmarks, static_landmarks;  // by tracklet id
+  std::set<int32_t> objects_seen;
+  bool has_X = false;
+  P3 X_world;
+  bool has_motions = false;
+  std::map<int32_t, P3> motions_world;
+  bool object_observed(int32_t obj) const { return objects_seen.count(obj) != 0; }
+};
+
+struct ObjectNode {
+  int32_t object_id = 0;
+  std::set<int64_t> dynamic_landmarks;
+};
+
+struct Map {
+  std::map<uint64_t, FrameNode> frames;
+  std::map<int64_t, LandmarkNode> landmarks;
+  std::map<int32_t, ObjectNode> objects;
+
+  const FrameNode* frame(uint64_t f) const {
+    auto it = frames.find(f);
+    return it == frames.end() ? nullptr : &it->second;
+  }
+  FrameNode* frame(uint64_t f) {
+    auto it = frames.find(f);
+    return it == frames.end() ? nullptr : &it->second;
+  }
+  const LandmarkNode* landmark(int64_t t) const {
+    auto it = landmarks.find(t);
+    return it == landmarks.end() ? nullptr : &it->second;
+  }
+  const ObjectNode* object(int32_t o) const {
+    auto it = objects.find(o);
+    return it == objects.end() ? nullptr : &it->second;
+  }
+  uint64_t first_frame_id() const {
+    DB_CHECK(!frames.empty(), DYNOHIP_ESTATE, "map has no frames");
+    return frames.begin()->first;
+  }
+  uint64_t last_frame_id() const {
+    DB_CHECK(!frames.empty(), DYNOHIP_ESTATE, "map has no frames");
+    return frames.rbegin()->first;
+  }
+
+  // Map::addOrUpdateMapStructures (Map.hpp:376-444)
+  void add(const dynob_measurement& m) {
+    const bool is_static = m.object_id == kBackgroundLabel;
+    auto lit = landmarks.find(m.tracklet_id);
+    if (lit == landmarks.end()) {
+      LandmarkNode n;
+      n.tracklet_id = m.tracklet_id;
+      n.object_id = m.object_id;
+      lit = landmarks.emplace(m.tracklet_id, n).first;
+    }
+    FrameNode& fn = frames[m.frame_id];
+    fn.frame_id = m.frame_id;
+    LandmarkNode& ln = lit->second;
+    // "this might fail of a tracklet get associated with a different object"
+    DB_CHECK(ln.object_id == m.object_id, DYNOHIP_EINVAL,
+             "tracklet " + std::to_string(m.tracklet_id) + " changed object label");
+    // LandmarkNode::add (MapNodes-inl.hpp:163-176)
+    DB_CHECK(!ln.seen_at(m.frame_id), DYNOHIP_EINVAL,
+             "Unable to add new measurement to landmark node " + std::to_string(m.tracklet_id) + " at frame " +
+                 std::to_string(m.frame_id) + " as a measurement already exists at this frame!");
+    ln.measurements[m.frame_id] = {m.landmark[0], m.landmark[1], m.landmark[2]};
+    if (is_static) {
+      fn.static_landmarks.insert(m.tracklet_id);
+    } else {
+      ObjectNode& on = objects[m.object_id];
+      on.object_id = m.object_id;
+      on.dynamic_landmarks.insert(m.tracklet_id);
+      fn.dynamic_landmarks.insert(m.tracklet_id);
+      fn.objects_seen.insert(m.object_id);
+    }
+  }
+
+  // FrameNode::objectObservedInPrevious / objectMotionExpected
+  // (MapNodes-inl.hpp:47-88)
+  bool object_observed_in_previous(uint64_t f, int32_t obj) const {
+    const FrameNode* p = frame(f - 1u);
+    return p && p->object_observed(obj);
+  }
+  bool object_motion_expected(uint64_t f, int32_t obj) const {
+    const FrameNode* fn = frame(f);
+    return fn && fn->object_observed(obj) && object_observed_in_previous(f, obj);
+  }
+  // ObjectNode::getSeenFrames (MapNodes-inl.hpp:237-245)
+  std::set<uint64_t> object_seen_frames(int32_t obj) const {
+    std::set<uint64_t> out;
+    const ObjectNode* on = object(obj);
+    if (!on) return out;
+    for (int64_t t : on->dynamic_landmarks)
+      for (const auto& kv : landmarks.at(t).measurements) out.insert(kv.first);
+    return out;
+  }
+  // ObjectNode::getLandmarksSeenAtFrame (MapNodes-inl.hpp:252-262)
+  std::vector<int64_t> object_landmarks_at(int32_t obj, uint64_t f) const {
+    std::vector<int64_t> out;
+    const ObjectNode* on = object(obj);
+    if (!on) return out;
+    for (int64_t t : on->dynamic_landmarks)
+      if (landmarks.at(t).seen_at(f)) out.push_back(t);
+    return out;
+  }
+  bool initial_sensor_pose(uint64_t f, P3* X) const {
+    const FrameNode* fn = frame(f);
+    if (!fn || !fn->has_X) return false;
+    if (X) *X = fn->X_world;
+    return true;
+  }
+  // Map::hasInitialObjectMotion (Map.hpp:204-224)
+  bool initial_object_motion(uint64_t f, int32_t obj, P3* H) const {
+    const FrameNode* fn = frame(f);
+    if (!fn || !fn->has_motions) return false;
+    auto it = fn->motions_world.find(obj);
+    if (it == fn->motions_world.end()) return false;
+    if (H) *H = it->second;
+    return true;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Values / factors
+// ---------------------------------------------------------------------------
+struct Value {
+  uint8_t kind;
+  double d[12];
+};
+using Values = std::map<uint64_t, Value>;  // gtsam::Values (ordered by key)
+
+Value pose_value(const P3& T) {
+  Value v;
+  v.kind = DYNOHIP_POSE3;
+  pose_to(T, v.d);
+  return v;
+}
+Value point_value(const double* p) {
+  Value v;
+  std::memset(&v, 0, sizeof(v));
+  v.kind = DYNOHIP_POINT3;
+  v.d[0] = p[0];
+  v.d[1] = p[1];
+  v.d[2] = p[2];
+  return v;
+}
+// gtsam::Values::insert (throws ValuesKeyAlreadyExists)
+void values_insert(Values& vals, uint64_t key, const Value& v) {
+  DB_CHECK(vals.emplace(key, v).second, DYNOHIP_ESTATE, "gtsam::ValuesKeyAlreadyExists");
+}
+void values_insert(Values& vals, const Values& other) {
+  for (const auto& kv : other) values_insert(vals, kv.first, kv.second);
+}
+void values_insert_or_assign(Values& vals, const Values& other) {
+  for (const auto& kv : other) vals[kv.first] = kv.second;
+}
+
+enum FactorType { kPoseToPoint = 0, kTernary = 1, kBetween = 2, kPrior = 3, kMotionPose = 4, kPoseSmoothing = 5 };
+constexpr int kNKeys[6] = {2, 3, 2, 1, 4, 3};
+constexpr int kDim[6] = {3, 3, 6, 6, 3, 6};
+constexpr int kMeas[6] = {3, 0, 12, 12, 0, 0};
+
+struct Noise {
+  double sigmas[6];
+  double huber;  // 0 = Gaussian
+};
+
+struct Factor {
+  uint8_t type;
+  uint64_t keys[4];
+  double meas[12];
+  Noise noise;
+};
+
+struct Graph {
+  std::vector<Factor> factors;
+  void add(uint8_t type, std::initializer_list<uint64_t> keys, const double* meas, const Noise& n) {
+    Factor f;
+    std::memset(&f, 0, sizeof(f));
+    f.type = type;
+    int i = 0;
+    for (uint64_t k : keys) f.keys[i++] = k;
+    if (kMeas[type]) std::memcpy(f.meas, meas, kMeas[type] * sizeof(double));
+    f.noise = n;
+    factors.push_back(f);
+  }
+  void append(const Graph& o) { factors.insert(factors.end(), o.factors.begin(), o.factors.end()); }
+};
+
+// SoA export of a factor list (dynohip_graph_view)
+struct GraphExport {
+  std::vector<uint64_t> keys[6];
+  std::vector<double> meas[6], sig[6], hub[6];
+  void build(const Graph& g) {
+    for (int t = 0; t < 6; ++t) {
+      keys[t].clear();
+      meas[t].clear();
+      sig[t].clear();
+      hub[t].clear();
+    }
+    for (const Factor& f : g.factors) {
+      const int t = f.type;
+      keys[t].insert(keys[t].end(), f.keys, f.keys + kNKeys[t]);
+      meas[t].insert(meas[t].end(), f.meas, f.meas + kMeas[t]);
+      sig[t].insert(sig[t].end(), f.noise.sigmas, f.noise.sigmas + kDim[t]);
+      hub[t].push_back(f.noise.huber);
+    }
+  }
+  void view(dynohip_graph_view* g) const {
+    dynohip_factor_block* dst[6] = {&g->pose_to_point, &g->landmark_motion_ternary, &g->between,
+                                    &g->prior, &g->landmark_motion_pose, &g->landmark_pose_smoothing};
+    for (int t = 0; t < 6; ++t) {
+      dst[t]->n = hub[t].size();
+      dst[t]->keys = keys[t].empty() ? nullptr : keys[t].data();
+      dst[t]->measured = meas[t].empty() ? nullptr : meas[t].data();
+      dst[t]->sigmas = sig[t].empty() ? nullptr : sig[t].data();
+      dst[t]->huber_k = hub[t].empty() ? nullptr : hub[t].data();
+    }
+  }
+};
+
+struct ValuesExport {
+  std::vector<uint64_t> keys;
+  std::vector<uint8_t> kinds;
+  std::vector<double> data;
+  void build(const Values& v) {
+    keys.clear();
+    kinds.clear();
+    data.clear();
+    for (const auto& kv : v) {
+      keys.push_back(kv.first);
+      kinds.push_back(kv.second.kind);
+      data.insert(data.end(), kv.second.d, kv.second.d + (kv.second.kind == DYNOHIP_POSE3 ? 12 : 3));
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Formulation (Formulation-impl.hpp) with the WorldMotion / WorldPose
+// callbacks
+// ---------------------------------------------------------------------------
+struct NoiseModels {
+  Noise static_point, dynamic_point, landmark_motion, odometry, initial_pose_prior, object_smoothing;
+};
+
+// UpdateObservationResult (Formulation.hpp:44-64)
+struct UpdateResult {
+  std::map<int32_t, std::set<uint64_t>> objects_affected_per_frame;
+  void affected(uint64_t frame, int32_t obj) { objects_affected_per_frame[obj].insert(frame); }
+};
+
+struct Formulation {
+  Map* map;
+  dynob_params params;
+  NoiseModels noise;
+  Values theta;
+  Graph factors;
+  std::set<uint64_t> is_other_values_in_map;       // Formulation.hpp:448
+  std::set<int64_t> is_dynamic_tracklet_in_map;    // WorldPoseEstimator.hpp:79
+  // WorldMotionAccessor::object_pose_cache_ (object -> frame -> pose)
+  std::map<int32_t, std::map<uint64_t, P3>> object_pose_cache;
+  std::string err;
+  GraphExport gexp;
+  ValuesExport vexp;
+
+  Formulation(Map* m, const dynob_params& p) : map(m), params(p) {
+    // RGBDBackendModule.cc:89-113 and BackendModule::setFactorParams
+    // (BackendModule.cc:56-85)
+    const double hk = p.use_robust_kernels ? p.k_huber_3d_points : 0.0;
+    auto iso = [](double s, double h) {
+      Noise n;
+      for (int i = 0; i < 6; ++i) n.sigmas[i] = s;
+      n.huber = h;
+      return n;
+    };
+    noise.static_point = iso(p.static_point_sigma, hk);
+    noise.dynamic_point = iso(p.dynamic_point_sigma, hk);
+    noise.landmark_motion = iso(p.motion_ternary_sigma, hk);
+    noise.initial_pose_prior = iso(p.initial_pose_prior_sigma, 0.0);
+    for (int i = 0; i < 6; ++i) {
+      noise.odometry.sigmas[i] = p.odometry_sigmas[i];
+      noise.object_smoothing.sigmas[i] = p.smoothing_sigmas[i];
+    }
+    noise.odometry.huber = noise.object_smoothing.huber = 0.0;
+  }
+
+  bool motion_formulation() const { return params.formulation == DYNOB_MOTION_IN_WORLD; }
+
+  // ---- accessor (Accessor-impl.hpp, WorldPoseEstimator.cc:31-81,
+  //      WorldMotionEstimator.cc:32-66) ----
+  const Value* query(uint64_t key) const {
+    auto it = theta.find(key);
+    return it == theta.end() ? nullptr : &it->second;
+  }
+  bool sensor_pose(uint64_t f, P3* X) const {
+    DB_CHECK(map->frame(f) != nullptr, DYNOHIP_ESTATE, "getSensorPose: frame " + std::to_string(f) + " not in map");
+    const Value* v = query(camera_pose_key(f));
+    if (!v) return false;
+    if (X) *X = pose_from(v->d);
+    return true;
+  }
+  bool object_motion(uint64_t f, int32_t obj, P3* H) const {
+    DB_CHECK(map->frame(f) != nullptr, DYNOHIP_ESTATE, "getObjectMotion: frame not in map");
+    if (motion_formulation()) {
+      const Value* v = query(motion_key(obj, f));
+      if (!v) return false;
+      if (H) *H = pose_from(v->d);
+      return true;
+    }
+    // WorldPoseAccessor::getObjectMotion: L_k * L_{k-1}^-1 for k >= 2
+    if (f < 2) return false;
+    P3 Lk, Lk1;
+    if (!object_pose(f, obj, &Lk) || !object_pose(f - 1u, obj, &Lk1)) return false;
+    if (H) *H = dynohip::compose(Lk, dynohip::inverse(Lk1));
+    return true;
+  }
+  bool object_pose(uint64_t f, int32_t obj, P3* L) const {
+    if (motion_formulation()) {
+      // WorldMotionAccessor::getObjectPose: the propagated cache
+      auto it = object_pose_cache.find(obj);
+      if (it == object_pose_cache.end()) return false;
+      auto jt = it->second.find(f);
+      if (jt == it->second.end()) return false;
+      if (L) *L = jt->second;
+      return true;
+    }
+    if (!map->frame(f)) return false;
+    const Value* v = query(object_pose_key(obj, f));
+    if (!v) return false;
+    if (L) *L = pose_from(v->d);
+    return true;
+  }
+  bool dynamic_landmark(uint64_t f, int64_t trk, double* p) const {
+    DB_CHECK(map->landmark(trk) != nullptr, DYNOHIP_ESTATE, "getDynamicLandmark: unknown tracklet");
+    const Value* v = query(dynamic_key(f, trk));
+    if (!v) return false;
+    if (p) std::memcpy(p, v->d, 3 * sizeof(double));
+    return true;
+  }
+  bool static_landmark(int64_t trk, double* p) const {
+    const LandmarkNode* ln = map->landmark(trk);
+    DB_CHECK(ln != nullptr, DYNOHIP_ESTATE, "getStaticLandmark: unknown tracklet");
+    DB_CHECK(ln->is_static(), DYNOHIP_EINVAL, "Static estimate requested but landmark is dynamic!");
+    const Value* v = query(static_key(trk));
+    if (!v) return false;
+    if (p) std::memcpy(p, v->d, 3 * sizeof(double));
+    return true;
+  }
+  // getDynamicLandmarkEstimates(frame, object) (Accessor-impl.hpp:133-164)
+  void dynamic_estimates(uint64_t f, int32_t obj, std::vector<int64_t>& trk, std::vector<double>& xyz) const {
+    const FrameNode* fn = map->frame(f);
+    DB_CHECK(fn != nullptr, DYNOHIP_ESTATE, "getDynamicLandmarkEstimates: frame not in map");
+    if (!fn->object_observed(obj)) return;
+    for (int64_t t : fn->dynamic_landmarks) {
+      if (map->landmarks.at(t).object_id != obj) continue;
+      double p[3];
+      if (dynamic_landmark(f, t, p)) {
+        trk.push_back(t);
+        xyz.insert(xyz.end(), p, p + 3);
+      }
+    }
+  }
+  // computeObjectCentroid (Accessor-impl.hpp:290-318): groupObjectCloud
+  // (world points, PointCloudProcess.cc:97-124) then pcl::computeCentroid —
+  // pcl::CentroidPoint accumulates the PointXYZ (float) coordinates in an
+  // Eigen::Vector3f and divides by the float count.
+  bool object_centroid(uint64_t f, int32_t obj, double* c) const {
+    std::vector<int64_t> trk;
+    std::vector<double> xyz;
+    dynamic_estimates(f, obj, trk, xyz);
+    if (trk.empty()) return false;
+    float acc[3] = {0.f, 0.f, 0.f};
+    for (size_t i = 0; i < trk.size(); ++i)
+      for (int d = 0; d < 3; ++d) acc[d] += static_cast<float>(xyz[3 * i + d]);
+    const float n = static_cast<float>(trk.size());
+    for (int d = 0; d < 3; ++d) c[d] = static_cast<double>(acc[d] / n);
+    return true;
+  }
+
+  // Formulation::getInitialOrLinearizedSensorPose (Formulation-impl.hpp:63-76)
+  P3 initial_or_linearized_sensor_pose(uint64_t f) const {
+    P3 X_theta, X_init;
+    const bool have_theta = sensor_pose(f, &X_theta);
+    DB_CHECK(map->initial_sensor_pose(f, &X_init), DYNOHIP_ESTATE,
+             "no initial sensor pose for frame " + std::to_string(f));
+    return have_theta ? X_theta : X_init;
+  }
+
+  // ---- graph construction ----
+  // Formulation::setInitialPose (Formulation-impl.hpp:83-89)
+  void set_initial_pose(uint64_t f, const P3& T, Values& new_values) {
+    values_insert(new_values, camera_pose_key(f), pose_value(T));
+    values_insert_or_assign(theta, new_values);
+  }
+  // Formulation::setInitialPosePrior (Formulation-impl.hpp:91-104)
+  void set_initial_pose_prior(uint64_t f, const P3& T, Graph& new_factors) {
+    Graph internal;
+    double m[12];
+    pose_to(T, m);
+    internal.add(kPrior, {camera_pose_key(f)}, m, noise.initial_pose_prior);
+    new_factors.append(internal);
+    factors.append(internal);
+  }
+  // Formulation::addOdometry (Formulation-impl.hpp:128-161)
+  void add_odometry(uint64_t f, const P3& T_world_camera, Values& new_values, Graph& new_factors) {
+    values_insert(new_values, camera_pose_key(f), pose_value(T_world_camera));
+    values_insert_or_assign(theta, new_values);
+    DB_CHECK(f > map->first_frame_id(), DYNOHIP_ESTATE, "addOdometry at the first frame");
+    P3 T_k_1;
+    DB_CHECK(map->initial_sensor_pose(f - 1u, &T_k_1), DYNOHIP_ESTATE,
+             "no frontend pose for frame " + std::to_string(f - 1u));
+    const P3 odom = dynohip::compose(dynohip::inverse(T_k_1), T_world_camera);
+    Graph internal;
+    double m[12];
+    pose_to(odom, m);
+    // factor_graph_tools::addBetweenFactor (FactorGraphTools.cc:73-83)
+    internal.add(kBetween, {camera_pose_key(f - 1u), camera_pose_key(f)}, m, noise.odometry);
+    factors.append(internal);
+    new_factors.append(internal);
+  }
+
+  // Formulation::updateStaticObservations (Formulation-impl.hpp:203-305)
+  void update_static(uint64_t k, Values& new_values, Graph& new_factors, bool do_backtrack) {
+    Graph internal;
+    const FrameNode* fk = map->frame(k);
+    DB_CHECK(fk != nullptr, DYNOHIP_ESTATE, "updateStaticObservations: frame not in map");
+    P3 T_world_camera_frontend;
+    DB_CHECK(map->initial_sensor_pose(k, &T_world_camera_frontend), DYNOHIP_ESTATE, "no frontend pose");
+    for (int64_t t : fk->static_landmarks) {
+      const LandmarkNode& ln = map->landmarks.at(t);
+      DB_CHECK(ln.is_static(), DYNOHIP_EINVAL, "Static estimate requested but landmark is dynamic!");
+      const uint64_t point_key = static_key(t);
+      if (is_other_values_in_map.count(point_key)) {
+        internal.add(kPoseToPoint, {camera_pose_key(k), point_key}, ln.measurement(k), noise.static_point);
+      } else {
+        if (static_cast<int64_t>(ln.num_observations()) < params.min_static_observations) continue;
+        for (const auto& kv : ln.measurements) {  // seen frames, ascending
+          const uint64_t seen = kv.first;
+          if (seen > k) break;
+          if (!do_backtrack && seen < k) continue;
+          internal.add(kPoseToPoint, {camera_pose_key(seen), point_key}, kv.second.data(), noise.static_point);
+        }
+        double lmk_world[3];
+        if (!static_landmark(t, lmk_world)) transform_from(T_world_camera_frontend, ln.measurement(k), lmk_world);
+        values_insert(new_values, point_key, point_value(lmk_world));
+        is_other_values_in_map.insert(point_key);
+      }
+    }
+    values_insert_or_assign(theta, new_values);
+    factors.append(internal);
+    new_factors.append(internal);
+  }
+
+  struct PointContext {
+    int64_t tracklet;
+    int32_t object;
+    uint64_t frame_k_1, frame_k;
+    P3 X_k_measured, X_k_1_measured;
+    bool is_starting_motion_frame;
+  };
+
+  // WorldMotionFormulation::dynamicPointUpdateCallback
+  // (WorldMotionEstimator.cc:155-238) and WorldPoseFormulation's
+  // (WorldPoseEstimator.cc:84-165)
+  void dynamic_point_update(const PointContext& c, UpdateResult& result, Values& new_values, Graph& nf) {
+    const LandmarkNode& ln = map->landmarks.at(c.tracklet);
+    const uint64_t key_k_1 = dynamic_key(c.frame_k_1, c.tracklet);
+    const uint64_t key_k = dynamic_key(c.frame_k, c.tracklet);
+    if (c.is_starting_motion_frame) {
+      if (motion_formulation())
+        DB_CHECK(query(key_k_1) == nullptr, DYNOHIP_ESTATE, "dynamic point at k-1 already in theta");
+      nf.add(kPoseToPoint, {camera_pose_key(c.frame_k_1), key_k_1}, ln.measurement(c.frame_k_1), noise.dynamic_point);
+      result.affected(c.frame_k_1, c.object);
+      double lmk[3];
+      if (const Value* v = query(key_k_1))
+        std::memcpy(lmk, v->d, sizeof(lmk));
+      else
+        transform_from(c.X_k_1_measured, ln.measurement(c.frame_k_1), lmk);
+      values_insert(new_values, key_k_1, point_value(lmk));
+    }
+    DB_CHECK(new_values.count(key_k_1) || query(key_k_1), DYNOHIP_ESTATE,
+             "previous dynamic point of tracklet " + std::to_string(c.tracklet) + " at frame " +
+                 std::to_string(c.frame_k_1) + " was never added");
+    nf.add(kPoseToPoint, {camera_pose_key(c.frame_k), key_k}, ln.measurement(c.frame_k), noise.dynamic_point);
+    result.affected(c.frame_k, c.object);
+    double lmk[3];
+    if (const Value* v = query(key_k))
+      std::memcpy(lmk, v->d, sizeof(lmk));
+    else
+      transform_from(c.X_k_measured, ln.measurement(c.frame_k), lmk);
+    values_insert(new_values, key_k, point_value(lmk));
+    if (motion_formulation()) {
+      nf.add(kTernary, {key_k_1, key_k, motion_key(c.object, c.frame_k)}, nullptr, noise.landmark_motion);
+    } else {
+      nf.add(kMotionPose,
+             {key_k_1, key_k, object_pose_key(c.object, c.frame_k_1), object_pose_key(c.object, c.frame_k)}, nullptr,
+             noise.landmark_motion);
+    }
+    result.affected(c.frame_k_1, c.object);
+    result.affected(c.frame_k, c.object);
+    is_dynamic_tracklet_in_map.insert(c.tracklet);
+  }
+
+  // WorldMotionFormulation::objectUpdateContext (WorldMotionEstimator.cc:240-316)
+  void object_update_motion(uint64_t frame, int32_t obj, bool has_motion_pair, Values& new_values, Graph& nf) {
+    const uint64_t H_k = motion_key(obj, frame);
+    if (!has_motion_pair) return;
+    if (!is_other_values_in_map.count(H_k)) {
+      P3 initial = pose_identity();
+      if (!params.init_H_with_identity) {
+        P3 m;
+        if (map->initial_object_motion(frame, obj, &m)) initial = m;
+        const P3 I = pose_identity();
+        std::memcpy(initial.R, I.R, sizeof(I.R));  // Pose3(Rot3::Identity(), t)
+      }
+      values_insert(new_values, H_k, pose_value(initial));
+      is_other_values_in_map.insert(H_k);
+    }
+    if (frame < 2) return;
+    const FrameNode* fk1 = map->frame(frame - 1u);
+    if (!fk1) return;
+    if (params.use_smoothing_factor && fk1->object_observed(obj)) {
+      const uint64_t H_k_1 = motion_key(obj, frame - 1u);
+      if (is_other_values_in_map.count(H_k_1) && is_other_values_in_map.count(H_k)) {
+        double I[12];
+        pose_to(pose_identity(), I);
+        nf.add(kBetween, {H_k_1, H_k}, I, noise.object_smoothing);
+      }
+    }
+  }
+
+  // WorldPoseFormulation::objectUpdateContext (WorldPoseEstimator.cc:168-283)
+  void object_update_pose(uint64_t frame, int32_t obj, Values& new_values, Graph& nf) {
+    const uint64_t L_k = object_pose_key(obj, frame);
+    if (!is_other_values_in_map.count(L_k)) {
+      P3 pose_k_1;
+      const bool have_k_1 = object_pose(frame - 1u, obj, &pose_k_1);
+      const std::set<uint64_t> seen = map->object_seen_frames(obj);
+      const uint64_t first_seen = *seen.begin();
+      P3 motion, object_pose_k;
+      if (map->initial_object_motion(frame, obj, &motion) && have_k_1) {
+        object_pose_k = dynohip::compose(motion, pose_k_1);
+        DB_CHECK(first_seen != frame, DYNOHIP_ESTATE, "object motion at the first seen frame");
+      } else {
+        double c[3];
+        DB_CHECK(object_centroid(frame, obj, c), DYNOHIP_ESTATE, "computeObjectCentroid failed");
+        P3 initial = pose_identity();
+        std::memcpy(initial.t, c, sizeof(c));
+        if (const Value* v = query(L_k))
+          object_pose_k = pose_from(v->d);
+        else
+          object_pose_k = initial;
+      }
+      values_insert(new_values, L_k, pose_value(object_pose_k));
+      is_other_values_in_map.insert(L_k);
+    }
+    if (params.use_smoothing_factor) {
+      if (frame < 2) return;
+      if (!map->frame(frame - 2u) || !map->frame(frame - 1u)) return;
+      const uint64_t L_k_2 = object_pose_key(obj, frame - 2u), L_k_1 = object_pose_key(obj, frame - 1u);
+      if (is_other_values_in_map.count(L_k_1) && is_other_values_in_map.count(L_k) &&
+          is_other_values_in_map.count(L_k_2))
+        nf.add(kPoseSmoothing, {L_k_2, L_k_1, L_k}, nullptr, noise.object_smoothing);
+    }
+  }
+
+  // Formulation::updateDynamicObservations (Formulation-impl.hpp:307-584)
+  void update_dynamic(uint64_t k, Values& new_values, Graph& new_factors, bool do_backtrack) {
+    constexpr size_t kMinNumberPoints = 3u;
+    Graph internal;
+    UpdateResult result;
+    const uint64_t k_1 = k - 1u;
+    const FrameNode* fk = map->frame(k);
+    DB_CHECK(fk != nullptr, DYNOHIP_ESTATE, "updateDynamicObservations: frame not in map");
+    DB_CHECK(map->frame(k_1) != nullptr, DYNOHIP_ESTATE, "updateDynamicObservations: frame k-1 not in map");
+    for (int32_t obj : fk->objects_seen) {
+      if (!map->object_motion_expected(k, obj)) continue;
+      const std::vector<int64_t> seen_k = map->object_landmarks_at(obj, k);
+      if (seen_k.size() < kMinNumberPoints || map->object_landmarks_at(obj, k_1).size() < kMinNumberPoints) continue;
+      for (int64_t t : seen_k) {
+        const LandmarkNode& ln = map->landmarks.at(t);
+        if (static_cast<int64_t>(ln.num_observations()) < params.min_dynamic_observations) continue;
+        if (!is_dynamic_tracklet_in_map.count(t)) {
+          const uint64_t first = ln.measurements.begin()->first;
+          uint64_t start;
+          if (do_backtrack) {
+            start = first + 1u;
+          } else {
+            start = k;
+            if (start < first + 1u) continue;  // "we will have to get it next frame"
+          }
+          auto start_it = ln.measurements.find(start);
+          DB_CHECK(start_it != ln.measurements.end(), DYNOHIP_ESTATE,
+                   "Starting motion frame is " + std::to_string(start) + " but first frame is " +
+                       std::to_string(first));
+          for (auto it = start_it; it != ln.measurements.end(); ++it) {
+            auto prev = std::prev(it);
+            DB_CHECK(it->first == prev->first + 1u, DYNOHIP_ESTATE,
+                     "tracklet " + std::to_string(t) + " is not seen in consecutive frames");
+            if (it->first > k) break;
+            P3 X_k_1;
+            DB_CHECK(sensor_pose(prev->first, &X_k_1), DYNOHIP_ESTATE,
+                     "Failed cam pose query at frame " + std::to_string(prev->first));
+            PointContext c;
+            c.tracklet = t;
+            c.object = obj;
+            c.frame_k_1 = prev->first;
+            c.frame_k = it->first;
+            // the reference reads the sensor pose at k-1 here as well
+            // (Formulation-impl.hpp:470-471), and initialises the point at k
+            // with it; kept for parity
+            c.X_k_measured = initial_or_linearized_sensor_pose(prev->first);
+            c.X_k_1_measured = X_k_1;
+            c.is_starting_motion_frame = (it == start_it);
+            Values local;
+            dynamic_point_update(c, result, local, internal);
+            values_insert(theta, local);
+            values_insert(new_values, local);
+          }
+        } else {
+          PointContext c;
+          c.tracklet = t;
+          c.object = obj;
+          c.frame_k_1 = k_1;
+          c.frame_k = k;
+          c.X_k_1_measured = initial_or_linearized_sensor_pose(k_1);
+          c.X_k_measured = initial_or_linearized_sensor_pose(k);
+          c.is_starting_motion_frame = false;
+          Values local;
+          dynamic_point_update(c, result, local, internal);
+          values_insert(theta, local);
+          values_insert(new_values, local);
+        }
+      }
+    }
+    for (const auto& kv : result.objects_affected_per_frame) {
+      const int32_t obj = kv.first;
+      DB_CHECK(kv.second.size() >= 2u, DYNOHIP_ESTATE, "object affected at fewer than two frames");
+      size_t idx = 0;
+      for (uint64_t frame : kv.second) {
+        Values local;
+        if (motion_formulation())
+          object_update_motion(frame, obj, idx > 0, local, internal);
+        else
+          object_update_pose(frame, obj, local, internal);
+        values_insert(theta, local);
+        values_insert(new_values, local);
+        ++idx;
+      }
+    }
+    factors.append(internal);
+    new_factors.append(internal);
+  }
+
+  // ---- WorldMotionAccessor::postUpdateCallback (WorldMotionEstimator.cc:68-152)
+  //      + propogateObjectPoses (DynamicObjects.cc:48-190) ----
+  std::map<int32_t, std::array<double, 3>> centroids(uint64_t f) const {
+    std::map<int32_t, std::array<double, 3>> out;
+    const FrameNode* fn = map->frame(f);
+    if (!fn) return out;
+    for (int32_t obj : fn->objects_seen) {
+      double c[3];
+      if (object_centroid(f, obj, c)) out[obj] = {c[0], c[1], c[2]};
+    }
+    return out;
+  }
+  static P3 slerp(const P3& X, const P3& Y, double t) {
+    // gtsam::interpolate: X * Expmap(t * Logmap(X^-1 Y)) (Pose3::slerp, GTSAM 4.2)
+    double xi[6];
+    dynohip::pose_logmap(dynohip::compose(dynohip::inverse(X), Y), xi);
+    for (double& v : xi) v *= t;
+    return dynohip::compose(X, dynohip::pose_expmap(xi));
+  }
+  void post_update() {
+    if (!motion_formulation()) return;  // WorldPoseAccessor has no cache
+    std::map<int32_t, std::map<uint64_t, P3>> object_poses;
+    if (map->frames.size() < 2) {
+      object_pose_cache = object_poses;
+      return;
+    }
+    auto it = std::next(map->frames.begin());
+    for (; it != map->frames.end(); ++it) {
+      const uint64_t k = it->first, k_1 = std::prev(it)->first;
+      DB_CHECK(k_1 + 1 == k, DYNOHIP_ESTATE, "map frames are not consecutive");
+      const auto c_k = centroids(k), c_k_1 = centroids(k_1);
+      // getObjectMotions(k): objects seen at k with a motion estimate
+      std::vector<std::pair<int32_t, P3>> motions;
+      for (int32_t obj : it->second.objects_seen) {
+        P3 H;
+        if (object_motion(k, obj, &H)) motions.emplace_back(obj, H);
+      }
+      for (const auto& om : motions) {
+        const int32_t obj = om.first;
+        DB_CHECK(c_k.count(obj) && c_k_1.count(obj), DYNOHIP_ESTATE, "motion without object centroids");
+        const auto& ck = c_k.at(obj);
+        const auto& ck1 = c_k_1.at(obj);
+        auto centroid_pose = [](const std::array<double, 3>& c) {
+          P3 T = pose_identity();
+          T.t[0] = c[0];
+          T.t[1] = c[1];
+          T.t[2] = c[2];
+          return T;
+        };
+        auto& per_frame = object_poses[obj];
+        if (per_frame.empty()) per_frame.emplace(k_1, centroid_pose(ck1));  // new object: pose at k-1
+        auto pk1 = per_frame.find(k_1);
+        if (pk1 != per_frame.end()) {
+          per_frame.emplace(k, dynohip::compose(om.second, pk1->second));
+        } else {
+          const size_t min_diff_frames = 3;
+          const uint64_t last_frame = per_frame.rbegin()->first;
+          const P3 last_pose = per_frame.rbegin()->second;
+          P3 current = last_pose;
+          current.t[0] = ck[0];
+          current.t[1] = ck[1];
+          current.t[2] = ck[2];
+          DB_CHECK(last_frame < k_1, DYNOHIP_ESTATE, "propogateObjectPoses: last frame not before k-1");
+          if (k - last_frame < min_diff_frames) {
+            const size_t N = k - last_frame + 1;
+            const double divisor = static_cast<double>(k - last_frame);
+            for (size_t j = 0; j < N; ++j) {
+              const double tt = static_cast<double>(j) / divisor;
+              per_frame.emplace(last_frame + j, slerp(last_pose, current, tt));
+            }
+          } else {
+            const P3 pose_k_1 = centroid_pose(ck1);
+            per_frame.emplace(k_1, pose_k_1);
+            per_frame.emplace(k, dynohip::compose(om.second, pose_k_1));
+          }
+        }
+      }
+    }
+    object_pose_cache = object_poses;
+  }
+
+  // Accessor::getObjectPoses() (Accessor-impl.hpp:96-116)
+  void object_poses_all(std::vector<int32_t>& objs, std::vector<uint64_t>& frames, std::vector<double>& poses) const {
+    std::map<int32_t, std::map<uint64_t, P3>> out;
+    for (const auto& fkv : map->frames)
+      for (int32_t obj : fkv.second.objects_seen) {
+        P3 L;
+        if (object_pose(fkv.first, obj, &L)) out[obj].emplace(fkv.first, L);
+      }
+    for (const auto& okv : out)
+      for (const auto& fkv : okv.second) {
+        objs.push_back(okv.first);
+        frames.push_back(fkv.first);
+        double d[12];
+        pose_to(fkv.second, d);
+        poses.insert(poses.end(), d, d + 12);
+      }
+  }
+};
+
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace dynob
+
+using namespace dynob;
+
+struct dynob_map {
+  Map map;
+  std::string err;
+};
+struct dynob_formulation {
+  std::unique_ptr<Formulation> f;
+};
+struct dynob_module {
+  dynob_params params;
+  dynob_module_params mp;
+  dynob_map map;
+  dynob_formulation updater;  // new_updater_
+  dynohip_sliding_window window;
+  bool bootstrapped = false;
+  dynohip_solver* solver = nullptr;
+  std::string err;
+  // last solved problem
+  GraphExport last_graph;
+  ValuesExport last_values;
+  std::vector<double> last_optimised;
+};
+
+namespace {
+
+template <typename Fn>
+int guard(std::string& err, Fn&& fn) {
+  try {
+    fn();
+    return DYNOHIP_OK;
+  } catch (const Error& e) {
+    err = e.what();
+    return e.code;
+  } catch (const std::exception& e) {
+    err = e.what();
+    return DYNOHIP_EINVAL;
+  }
+}
+
+int64_t list_out(const std::vector<int64_t>& v, int64_t* out, size_t cap, size_t* n_out) {
+  if (n_out) *n_out = v.size();
+  if (out)
+    for (size_t i = 0; i < v.size() && i < cap; ++i) out[i] = v[i];
+  return static_cast<int64_t>(v.size());
+}
+
+// RGBDBackendModule::constructGraph (RGBDBackendModule.cc:246-296): a fresh
+// updater over [from, to]; its theta_ / factors_ are exactly the returned
+// new_values / new_factors.
+std::unique_ptr<Formulation> construct_graph(Map* map, const dynob_params& p, uint64_t from, uint64_t to,
+                                             bool set_initial_camera_pose_prior) {
+  DB_CHECK(from < to, DYNOHIP_EINVAL, "constructGraph: from >= to");
+  DB_CHECK(from >= map->first_frame_id() && to <= map->last_frame_id(), DYNOHIP_ESTATE,
+           "constructGraph: window outside the map");
+  auto u = std::make_unique<Formulation>(map, p);
+  Values new_values;
+  Graph new_factors;
+  for (uint64_t f = from; f <= to; ++f) {
+    P3 T;
+    DB_CHECK(map->initial_sensor_pose(f, &T), DYNOHIP_ESTATE, "no frontend pose for frame " + std::to_string(f));
+    if (f == from) {
+      u->set_initial_pose(f, T, new_values);
+      if (set_initial_camera_pose_prior) u->set_initial_pose_prior(f, T, new_factors);
+    } else {
+      u->add_odometry(f, T, new_values, new_factors);
+      u->update_dynamic(f, new_values, new_factors, false);
+    }
+    u->update_static(f, new_values, new_factors, false);
+  }
+  return u;
+}
+
+int solve(dynob_module* m, const Formulation& problem, dynob_spin_result* r) {
+  m->last_graph.build(problem.factors);
+  m->last_values.build(problem.theta);
+  m->last_optimised = m->last_values.data;
+  if (!m->mp.optimize) return DYNOHIP_OK;
+  if (!m->solver) {
+    const int rc = dynohip_create(m->mp.device_id, &m->solver);
+    if (rc != DYNOHIP_OK) {
+      m->err = "dynohip_create failed";
+      return rc;
+    }
+  }
+  const double t0 = now_ms();
+  dynohip_graph_view gv;
+  m->last_graph.view(&gv);
+  int rc = dynohip_set_graph(m->solver, &gv);
+  if (rc == DYNOHIP_OK)
+    rc = dynohip_set_values(m->solver, m->last_values.keys.data(), m->last_values.kinds.data(),
+                            m->last_values.data.data(), m->last_values.keys.size());
+  dynohip_lm_summary s;
+  if (rc == DYNOHIP_OK) rc = dynohip_optimize(m->solver, &m->mp.lm, &s);
+  if (rc == DYNOHIP_OK)
+    rc = dynohip_get_values(m->solver, m->last_optimised.data(), m->last_optimised.size());
+  if (rc != DYNOHIP_OK) {
+    m->err = std::string("LM solve failed: ") + dynohip_last_error(m->solver);
+    return rc;
+  }
+  r->optimized = 1;
+  r->iterations = s.iterations;
+  r->inner_iterations = s.inner_iterations;
+  r->error_before = s.initial_error;
+  r->error_after = s.final_error;
+  r->ms_optimize = now_ms() - t0;
+  // Formulation::updateTheta (Formulation-impl.hpp:53-60): insert_or_assign
+  Values opt;
+  size_t off = 0;
+  for (size_t i = 0; i < m->last_values.keys.size(); ++i) {
+    Value v;
+    std::memset(&v, 0, sizeof(v));
+    v.kind = m->last_values.kinds[i];
+    const size_t len = v.kind == DYNOHIP_POSE3 ? 12 : 3;
+    std::memcpy(v.d, m->last_optimised.data() + off, len * sizeof(double));
+    off += len;
+    opt[m->last_values.keys[i]] = v;
+  }
+  values_insert_or_assign(m->updater.f->theta, opt);
+  return DYNOHIP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+// ---------------------------------------------------------------- map ----
+int dynob_map_create(dynob_map** out) {
+  if (!out) return DYNOHIP_EINVAL;
+  *out = new dynob_map();
+  return DYNOHIP_OK;
+}
+void dynob_map_destroy(dynob_map* m) { delete m; }
+const char* dynob_map_last_error(const dynob_map* m) { return m ? m->err.c_str() : "null map"; }
+
+int dynob_map_update_observations(dynob_map* m, const dynob_measurement* meas, size_t n) {
+  if (!m || (n && !meas)) return DYNOHIP_EINVAL;
+  return guard(m->err, [&] {
+    for (size_t i = 0; i < n; ++i) m->map.add(meas[i]);
+  });
+}
+
+int dynob_map_update_sensor_pose(dynob_map* m, uint64_t frame_id, const double* pose12) {
+  if (!m || !pose12) return DYNOHIP_EINVAL;
+  return guard(m->err, [&] {
+    FrameNode* fn = m->map.frame(frame_id);
+    DB_CHECK(fn != nullptr, DYNOHIP_ESTATE, "updateSensorPoseMeasurement: frame " + std::to_string(frame_id) +
+                                                 " not in map");
+    fn->has_X = true;
+    fn->X_world = pose_from(pose12);
+  });
+}
+
+int dynob_map_update_object_motions(dynob_map* m, uint64_t frame_id, const int32_t* ids, const double* motions,
+                                    size_t n) {
+  if (!m || (n && (!ids || !motions))) return DYNOHIP_EINVAL;
+  return guard(m->err, [&] {
+    FrameNode* fn = m->map.frame(frame_id);
+    DB_CHECK(fn != nullptr, DYNOHIP_ESTATE, "updateObjectMotionMeasurements: frame not in map");
+    fn->has_motions = true;
+    fn->motions_world.clear();
+    for (size_t i = 0; i < n; ++i) fn->motions_world[ids[i]] = pose_from(motions + 12 * i);
+  });
+}
+
+int64_t dynob_map_query(const dynob_map* mh, int what, int64_t a, int64_t b, int64_t* out, size_t cap,
+                        size_t* n_out) {
+  if (!mh) return DYNOHIP_EINVAL;
+  const Map& m = mh->map;
+  if (n_out) *n_out = 0;
+  const uint64_t fa = static_cast<uint64_t>(a);
+  std::vector<int64_t> v;
+  switch (what) {
+    case DYNOB_Q_FRAME_EXISTS: return m.frame(fa) != nullptr;
+    case DYNOB_Q_LANDMARK_EXISTS: return m.landmark(a) != nullptr;
+    case DYNOB_Q_OBJECT_EXISTS: return m.object(static_cast<int32_t>(a)) != nullptr;
+    case DYNOB_Q_NUM_OBJECTS: return static_cast<int64_t>(m.objects.size());
+    case DYNOB_Q_OBJECT_OBSERVED: {
+      const FrameNode* fn = m.frame(fa);
+      return fn && fn->object_observed(static_cast<int32_t>(b));
+    }
+    case DYNOB_Q_OBJECT_OBSERVED_IN_PREVIOUS:
+      return m.frame(fa) ? m.object_observed_in_previous(fa, static_cast<int32_t>(b)) : DYNOHIP_EINVAL;
+    case DYNOB_Q_OBJECT_MOTION_EXPECTED:
+      return m.frame(fa) ? m.object_motion_expected(fa, static_cast<int32_t>(b)) : DYNOHIP_EINVAL;
+    case DYNOB_Q_LANDMARK_NUM_OBS: {
+      const LandmarkNode* ln = m.landmark(a);
+      return ln ? static_cast<int64_t>(ln->num_observations()) : DYNOHIP_EINVAL;
+    }
+    case DYNOB_Q_LANDMARK_OBJECT: {
+      const LandmarkNode* ln = m.landmark(a);
+      return ln ? ln->object_id : DYNOHIP_EINVAL;
+    }
+    case DYNOB_Q_FIRST_FRAME: return m.frames.empty() ? DYNOHIP_ESTATE : static_cast<int64_t>(m.frames.begin()->first);
+    case DYNOB_Q_LAST_FRAME: return m.frames.empty() ? DYNOHIP_ESTATE : static_cast<int64_t>(m.frames.rbegin()->first);
+    case DYNOB_Q_FRAME_IDS:
+      for (const auto& kv : m.frames) v.push_back(static_cast<int64_t>(kv.first));
+      return list_out(v, out, cap, n_out);
+    case DYNOB_Q_OBJECT_IDS:
+      for (const auto& kv : m.objects) v.push_back(kv.first);
+      return list_out(v, out, cap, n_out);
+    case DYNOB_Q_STATIC_TRACKLETS_BY_FRAME:
+    case DYNOB_Q_DYNAMIC_TRACKLETS_BY_FRAME:
+    case DYNOB_Q_FRAME_OBJECTS_SEEN: {
+      const FrameNode* fn = m.frame(fa);
+      if (!fn) return DYNOHIP_EINVAL;
+      if (what == DYNOB_Q_STATIC_TRACKLETS_BY_FRAME) v.assign(fn->static_landmarks.begin(), fn->static_landmarks.end());
+      if (what == DYNOB_Q_DYNAMIC_TRACKLETS_BY_FRAME)
+        v.assign(fn->dynamic_landmarks.begin(), fn->dynamic_landmarks.end());
+      if (what == DYNOB_Q_FRAME_OBJECTS_SEEN) v.assign(fn->objects_seen.begin(), fn->objects_seen.end());
+      return list_out(v, out, cap, n_out);
+    }
+    case DYNOB_Q_LANDMARK_SEEN_FRAMES: {
+      const LandmarkNode* ln = m.landmark(a);
+      if (!ln) return DYNOHIP_EINVAL;
+      for (const auto& kv : ln->measurements) v.push_back(static_cast<int64_t>(kv.first));
+      return list_out(v, out, cap, n_out);
+    }
+    case DYNOB_Q_OBJECT_SEEN_FRAMES: {
+      if (!m.object(static_cast<int32_t>(a))) return DYNOHIP_EINVAL;
+      for (uint64_t f : m.object_seen_frames(static_cast<int32_t>(a))) v.push_back(static_cast<int64_t>(f));
+      return list_out(v, out, cap, n_out);
+    }
+    case DYNOB_Q_OBJECT_LANDMARKS: {
+      const ObjectNode* on = m.object(static_cast<int32_t>(a));
+      if (!on) return DYNOHIP_EINVAL;
+      v.assign(on->dynamic_landmarks.begin(), on->dynamic_landmarks.end());
+      return list_out(v, out, cap, n_out);
+    }
+    case DYNOB_Q_OBJECT_LANDMARKS_AT_FRAME:
+      if (!m.object(static_cast<int32_t>(a))) return DYNOHIP_EINVAL;
+      return list_out(m.object_landmarks_at(static_cast<int32_t>(a), static_cast<uint64_t>(b)), out, cap, n_out);
+    default: return DYNOHIP_EINVAL;
+  }
+}
+
+// -------------------------------------------------------- formulation ----
+void dynob_params_default(dynob_params* p, int shipped_flags) {
+  if (!p) return;
+  std::memset(p, 0, sizeof(*p));
+  p->formulation = DYNOB_MOTION_IN_WORLD;
+  p->min_static_observations = 2;
+  p->min_dynamic_observations = 3;
+  p->use_smoothing_factor = 1;
+  p->init_H_with_identity = 1;
+  p->use_robust_kernels = 1;
+  p->k_huber_3d_points = 1e-4;
+  p->static_point_sigma = 0.06;
+  p->dynamic_point_sigma = 0.0625;
+  p->initial_pose_prior_sigma = 1e-4;
+  // backend.flags:8-19 vs BackendParams.cc:26-35
+  const double odo_r = shipped_flags ? 0.05 : 0.02, odo_t = shipped_flags ? 0.1 : 0.01;
+  const double sm_r = 0.01, sm_t = shipped_flags ? 0.01 : 0.1;
+  p->motion_ternary_sigma = shipped_flags ? 1e-5 : 0.01;
+  for (int i = 0; i < 3; ++i) {
+    p->odometry_sigmas[i] = odo_r;
+    p->odometry_sigmas[3 + i] = odo_t;
+    p->smoothing_sigmas[i] = sm_r;
+    p->smoothing_sigmas[3 + i] = sm_t;
+  }
+}
+
+static bool params_valid(const dynob_params* p) {
+  if (!p || (p->formulation != DYNOB_MOTION_IN_WORLD && p->formulation != DYNOB_LL_WORLD)) return false;
+  if (!(p->static_point_sigma > 0 && p->dynamic_point_sigma > 0 && p->motion_ternary_sigma > 0 &&
+        p->initial_pose_prior_sigma > 0))
+    return false;
+  for (int i = 0; i < 6; ++i)
+    if (!(p->odometry_sigmas[i] > 0 && p->smoothing_sigmas[i] > 0)) return false;
+  return true;
+}
+
+int dynob_formulation_create(dynob_map* map, const dynob_params* p, dynob_formulation** out) {
+  if (!map || !out || !params_valid(p)) return DYNOHIP_EINVAL;
+  auto* f = new dynob_formulation();
+  f->f = std::make_unique<Formulation>(&map->map, *p);
+  *out = f;
+  return DYNOHIP_OK;
+}
+void dynob_formulation_destroy(dynob_formulation* f) { delete f; }
+const char* dynob_formulation_last_error(const dynob_formulation* f) { return f ? f->f->err.c_str() : "null"; }
+
+int dynob_set_initial_pose(dynob_formulation* f, uint64_t frame_id, const double* pose12) {
+  if (!f || !pose12) return DYNOHIP_EINVAL;
+  return guard(f->f->err, [&] {
+    Values nv;
+    f->f->set_initial_pose(frame_id, pose_from(pose12), nv);
+  });
+}
+int dynob_set_initial_pose_prior(dynob_formulation* f, uint64_t frame_id, const double* pose12) {
+  if (!f || !pose12) return DYNOHIP_EINVAL;
+  return guard(f->f->err, [&] {
+    Graph nf;
+    f->f->set_initial_pose_prior(frame_id, pose_from(pose12), nf);
+  });
+}
+int dynob_add_odometry(dynob_formulation* f, uint64_t frame_id, const double* pose12) {
+  if (!f || !pose12) return DYNOHIP_EINVAL;
+  return guard(f->f->err, [&] {
+    Values nv;
+    Graph nf;
+    f->f->add_odometry(frame_id, pose_from(pose12), nv, nf);
+  });
+}
+int dynob_update_static_observations(dynob_formulation* f, uint64_t frame_id, int do_backtrack) {
+  if (!f) return DYNOHIP_EINVAL;
+  return guard(f->f->err, [&] {
+    Values nv;
+    Graph nf;
+    f->f->update_static(frame_id, nv, nf, do_backtrack != 0);
+  });
+}
+int dynob_update_dynamic_observations(dynob_formulation* f, uint64_t frame_id, int do_backtrack) {
+  if (!f) return DYNOHIP_EINVAL;
+  return guard(f->f->err, [&] {
+    Values nv;
+    Graph nf;
+    f->f->update_dynamic(frame_id, nv, nf, do_backtrack != 0);
+  });
+}
+int dynob_update_theta(dynob_formulation* f, const uint64_t* keys, const uint8_t* kinds, const double* data,
+                       size_t n) {
+  if (!f || (n && (!keys || !kinds || !data))) return DYNOHIP_EINVAL;
+  return guard(f->f->err, [&] {
+    Values v;
+    size_t off = 0;
+    for (size_t i = 0; i < n; ++i) {
+      DB_CHECK(kinds[i] == DYNOHIP_POSE3 || kinds[i] == DYNOHIP_POINT3, DYNOHIP_EINVAL, "bad value kind");
+      Value x;
+      std::memset(&x, 0, sizeof(x));
+      x.kind = kinds[i];
+      const size_t len = kinds[i] == DYNOHIP_POSE3 ? 12 : 3;
+      std::memcpy(x.d, data + off, len * sizeof(double));
+      off += len;
+      v[keys[i]] = x;
+    }
+    values_insert_or_assign(f->f->theta, v);
+  });
+}
+
+int dynob_formulation_graph(dynob_formulation* f, dynohip_graph_view* g) {
+  if (!f || !g) return DYNOHIP_EINVAL;
+  f->f->gexp.build(f->f->factors);
+  f->f->gexp.view(g);
+  return DYNOHIP_OK;
+}
+int dynob_formulation_values(dynob_formulation* f, const uint64_t** keys, const uint8_t** kinds,
+                             const double** data, size_t* n, size_t* n_doubles) {
+  if (!f) return DYNOHIP_EINVAL;
+  f->f->vexp.build(f->f->theta);
+  if (keys) *keys = f->f->vexp.keys.data();
+  if (kinds) *kinds = f->f->vexp.kinds.data();
+  if (data) *data = f->f->vexp.data.data();
+  if (n) *n = f->f->vexp.keys.size();
+  if (n_doubles) *n_doubles = f->f->vexp.data.size();
+  return DYNOHIP_OK;
+}
+int dynob_formulation_factor_types(dynob_formulation* f, uint8_t* types, size_t cap, size_t* n_out) {
+  if (!f) return DYNOHIP_EINVAL;
+  const auto& fs = f->f->factors.factors;
+  if (n_out) *n_out = fs.size();
+  if (types)
+    for (size_t i = 0; i < fs.size() && i < cap; ++i) types[i] = fs[i].type;
+  return DYNOHIP_OK;
+}
+
+int dynob_get_sensor_pose(dynob_formulation* f, uint64_t frame_id, double* pose12) {
+  if (!f) return DYNOHIP_EINVAL;
+  int found = 0;
+  const int rc = guard(f->f->err, [&] {
+    P3 X;
+    found = f->f->sensor_pose(frame_id, &X);
+    if (found && pose12) pose_to(X, pose12);
+  });
+  return rc == DYNOHIP_OK ? found : rc;
+}
+
+int dynob_get_object_motions(dynob_formulation* f, uint64_t frame_id, int32_t* ids, double* motions, size_t cap,
+                             size_t* n_out) {
+  if (!f) return DYNOHIP_EINVAL;
+  return guard(f->f->err, [&] {
+    size_t n = 0;
+    const FrameNode* fn = f->f->map->frame(frame_id);
+    if (fn)
+      for (int32_t obj : fn->objects_seen) {
+        P3 H;
+        if (!f->f->object_motion(frame_id, obj, &H)) continue;
+        if (n < cap) {
+          if (ids) ids[n] = obj;
+          if (motions) pose_to(H, motions + 12 * n);
+        }
+        ++n;
+      }
+    if (n_out) *n_out = n;
+  });
+}
+
+int dynob_get_dynamic_landmarks(dynob_formulation* f, uint64_t frame_id, int64_t* tracklets, int32_t* objects,
+                                double* xyz, size_t cap, size_t* n_out) {
+  if (!f) return DYNOHIP_EINVAL;
+  return guard(f->f->err, [&] {
+    const FrameNode* fn = f->f->map->frame(frame_id);
+    DB_CHECK(fn != nullptr, DYNOHIP_ESTATE, "getDynamicLandmarkEstimates: frame not in map");
+    size_t n = 0;
+    for (int32_t obj : fn->objects_seen) {
+      std::vector<int64_t> trk;
+      std::vector<double> p;
+      f->f->dynamic_estimates(frame_id, obj, trk, p);
+      for (size_t i = 0; i < trk.size(); ++i, ++n) {
+        if (n >= cap) continue;
+        if (tracklets) tracklets[n] = trk[i];
+        if (objects) objects[n] = obj;
+        if (xyz) std::memcpy(xyz + 3 * n, &p[3 * i], 3 * sizeof(double));
+      }
+    }
+    if (n_out) *n_out = n;
+  });
+}
+
+int dynob_get_static_landmarks(dynob_formulation* f, uint64_t frame_id, int64_t* tracklets, double* xyz, size_t cap,
+                               size_t* n_out) {
+  if (!f) return DYNOHIP_EINVAL;
+  return guard(f->f->err, [&] {
+    std::vector<int64_t> ids;
+    if (frame_id == UINT64_MAX) {  // getFullStaticMap (Accessor-impl.hpp:194-214)
+      for (const auto& kv : f->f->map->landmarks)
+        if (kv.second.is_static()) ids.push_back(kv.first);
+    } else {  // getStaticLandmarkEstimates (Accessor-impl.hpp:166-192)
+      const FrameNode* fn = f->f->map->frame(frame_id);
+      DB_CHECK(fn != nullptr, DYNOHIP_ESTATE, "getStaticLandmarkEstimates: frame not in map");
+      ids.assign(fn->static_landmarks.begin(), fn->static_landmarks.end());
+    }
+    size_t n = 0;
+    for (int64_t t : ids) {
+      double p[3];
+      if (!f->f->static_landmark(t, p)) continue;
+      if (n < cap) {
+        if (tracklets) tracklets[n] = t;
+        if (xyz) std::memcpy(xyz + 3 * n, p, sizeof(p));
+      }
+      ++n;
+    }
+    if (n_out) *n_out = n;
+  });
+}
+
+int dynob_object_centroid(dynob_formulation* f, uint64_t frame_id, int32_t object_id, double* xyz) {
+  if (!f || !xyz) return DYNOHIP_EINVAL;
+  int found = 0;
+  const int rc = guard(f->f->err, [&] { found = f->f->object_centroid(frame_id, object_id, xyz); });
+  return rc == DYNOHIP_OK ? found : rc;
+}
+
+int dynob_post_update(dynob_formulation* f) {
+  if (!f) return DYNOHIP_EINVAL;
+  return guard(f->f->err, [&] { f->f->post_update(); });
+}
+
+int dynob_get_object_poses(dynob_formulation* f, int32_t* objects, uint64_t* frames, double* poses12, size_t cap,
+                           size_t* n_out) {
+  if (!f) return DYNOHIP_EINVAL;
+  return guard(f->f->err, [&] {
+    std::vector<int32_t> o;
+    std::vector<uint64_t> fr;
+    std::vector<double> p;
+    f->f->object_poses_all(o, fr, p);
+    if (n_out) *n_out = o.size();
+    for (size_t i = 0; i < o.size() && i < cap; ++i) {
+      if (objects) objects[i] = o[i];
+      if (frames) frames[i] = fr[i];
+      if (poses12) std::memcpy(poses12 + 12 * i, &p[12 * i], 12 * sizeof(double));
+    }
+  });
+}
+
+// ------------------------------------------------------------- module ----
+void dynob_module_params_default(dynob_module_params* p) {
+  if (!p) return;
+  std::memset(p, 0, sizeof(*p));
+  p->use_full_batch_opt = 1;  // RGBDBackendModule.cc:54
+  p->full_batch_frame = -1;
+  p->opt_window_size = 10;    // RGBDBackendModule.cc:51-52
+  p->opt_window_overlap = 4;
+  p->optimize = 1;
+  p->device_id = 0;
+  p->post_update = 1;
+  dynohip_lm_params_default(&p->lm);
+}
+
+int dynob_module_create(const dynob_params* p, const dynob_module_params* mp, dynob_module** out) {
+  if (!out || !mp || !params_valid(p)) return DYNOHIP_EINVAL;
+  if (!mp->use_full_batch_opt && (mp->opt_window_size <= 0 || mp->opt_window_overlap < 0)) return DYNOHIP_EINVAL;
+  auto* m = new dynob_module();
+  m->params = *p;
+  m->mp = *mp;
+  m->updater.f = std::make_unique<Formulation>(&m->map.map, *p);
+  dynohip_sliding_window_init(&m->window, mp->opt_window_size, mp->opt_window_overlap);
+  *out = m;
+  return DYNOHIP_OK;
+}
+
+void dynob_module_destroy(dynob_module* m) {
+  if (!m) return;
+  if (m->solver) dynohip_destroy(m->solver);
+  delete m;
+}
+const char* dynob_module_last_error(const dynob_module* m) { return m ? m->err.c_str() : "null module"; }
+
+int dynob_module_spin(dynob_module* m, const dynob_input_packet* in, dynob_spin_result* r) {
+  if (!m || !in) return DYNOHIP_EINVAL;
+  dynob_spin_result local;
+  if (!r) r = &local;
+  std::memset(r, 0, sizeof(*r));
+  return guard(m->err, [&] {
+    const double t0 = now_ms();
+    Formulation& up = *m->updater.f;
+    const uint64_t k = in->frame_id;
+    // RGBDBackendModule::updateMap (RGBDBackendModule.cc:229-244)
+    Map& map = m->map.map;
+    for (size_t i = 0; i < in->n_static; ++i) map.add(in->static_measurements[i]);
+    for (size_t i = 0; i < in->n_dynamic; ++i) map.add(in->dynamic_measurements[i]);
+    // updateSensorPoseMeasurement: CHECK_NOTNULL(frame_node) (Map.hpp:100-105)
+    DB_CHECK(map.frame(k) != nullptr, DYNOHIP_ESTATE, "frame " + std::to_string(k) + " has no measurement");
+    FrameNode& fn = *map.frame(k);
+    fn.has_X = true;
+    fn.X_world = pose_from(in->T_world_camera);
+    fn.has_motions = true;
+    fn.motions_world.clear();
+    for (size_t i = 0; i < in->n_motions; ++i) fn.motions_world[in->motion_object_ids[i]] = pose_from(in->motions12 + 12 * i);
+    const P3 T_k = fn.X_world;
+    Values nv;
+    Graph nf;
+    if (!m->bootstrapped) {
+      // boostrapSpinImpl (RGBDBackendModule.cc:129-152)
+      uint64_t s, e;
+      DB_CHECK(dynohip_sliding_window_check(&m->window, k, &s, &e) == 0, DYNOHIP_ESTATE,
+               "sliding window triggered on the first frame");
+      up.set_initial_pose(k, T_k, nv);
+      up.set_initial_pose_prior(k, T_k, nf);
+      m->bootstrapped = true;
+      return;
+    }
+    // nominalSpinImpl (RGBDBackendModule.cc:154-227)
+    up.add_odometry(k, T_k, nv, nf);
+    up.update_static(k, nv, nf, false);
+    up.update_dynamic(k, nv, nf, false);
+    r->ms_construct = now_ms() - t0;
+    if (m->mp.use_full_batch_opt) {
+      if (dynohip_full_batch_trigger(m->mp.full_batch_frame, k)) {
+        const int rc = solve(m, up, r);
+        DB_CHECK(rc == DYNOHIP_OK, rc, m->err);
+      }
+    } else {
+      uint64_t s = 0, e = 0;
+      if (dynohip_sliding_window_check(&m->window, k, &s, &e) == 1) {
+        const double tc = now_ms();
+        auto window = construct_graph(&map, m->params, s, e, true);
+        r->ms_construct += now_ms() - tc;
+        r->window_start = s;
+        r->window_end = e;
+        const int rc = solve(m, *window, r);
+        DB_CHECK(rc == DYNOHIP_OK, rc, m->err);
+      }
+    }
+    if (m->mp.post_update) up.post_update();
+  });
+}
+
+dynob_map* dynob_module_map(dynob_module* m) { return m ? &m->map : nullptr; }
+dynob_formulation* dynob_module_formulation(dynob_module* m) { return m ? &m->updater : nullptr; }
+
+int dynob_module_last_problem(dynob_module* m, dynohip_graph_view* g, const uint64_t** keys, const uint8_t** kinds,
+                              const double** initial, const double** optimised, size_t* n, size_t* n_doubles) {
+  if (!m) return DYNOHIP_EINVAL;
+  if (g) m->last_graph.view(g);
+  if (keys) *keys = m->last_values.keys.data();
+  if (kinds) *kinds = m->last_values.kinds.data();
+  if (initial) *initial = m->last_values.data.data();
+  if (optimised) *optimised = m->last_optimised.data();
+  if (n) *n = m->last_values.keys.size();
+  if (n_doubles) *n_doubles = m->last_values.data.size();
+  return DYNOHIP_OK;
+}
+
+}  // extern "C"

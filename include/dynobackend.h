@@ -1,0 +1,252 @@
+/*
+ * dynobackend.h — C-ABI of the host-side backend module around the LM call
+ * sites: the graph-construction mirror that
+ * turns frontend output packets into the factor graph the GPU solver
+ * consumes, and the estimate accessors / output packet read back from it.
+ *
+ * It mirrors, with the same names and integer bookkeeping:
+ *   Map / FrameNode / LandmarkNode / ObjectNode
+ *       dynosam/include/dynosam/common/Map.hpp:112-444,
+ *       dynosam/include/dynosam/common/MapNodes.hpp,
+ *       dynosam/include/dynosam/common/MapNodes-inl.hpp:37-262
+ *   Formulation<Map> (theta_, factors_, setInitialPose, setInitialPosePrior,
+ *       addOdometry, updateStaticObservations, updateDynamicObservations,
+ *       updateTheta)  dynosam/include/dynosam/backend/Formulation-impl.hpp:46-584
+ *   WorldMotionFormulation (MotionInWorld, backend_updater_enum 0)
+ *       dynosam/src/backend/rgbd/WorldMotionEstimator.cc:155-316
+ *   WorldPoseFormulation (LLWorld, backend_updater_enum 1)
+ *       dynosam/src/backend/rgbd/WorldPoseEstimator.cc:84-286
+ *   Accessor queries and WorldMotionAccessor::postUpdateCallback (object pose
+ *       propagation)  dynosam/include/dynosam/backend/Accessor-impl.hpp:40-365,
+ *       WorldMotionEstimator.cc:32-152, dynosam/src/common/DynamicObjects.cc:48-190
+ *   RGBDBackendModule spin (bootstrap / nominal, full-batch trigger, sliding
+ *       window constructGraph + LM, updateTheta, constructOutputPacket)
+ *       dynosam/src/backend/RGBDBackendModule.cc:129-411
+ *
+ * The LM solves themselves go through include/dynohip.h (libdynohip.so,
+ * the HIP path); everything declared here is host code and runs without a
+ * GPU unless a module is created with `optimize = 1`.
+ *
+ * Errors: the reference aborts (glog CHECK / LOG(FATAL)) or throws
+ * (DynosamException, gtsam::ValuesKeyAlreadyExists); here every entry point
+ * returns a dynohip_status (< 0 on error) and the message is available via
+ * the handle's *_last_error(). A handle is used from one thread.
+ */
+#ifndef DYNOBACKEND_H_
+#define DYNOBACKEND_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "dynohip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* One tracked landmark measurement (TrackedValueStatus<LandmarkKeypoint>:
+   tracklet, frame, object label, and the 3-D landmark in the camera frame;
+   the 2-D keypoint is not used by the backend). object_id 0 is the
+   background label (static); Map::addOrUpdateMapStructures checks that
+   is_static == (object_id == 0), Map.hpp:381-382. */
+typedef struct {
+  int64_t tracklet_id;
+  int32_t object_id;
+  int32_t reserved;
+  uint64_t frame_id;
+  double landmark[3];
+} dynob_measurement;
+
+/* ------------------------------------------------------------------ */
+/* Map                                                                 */
+/* ------------------------------------------------------------------ */
+typedef struct dynob_map dynob_map;
+
+int dynob_map_create(dynob_map** out);
+void dynob_map_destroy(dynob_map* m);
+const char* dynob_map_last_error(const dynob_map* m);
+
+/* Map::updateObservations (Map.hpp:76-98): throws (here: DYNOHIP_EINVAL)
+   on a second measurement of a tracklet at the same frame
+   (LandmarkNode::add, MapNodes-inl.hpp:163-176). */
+int dynob_map_update_observations(dynob_map* m, const dynob_measurement* meas, size_t n);
+/* Map::updateSensorPoseMeasurement / updateObjectMotionMeasurements
+   (Map.hpp:100-112); the frame must exist. Poses are 12 doubles. */
+int dynob_map_update_sensor_pose(dynob_map* m, uint64_t frame_id, const double* pose12);
+int dynob_map_update_object_motions(dynob_map* m, uint64_t frame_id, const int32_t* object_ids,
+                                    const double* motions12, size_t n);
+
+/* Map queries. Booleans / counts are returned as the value (>= 0); list
+   queries write up to `cap` ids to `out` (ascending, the FastMapNodeSet
+   order) and the full length to *n_out. a / b as listed. */
+enum {
+  DYNOB_Q_FRAME_EXISTS = 1,             /* a = frame                       */
+  DYNOB_Q_LANDMARK_EXISTS = 2,          /* a = tracklet                    */
+  DYNOB_Q_OBJECT_EXISTS = 3,            /* a = object                      */
+  DYNOB_Q_NUM_OBJECTS = 4,
+  DYNOB_Q_OBJECT_OBSERVED = 5,          /* a = frame, b = object           */
+  DYNOB_Q_OBJECT_OBSERVED_IN_PREVIOUS = 6,
+  DYNOB_Q_OBJECT_MOTION_EXPECTED = 7,
+  DYNOB_Q_LANDMARK_NUM_OBS = 8,         /* a = tracklet                    */
+  DYNOB_Q_LANDMARK_OBJECT = 9,          /* a = tracklet                    */
+  DYNOB_Q_FIRST_FRAME = 10,
+  DYNOB_Q_LAST_FRAME = 11,
+  /* lists */
+  DYNOB_Q_FRAME_IDS = 20,
+  DYNOB_Q_OBJECT_IDS = 21,
+  DYNOB_Q_STATIC_TRACKLETS_BY_FRAME = 22,  /* a = frame                    */
+  DYNOB_Q_DYNAMIC_TRACKLETS_BY_FRAME = 23, /* a = frame                    */
+  DYNOB_Q_FRAME_OBJECTS_SEEN = 24,         /* a = frame                    */
+  DYNOB_Q_LANDMARK_SEEN_FRAMES = 25,       /* a = tracklet                 */
+  DYNOB_Q_OBJECT_SEEN_FRAMES = 26,         /* a = object                   */
+  DYNOB_Q_OBJECT_LANDMARKS = 27,           /* a = object                   */
+  DYNOB_Q_OBJECT_LANDMARKS_AT_FRAME = 28   /* a = object, b = frame        */
+};
+int64_t dynob_map_query(const dynob_map* m, int what, int64_t a, int64_t b, int64_t* out, size_t cap,
+                        size_t* n_out);
+
+/* ------------------------------------------------------------------ */
+/* Formulation                                                         */
+/* ------------------------------------------------------------------ */
+enum { DYNOB_MOTION_IN_WORLD = 0, DYNOB_LL_WORLD = 1 };
+
+/* BackendParams + FormulationParams + the backend flags the formulations
+   read (Appendix B of SURVEY.md). dynob_params_default(p, 1) gives the
+   shipped dynosam/params/backend.flags values, (p, 0) the code defaults
+   (BackendParams.cc:26-40). */
+typedef struct {
+  int formulation;               /* DYNOB_MOTION_IN_WORLD / DYNOB_LL_WORLD  */
+  int min_static_observations;   /* 2  (BackendParams.hpp:73)              */
+  int min_dynamic_observations;  /* 3  (BackendParams.hpp:74)              */
+  int use_smoothing_factor;      /* 1  (Types.cc:35)                       */
+  int init_H_with_identity;      /* 1  (RGBDBackendModule.cc:71)           */
+  int use_robust_kernels;        /* 1  (BackendParams.hpp:56)              */
+  double k_huber_3d_points;      /* 1e-4 (BackendParams.hpp:57)            */
+  double static_point_sigma;     /* 0.06                                    */
+  double dynamic_point_sigma;    /* 0.0625                                  */
+  double motion_ternary_sigma;   /* flags 1e-5 / code 0.01                  */
+  double odometry_sigmas[6];     /* [rot x3, trans x3] (BackendModule.cc:65-70) */
+  double smoothing_sigmas[6];    /* (BackendModule.cc:78-83)                */
+  double initial_pose_prior_sigma; /* 1e-4 isotropic (BackendModule.cc:72) */
+} dynob_params;
+
+void dynob_params_default(dynob_params* p, int shipped_flags);
+
+typedef struct dynob_formulation dynob_formulation;
+
+/* A formulation holds a reference to `map` (which must outlive it). */
+int dynob_formulation_create(dynob_map* map, const dynob_params* p, dynob_formulation** out);
+void dynob_formulation_destroy(dynob_formulation* f);
+const char* dynob_formulation_last_error(const dynob_formulation* f);
+
+int dynob_set_initial_pose(dynob_formulation* f, uint64_t frame_id, const double* pose12);
+int dynob_set_initial_pose_prior(dynob_formulation* f, uint64_t frame_id, const double* pose12);
+int dynob_add_odometry(dynob_formulation* f, uint64_t frame_id, const double* pose12);
+int dynob_update_static_observations(dynob_formulation* f, uint64_t frame_id, int do_backtrack);
+int dynob_update_dynamic_observations(dynob_formulation* f, uint64_t frame_id, int do_backtrack);
+/* Formulation::updateTheta: theta_.insert_or_assign(values) */
+int dynob_update_theta(dynob_formulation* f, const uint64_t* keys, const uint8_t* kinds, const double* data,
+                       size_t n);
+
+/* factors_ as a graph view (grouped by type, insertion order within a type)
+   and theta_ in key order (the gtsam::Values order). The pointers stay
+   valid until the next mutating call on the formulation. */
+int dynob_formulation_graph(dynob_formulation* f, dynohip_graph_view* g);
+int dynob_formulation_values(dynob_formulation* f, const uint64_t** keys, const uint8_t** kinds,
+                             const double** data, size_t* n, size_t* n_doubles);
+/* Global insertion order of factors_: per factor its type (the index of
+   its block in dynohip_graph_view) */
+int dynob_formulation_factor_types(dynob_formulation* f, uint8_t* types, size_t cap, size_t* n_out);
+
+/* ---- Accessor (theta queries, Accessor-impl.hpp) -------------------- */
+/* getSensorPose: 1 and the pose if X(frame) is in theta, 0 if not */
+int dynob_get_sensor_pose(dynob_formulation* f, uint64_t frame_id, double* pose12);
+/* getObjectMotions(frame): objects seen at frame with a motion estimate */
+int dynob_get_object_motions(dynob_formulation* f, uint64_t frame_id, int32_t* object_ids, double* motions12,
+                             size_t cap, size_t* n_out);
+/* getDynamicLandmarkEstimates(frame) (objects in id order, landmarks in
+   tracklet order); getStaticLandmarkEstimates(frame), or the full static
+   map (getFullStaticMap) when frame_id == UINT64_MAX */
+int dynob_get_dynamic_landmarks(dynob_formulation* f, uint64_t frame_id, int64_t* tracklets, int32_t* objects,
+                                double* xyz, size_t cap, size_t* n_out);
+int dynob_get_static_landmarks(dynob_formulation* f, uint64_t frame_id, int64_t* tracklets, double* xyz,
+                               size_t cap, size_t* n_out);
+/* Accessor::computeObjectCentroid (PCL CentroidPoint semantics: FP32
+   accumulation in landmark order). Returns 1 and the centroid, 0 if the
+   object has no landmark estimate at the frame. */
+int dynob_object_centroid(dynob_formulation* f, uint64_t frame_id, int32_t object_id, double* xyz);
+/* Accessor::postUpdateCallback: WorldMotion propagates object poses through
+   the motions from the first frame (WorldMotionEstimator.cc:68-152,
+   DynamicObjects.cc:48-190); LLWorld reads them from theta. */
+int dynob_post_update(dynob_formulation* f);
+/* getObjectPoses(): every (object, frame, pose) in object then frame order */
+int dynob_get_object_poses(dynob_formulation* f, int32_t* objects, uint64_t* frames, double* poses12, size_t cap,
+                           size_t* n_out);
+
+/* ------------------------------------------------------------------ */
+/* RGBDBackendModule                                                   */
+/* ------------------------------------------------------------------ */
+/* RGBDInstanceOutputPacket as the backend reads it (RGBDBackendModule.cc:
+   306-320): frontend camera pose, static / dynamic landmark measurements and
+   the frontend object motion estimates. */
+typedef struct {
+  uint64_t frame_id;
+  double timestamp;
+  double T_world_camera[12];
+  const dynob_measurement* static_measurements;
+  size_t n_static;
+  const dynob_measurement* dynamic_measurements;
+  size_t n_dynamic;
+  const int32_t* motion_object_ids;
+  const double* motions12;
+  size_t n_motions;
+} dynob_input_packet;
+
+typedef struct {
+  int use_full_batch_opt;   /* FLAGS_use_full_batch_opt (code 1, flags 0)  */
+  int64_t full_batch_frame; /* BackendParams::full_batch_frame             */
+  int opt_window_size;      /* FLAGS_opt_window_size 10                    */
+  int opt_window_overlap;   /* FLAGS_opt_window_overlap 4                  */
+  int optimize;             /* 1: run LM on the GPU (libdynohip); 0: build
+                               graphs only (host, for tests)               */
+  int device_id;
+  int post_update;          /* 1: postUpdateCallback every spin (as the
+                               reference); 0: skip                          */
+  int reserved;
+  dynohip_lm_params lm;     /* default-constructed LevenbergMarquardtParams */
+} dynob_module_params;
+
+void dynob_module_params_default(dynob_module_params* p);
+
+typedef struct {
+  int optimized;            /* an LM solve ran in this spin                 */
+  int iterations, inner_iterations;
+  int reserved;
+  uint64_t window_start, window_end;  /* sliding window range if optimized */
+  double error_before, error_after;   /* graph.error before / after        */
+  double ms_construct, ms_optimize;   /* host wall time of graph
+                                         construction / LM (incl. upload)  */
+} dynob_spin_result;
+
+typedef struct dynob_module dynob_module;
+
+int dynob_module_create(const dynob_params* p, const dynob_module_params* mp, dynob_module** out);
+void dynob_module_destroy(dynob_module* m);
+const char* dynob_module_last_error(const dynob_module* m);
+/* ModuleBase::spinOnce: the first packet bootstraps, later ones run
+   nominalSpinImpl. */
+int dynob_module_spin(dynob_module* m, const dynob_input_packet* in, dynob_spin_result* out);
+/* The module's map and its persistent formulation (new_updater_) */
+dynob_map* dynob_module_map(dynob_module* m);
+dynob_formulation* dynob_module_formulation(dynob_module* m);
+/* The last solved problem (full batch: theta/factors; sliding window: the
+   constructGraph output) before the solve: graph + initial values, and the
+   optimised values, valid until the next spin. */
+int dynob_module_last_problem(dynob_module* m, dynohip_graph_view* g, const uint64_t** keys, const uint8_t** kinds,
+                              const double** initial, const double** optimised, size_t* n, size_t* n_doubles);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DYNOBACKEND_H_ */

@@ -56,3 +56,19 @@ def test_no_device_create_fails_cleanly():
     lib = _native.load("libdynohip.so")
     h = C.c_void_p()
     assert lib.dynohip_create(0, C.byref(h)) != 0
+
+
+def test_dynobackend_exports_every_declared_symbol():
+    lib = C.CDLL(_native.lib_path("libdynohip.so"))
+    names = declared("dynobackend.h", "dynob_")
+    assert len(names) > 30
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_backend_struct_sizes():
+    assert C.sizeof(_abi.Measurement) == 8 + 4 + 4 + 8 + 24
+    assert C.sizeof(_abi.BackendParams) == 6 * 4 + 4 * 8 + 12 * 8 + 8
+    assert C.sizeof(_abi.InputPacket) == 8 + 8 + 96 + 8 * 7
+    assert C.sizeof(_abi.ModuleParams) == 4 + 4 + 8 + 4 * 6 + C.sizeof(_abi.LMParams)
+    assert C.sizeof(_abi.SpinResult) == 4 * 4 + 8 * 6
