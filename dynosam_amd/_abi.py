@@ -247,3 +247,17 @@ class SpinResult(C.Structure):
         ("ms_construct", C.c_double),
         ("ms_optimize", C.c_double),
     ]
+
+
+class GroundTruth(C.Structure):
+    """dynob_ground_truth"""
+    _fields_ = [
+        ("n_frames", C.c_size_t),
+        ("frame_ids", C.POINTER(C.c_uint64)),
+        ("X_world12", C.POINTER(C.c_double)),
+        ("n_objects", C.c_size_t),
+        ("object_frame_ids", C.POINTER(C.c_uint64)),
+        ("object_ids", C.POINTER(C.c_int32)),
+        ("L_world12", C.POINTER(C.c_double)),
+        ("prev_H_current_world12", C.POINTER(C.c_double)),
+    ]

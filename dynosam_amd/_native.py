@@ -146,6 +146,8 @@ def _declare(name, lib):
             ("dynob_object_centroid", [vp_, C.c_uint64, C.c_int32, D], C.c_int),
             ("dynob_post_update", [vp_], C.c_int),
             ("dynob_get_object_poses", [vp_, I32_, U64, D, C.c_size_t, SZ], C.c_int),
+            ("dynob_log_backend_from_map", [vp_, C.c_char_p, C.c_char_p, C.c_int, C.c_int64, P(_abi.GroundTruth)],
+             C.c_int),
             ("dynob_module_params_default", [P(_abi.ModuleParams)], None),
             ("dynob_module_create", [P(_abi.BackendParams), P(_abi.ModuleParams), P(vp_)], C.c_int),
             ("dynob_module_destroy", [vp_], None),

@@ -282,6 +282,37 @@ class Formulation:
     def postUpdateCallback(self):
         self._check(self._lib.dynob_post_update(self._h))
 
+    def logBackendFromMap(self, output_dir, module_name=None, use_full_batch_opt=False, full_batch_frame=-1,
+                          ground_truth=None):
+        """Formulation::logBackendFromMap (Formulation-impl.hpp:586-644):
+        writes the reference's backend CSV logs into `output_dir`.
+        ground_truth: None or dict(X={frame: pose12}, objects={(frame, object): (L12, H12)})."""
+        gt_ptr = None
+        keep = []
+        if ground_truth is not None:
+            g = _abi.GroundTruth()
+            fr = np.array(sorted(ground_truth.get("X", {})), dtype=np.uint64)
+            X = np.ascontiguousarray([np.asarray(ground_truth["X"][int(f)], float).reshape(12) for f in fr],
+                                     dtype=np.float64).reshape(-1)
+            ok = sorted(ground_truth.get("objects", {}))
+            of = np.array([k[0] for k in ok], dtype=np.uint64)
+            oo = np.array([k[1] for k in ok], dtype=np.int32)
+            Lw = np.ascontiguousarray([np.asarray(ground_truth["objects"][k][0], float).reshape(12) for k in ok],
+                                      dtype=np.float64).reshape(-1)
+            Hw = np.ascontiguousarray([np.asarray(ground_truth["objects"][k][1], float).reshape(12) for k in ok],
+                                      dtype=np.float64).reshape(-1)
+            keep = [fr, X, of, oo, Lw, Hw]
+            g.n_frames, g.frame_ids, g.X_world12 = fr.shape[0], fr.ctypes.data_as(C.POINTER(C.c_uint64)), _dp(X)
+            g.n_objects = len(ok)
+            g.object_frame_ids = of.ctypes.data_as(C.POINTER(C.c_uint64))
+            g.object_ids = oo.ctypes.data_as(C.POINTER(C.c_int32))
+            g.L_world12, g.prev_H_current_world12 = _dp(Lw), _dp(Hw)
+            gt_ptr = C.byref(g)
+        self._check(self._lib.dynob_log_backend_from_map(
+            self._h, str(output_dir).encode(), (module_name or "").encode(), int(use_full_batch_opt),
+            full_batch_frame, gt_ptr))
+        del keep
+
     def getObjectPoses(self):
         """ObjectPoseMap: {object: {frame: pose12}}"""
         n = C.c_size_t()

@@ -183,6 +183,35 @@ int dynob_post_update(dynob_formulation* f);
 int dynob_get_object_poses(dynob_formulation* f, int32_t* objects, uint64_t* frames, double* poses12, size_t cap,
                            size_t* n_out);
 
+/* ---- BackendLogger / Formulation::logBackendFromMap ----------------- */
+/* Ground truth for the logs (GroundTruthInputPacket: X_world_ per frame,
+   ObjectPoseGT::L_world_ and prev_H_current_world_ per (frame, object)).
+   Any array may be null when its count is 0. */
+typedef struct {
+  size_t n_frames;
+  const uint64_t* frame_ids;
+  const double* X_world12;
+  size_t n_objects;
+  const uint64_t* object_frame_ids;
+  const int32_t* object_ids;
+  const double* L_world12;
+  const double* prev_H_current_world12;
+} dynob_ground_truth;
+
+/* Formulation::logBackendFromMap (Formulation-impl.hpp:586-644) through
+   EstimationModuleLogger (dynosam/src/logger/Logger.cc:139-360): writes
+   <module>_camera_pose_log.csv, _object_pose_log.csv, _object_motion_log.csv,
+   _map_points_log.csv, _object_bbx_log.csv (header only) and
+   frame_id_timestamp.csv (header only) into `output_dir`, with the
+   reference's columns, quaternions (Eigen's rotation-matrix conversion) and
+   number formatting (default ostream precision). module_name null or empty:
+   the formulation's logger prefix ("rgbd_motion_world" /
+   "rgbd_LL_world_identity"). gt may be null (identity ground truth). Call
+   dynob_post_update first for the object poses, as the reference's
+   destructor does (RGBDBackendModule.cc:118-127). */
+int dynob_log_backend_from_map(dynob_formulation* f, const char* output_dir, const char* module_name,
+                               int use_full_batch_opt, int64_t full_batch_frame, const dynob_ground_truth* gt);
+
 /* ------------------------------------------------------------------ */
 /* RGBDBackendModule                                                   */
 /* ------------------------------------------------------------------ */

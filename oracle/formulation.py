@@ -391,3 +391,42 @@ def run_stream(packets, full_batch=True, window=10, overlap=4, **kw):
             if cond:
                 windows.append((s, e, construct_graph(mp, s, e, kw)))
     return main, windows
+
+
+def eigen_quaternion(R):
+    """Eigen::Quaternion(Matrix3) (quaternionbase_assign_impl), as
+    gtsam::Rot3::toQuaternion returns it; (x, y, z, w)."""
+    m = np.asarray(R, float).reshape(3, 3)
+    t = m[0, 0] + m[1, 1] + m[2, 2]
+    if t > 0.0:
+        t = np.sqrt(t + 1.0)
+        w = 0.5 * t
+        t = 0.5 / t
+        return ((m[2, 1] - m[1, 2]) * t, (m[0, 2] - m[2, 0]) * t, (m[1, 0] - m[0, 1]) * t, w)
+    i = 0
+    if m[1, 1] > m[0, 0]:
+        i = 1
+    if m[2, 2] > m[i, i]:
+        i = 2
+    j, k = (i + 1) % 3, (i + 2) % 3
+    c = [0.0, 0.0, 0.0]
+    t = np.sqrt(m[i, i] - m[j, j] - m[k, k] + 1.0)
+    c[i] = 0.5 * t
+    t = 0.5 / t
+    w = (m[k, j] - m[j, k]) * t
+    c[j] = (m[j, i] + m[i, j]) * t
+    c[k] = (m[k, i] + m[i, k]) * t
+    return (c[0], c[1], c[2], w)
+
+
+def csv_field(v):
+    """One value streamed into a default-formatted std::stringstream
+    (CsvWriter::add, utils/CsvParser.hpp:279-289)."""
+    if isinstance(v, (int, np.integer)):
+        return str(int(v))
+    return "%g" % float(v)
+
+
+def pose_fields(p12, gt12):
+    q, g = eigen_quaternion(p12[:9]), eigen_quaternion(gt12[:9])
+    return list(p12[9:12]) + list(q) + list(gt12[9:12]) + list(g)

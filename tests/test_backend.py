@@ -419,3 +419,79 @@ def test_module_llworld_full_batch_gpu(gpu_available):
     assert r["optimized"] == 1
     assert r["error_before"] == pytest.approx(s.initial_error, rel=1e-9)
     assert r["error_after"] == pytest.approx(s.final_error, rel=1e-4, abs=1e-6)
+
+
+def _read_csv(path):
+    lines = open(path).read().split("\n")
+    return lines[0].split(","), [ln.split(",") for ln in lines[1:] if ln]
+
+
+@pytest.mark.parametrize("with_gt", [False, True])
+def test_backend_csv_logs(tmp_path, with_gt):
+    """logBackendFromMap through EstimationModuleLogger: file set, columns,
+    rows and formatting against the restated CsvWriter / Eigen quaternion."""
+    packets, gt = stream.generate(STREAMS["basic"])
+    m = backend.RGBDBackendModule(full_batch_frame=len(packets), optimize=False)
+    for p in packets:
+        m.spinOnce(p)
+    f = m.formulation
+    f.postUpdateCallback()
+    I12 = ofm.p12_of(np.eye(4))
+    gtd = None
+    if with_gt:
+        gtd = dict(X={k: stream.pose12(gt["X"][k]) for k in range(len(packets))}, objects={})
+        for o, Ls in gt["L"].items():
+            for k in range(1, len(packets)):
+                gtd["objects"][(k, o)] = (stream.pose12(Ls[k]), stream.pose12(Ls[k] @ stream.inv(Ls[k - 1])))
+    f.logBackendFromMap(tmp_path, ground_truth=gtd)
+    name = "rgbd_motion_world"
+    files = sorted(os.listdir(tmp_path))
+    assert files == sorted([f"{name}_object_pose_log.csv", f"{name}_object_bbx_log.csv",
+                            f"{name}_object_motion_log.csv", f"{name}_camera_pose_log.csv",
+                            f"{name}_map_points_log.csv", "frame_id_timestamp.csv"])
+    hdr, rows = _read_csv(tmp_path / f"{name}_camera_pose_log.csv")
+    assert hdr == ["frame_id", "tx", "ty", "tz", "qx", "qy", "qz", "qw", "gt_tx", "gt_ty", "gt_tz", "gt_qx",
+                   "gt_qy", "gt_qz", "gt_qw"]
+    assert len(rows) == len(packets)
+    for k, row in enumerate(rows):
+        g12 = gtd["X"][k] if with_gt else I12
+        assert row == [ofm.csv_field(k)] + [ofm.csv_field(x) for x in ofm.pose_fields(f.getSensorPose(k), g12)]
+    hdr, rows = _read_csv(tmp_path / f"{name}_object_motion_log.csv")
+    exp = []
+    for k in range(len(packets)):
+        for o, H in f.getObjectMotions(k).items():
+            g12 = gtd["objects"][(k, o)][1] if with_gt else I12
+            exp.append([ofm.csv_field(k), ofm.csv_field(o)] + [ofm.csv_field(x) for x in ofm.pose_fields(H, g12)])
+    assert rows == exp and len(exp) > 10
+    hdr, rows = _read_csv(tmp_path / f"{name}_object_pose_log.csv")
+    poses = f.getObjectPoses()
+    exp = []
+    for k in range(len(packets)):
+        for o in sorted(poses):
+            if k in poses[o]:
+                g12 = gtd["objects"][(k, o)][0] if with_gt else I12
+                exp.append([ofm.csv_field(k), ofm.csv_field(o)] +
+                           [ofm.csv_field(x) for x in ofm.pose_fields(poses[o][k], g12)])
+    assert rows == exp and len(exp) > 10
+    hdr, rows = _read_csv(tmp_path / f"{name}_map_points_log.csv")
+    assert hdr == ["frame_id", "object_id", "tracklet_id", "x_world", "y_world", "z_world"]
+    exp = []
+    for k in range(len(packets)):
+        st_trk, st_xyz = f.getStaticLandmarkEstimates(k)
+        exp += [[str(k), "0", str(t)] + [ofm.csv_field(x) for x in p] for t, p in zip(st_trk, st_xyz)]
+        trk, obj, xyz = f.getDynamicLandmarkEstimates(k)
+        exp += [[str(k), str(o), str(t)] + [ofm.csv_field(x) for x in p] for t, o, p in zip(trk, obj, xyz)]
+    assert rows == exp
+    _, rows = _read_csv(tmp_path / f"{name}_object_bbx_log.csv")
+    assert rows == []
+
+
+def test_eigen_quaternion_restatement_branches():
+    # all four branches of the conversion reproduce R
+    for xi in ([0.1, 0.2, 0.3, 0, 0, 0], [3.0, 0.1, 0.0, 0, 0, 0], [0.0, 3.0, 0.1, 0, 0, 0], [0.1, 0.0, 3.0, 0, 0, 0]):
+        R = stream.expmap(xi)[:3, :3]
+        x, y, z, w = ofm.eigen_quaternion(R)
+        Rq = np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                       [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                       [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+        np.testing.assert_allclose(Rq, R, atol=1e-12)
