@@ -47,9 +47,12 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default=None, help="C2 (windows mode default) / C5 (partitioned default) / ...")
-    ap.add_argument("--mode", default="windows", choices=("windows", "partitioned"),
+    ap.add_argument("--mode", default="windows", choices=("windows", "partitioned", "stream"),
                     help="windows: one independent graph per rank (weak scaling); partitioned: one graph split "
-                         "over the ranks (strong scaling)")
+                         "over the ranks (strong scaling); stream: the backend module replays a synthetic "
+                         "frontend stream per rank (graph construction + sliding-window LM, weak scaling)")
+    ap.add_argument("--full-batch", action="store_true", help="stream mode: one full-batch solve at the last frame "
+                                                             "instead of the sliding window (shipped flags)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample (s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -86,6 +89,85 @@ def cpu_baseline(graph, values, seconds):
     }
 
 
+def stream_main(args, world, rank, local_rank, dist):
+    """--mode stream: RGBDBackendModule (dynosam_amd.backend) replays a
+    synthetic frontend stream of the config's shape — per frame Map update +
+    Formulation update, and either the sliding window (shipped
+    backend.flags: window 10 / overlap 4, constructGraph + LM per trigger)
+    or one full-batch solve at the last frame. One step = one replay of the
+    whole stream through a fresh module; value = LM iterations of all
+    solves on all ranks / wall time (host graph construction, plan build and
+    value upload are inside the timed region: this is the drop-in module's
+    end-to-end rate)."""
+    import torch
+    from dynosam_amd import backend, stream, synth
+
+    c = synth.CONFIGS[args.config]
+    cfg = stream.StreamConfig(frames=c["frames"], objects=c["objects"], static_landmarks=c["static_landmarks"],
+                              dyn_slots=c["dyn_slots"], object_visible_frames=c.get("object_visible_frames", 0),
+                              seed=42 + rank)
+    packets, _ = stream.generate(cfg)
+
+    def replay():
+        m = backend.RGBDBackendModule(use_full_batch_opt=args.full_batch, full_batch_frame=len(packets),
+                                      optimize=True, device_id=local_rank, post_update=False)
+        it = inner = solves = 0
+        ms_c = ms_o = 0.0
+        for p in packets:
+            r = m.spinOnce(p)
+            ms_c += r["ms_construct"]
+            if r["optimized"]:
+                it += r["iterations"]
+                inner += r["inner_iterations"]
+                solves += 1
+                ms_o += r["ms_optimize"]
+        return it, inner, solves, ms_c, ms_o
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        replay()
+    barrier()
+    t0 = time.perf_counter()
+    iters = inner = solves = 0
+    ms_c = ms_o = 0.0
+    for _ in range(args.steps):
+        a, b, n, c1, c2 = replay()
+        iters, inner, solves, ms_c, ms_o = iters + a, inner + b, solves + n, ms_c + c1, ms_o + c2
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        cnt = torch.tensor([iters, inner, solves], dtype=torch.float64, device="cuda")
+        dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
+        iters, inner, solves = (int(x) for x in cnt.tolist())
+    if rank == 0:
+        out = {
+            "metric": "LM iterations/sec + ms/iter, full-batch dynamic factor graph",
+            "value": iters / dt, "unit": "LM iterations/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": 1e3 * dt / args.steps,
+            "ms_per_iter": 1e3 * dt * world / max(iters, 1), "ms_per_inner_iter": 1e3 * dt * world / max(inner, 1),
+            "lm_iterations_per_step": iters / (args.steps * world), "solves_per_step": solves / (args.steps * world),
+            "ms_per_frame_construction": ms_c / (args.steps * len(packets)),
+            "ms_per_solve_incl_upload": ms_o / max(solves / world, 1),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic frontend stream (dynosam_amd.stream, seed 42 + rank)",
+            "config": {"workload": f"{args.config}-shaped stream through RGBDBackendModule, "
+                                   + ("full batch at the last frame" if args.full_batch else
+                                      "sliding window 10 / overlap 4 (backend.flags)"),
+                       "frames": cfg.frames, "objects": cfg.objects,
+                       "parallelism": f"stream-sharded x{world} (one module per rank, no data-path collective)"},
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     if args.config is None:
@@ -101,6 +183,8 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
         dist.init_process_group(backend="nccl")
+    if args.mode == "stream":
+        return stream_main(args, world, rank, local_rank, dist)
     from dynosam_amd import synth
     from dynosam_amd.optimizer import Solver
 

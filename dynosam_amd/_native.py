@@ -148,6 +148,13 @@ def _declare(name, lib):
             ("dynob_get_object_poses", [vp_, I32_, U64, D, C.c_size_t, SZ], C.c_int),
             ("dynob_log_backend_from_map", [vp_, C.c_char_p, C.c_char_p, C.c_int, C.c_int64, P(_abi.GroundTruth)],
              C.c_int),
+            ("dynob_replay_open", [C.c_char_p, P(vp_)], C.c_int),
+            ("dynob_replay_parse", [P(C.c_uint8), C.c_size_t, P(vp_)], C.c_int),
+            ("dynob_replay_destroy", [vp_], None),
+            ("dynob_replay_last_error", [vp_], C.c_char_p),
+            ("dynob_replay_num_packets", [vp_], C.c_size_t),
+            ("dynob_replay_packet", [vp_, C.c_size_t, P(_abi.InputPacket)], C.c_int),
+            ("dynob_replay_ground_truth", [vp_, C.c_size_t, D, I32_, D, D, C.c_size_t, SZ], C.c_int),
             ("dynob_module_params_default", [P(_abi.ModuleParams)], None),
             ("dynob_module_create", [P(_abi.BackendParams), P(_abi.ModuleParams), P(vp_)], C.c_int),
             ("dynob_module_destroy", [vp_], None),

@@ -239,6 +239,19 @@ extern "C" int dynohip_plan_export(const dynohip_graph_view* g, const uint64_t* 
   else if (nm == "sep_slot_ranges") vec(P.sep_slot_ranges);
   else if (nm == "sep_tile_ranges") vec(P.sep_tile_ranges);
   else if (nm == "red_a") vec(P.red_A);
+  else if (nm.size() > 6 && nm.compare(nm.size() - 6, 6, "_start") == 0) {  // gather lists, e.g. "gRed_start"
+    const std::string gl = nm.substr(0, nm.size() - 6);
+    const GatherList* G = gl == "gD" ? &P.gD : gl == "gE" ? &P.gE : gl == "gGp" ? &P.gGp : gl == "gW" ? &P.gW
+                        : gl == "gRed" ? &P.gRed : gl == "gGred" ? &P.gGred : nullptr;
+    if (!G) return DYNOHIP_EINVAL;
+    raw(G->start.data(), G->start.size() * sizeof(int64_t));
+  } else if (nm.size() > 4 && nm.compare(nm.size() - 4, 4, "_ent") == 0) {
+    const std::string gl = nm.substr(0, nm.size() - 4);
+    const GatherList* G = gl == "gD" ? &P.gD : gl == "gE" ? &P.gE : gl == "gGp" ? &P.gGp : gl == "gW" ? &P.gW
+                        : gl == "gRed" ? &P.gRed : gl == "gGred" ? &P.gGred : nullptr;
+    if (!G) return DYNOHIP_EINVAL;
+    raw(G->ent.data(), G->ent.size() * sizeof(GEntry));
+  }
   else if (nm == "red_b") vec(P.red_B);
   else if (nm == "value_owner") vec(part.value_owner);
   else if (nm == "damp_row") {

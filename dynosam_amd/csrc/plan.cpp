@@ -1,3 +1,6 @@
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 // plan.cpp — factor graph -> device layout / gather lists (see plan.hpp).
 #include "plan.hpp"
 
@@ -5,6 +8,7 @@
 #include <cmath>
 #include <cstring>
 #include <numeric>
+#include <thread>
 #include <unordered_map>
 
 namespace dynohip {
@@ -46,6 +50,64 @@ uint32_t b_off(const TypePlan& tp, int type, int i) {
 }
 
 // build a CSR gather list from (target, entry) pairs, stable in generation order
+constexpr int pose_slots(int t) {
+  int n = 0;
+  for (int s = 0; s < 4; ++s) n += kSlotKind[t][s] == 0;
+  return n;
+}
+constexpr int kNPoseSlots[kNTypes] = {pose_slots(0), pose_slots(1), pose_slots(2), pose_slots(3), pose_slots(4),
+                                      pose_slots(5)};
+
+// open-addressing key -> index table (linear probing, power-of-two size);
+// replaces std::unordered_map on the hot key lookups of planning
+class KeyIndex {
+ public:
+  explicit KeyIndex(size_t n) {
+    size_t cap = 16;
+    while (cap < 2 * n + 1) cap <<= 1;
+    mask_ = cap - 1;
+    keys_.assign(cap, 0);
+    vals_.assign(cap, -1);
+  }
+  // false if the key is already present
+  bool insert(uint64_t key, int32_t v) {
+    size_t h = hash(key);
+    while (vals_[h] >= 0) {
+      if (keys_[h] == key) return false;
+      h = (h + 1) & mask_;
+    }
+    keys_[h] = key;
+    vals_[h] = v;
+    return true;
+  }
+  int32_t find(uint64_t key) const {
+    size_t h = hash(key);
+    while (vals_[h] >= 0) {
+      if (keys_[h] == key) return vals_[h];
+      h = (h + 1) & mask_;
+    }
+    return -1;
+  }
+
+ private:
+  size_t hash(uint64_t k) const { return static_cast<size_t>((k * 0x9E3779B97F4A7C15ull) >> 17) & mask_; }
+  size_t mask_;
+  std::vector<uint64_t> keys_;
+  std::vector<int32_t> vals_;
+};
+
+// CSR by counting: ntargets lists; `emit(fn)` enumerates (target, entry)
+// in list order, and is called twice (count, fill)
+template <typename Emit>
+void csr_two_pass(size_t ntargets, Emit&& emit, GatherList& out) {
+  out.start.assign(ntargets + 1, 0);
+  emit([&](int32_t t, const GEntry&) { out.start[t + 1]++; });
+  for (size_t t = 0; t < ntargets; ++t) out.start[t + 1] += out.start[t];
+  out.ent.resize(out.start[ntargets]);
+  std::vector<int64_t> cur(out.start.begin(), out.start.end() - 1);
+  emit([&](int32_t t, const GEntry& e) { out.ent[cur[t]++] = e; });
+}
+
 void to_csr(size_t ntargets, std::vector<std::pair<int32_t, GEntry>>& pairs, GatherList& out) {
   out.start.assign(ntargets + 1, 0);
   for (auto& p : pairs) out.start[p.first + 1]++;
@@ -59,17 +121,27 @@ void to_csr(size_t ntargets, std::vector<std::pair<int32_t, GEntry>>& pairs, Gat
 
 }  // namespace
 
+static double plan_now() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+static void plan_mark(const char* what, double& t) {
+  static const bool on = std::getenv("DYNOHIP_PLAN_TIMING") != nullptr;
+  const double n = plan_now();
+  if (on) std::fprintf(stderr, "[plan] %-28s %8.2f ms\n", what, n - t);
+  t = n;
+}
+
 int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t* kind, size_t n, Plan& P,
                std::string& err, int nranks, int rank, bool with_schedule) {
+  double tmark = plan_now();
   P = Plan();
   P.nranks = nranks;
   P.rank = rank;
   // ---- values: key lookup ----
-  std::unordered_map<uint64_t, int32_t> key_to_user;
-  key_to_user.reserve(n * 2 + 1);
+  KeyIndex key_to_user(n);
   for (size_t i = 0; i < n; ++i) {
     if (kind[i] > 1) { err = "bad value kind"; return DYNOHIP_EINVAL; }
-    if (!key_to_user.emplace(keys[i], static_cast<int32_t>(i)).second) { err = "duplicate value key"; return DYNOHIP_EINVAL; }
+    if (!key_to_user.insert(keys[i], static_cast<int32_t>(i))) { err = "duplicate value key"; return DYNOHIP_EINVAL; }
   }
   P.user_kind.assign(kind, kind + n);
   P.user_idx.assign(n, -1);
@@ -89,18 +161,18 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
     for (size_t i = 0; i < b->n; ++i)
       for (int s = 0; s < kNKeys[t]; ++s) {
         const uint64_t key = b->keys[i * kNKeys[t] + s];
-        auto it = key_to_user.find(key);
-        if (it == key_to_user.end()) {
+        const int32_t u = key_to_user.find(key);
+        if (u < 0) {
           err = "factor type " + std::to_string(t) + " #" + std::to_string(i) + ": key " + std::to_string(key) +
                 " does not exist in the values";
           return DYNOHIP_EKEY;
         }
         const int want = kSlotKind[t][s] == 0 ? DYNOHIP_POSE3 : DYNOHIP_POINT3;
-        if (kind[it->second] != want) {
+        if (kind[u] != want) {
           err = "factor type " + std::to_string(t) + " #" + std::to_string(i) + ": key has wrong value kind";
           return DYNOHIP_EINVAL;
         }
-        fuser[t][i * kNKeys[t] + s] = it->second;
+        fuser[t][i * kNKeys[t] + s] = u;
       }
     for (size_t i = 0; i < b->n * kDim[t]; ++i)
       if (!(b->sigmas[i] > 0.0) || !std::isfinite(b->sigmas[i])) { err = "non-positive sigma"; return DYNOHIP_EINVAL; }
@@ -108,6 +180,7 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
       if (!std::isfinite(b->measured[i])) { err = "non-finite measurement"; return DYNOHIP_ENONFINITE; }
   }
 
+  plan_mark("before poses: frame order", tmark);
   // ---- poses: frame order ----
   {
     std::vector<PoseSortKey> ps;
@@ -127,6 +200,7 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
     }
   }
 
+  plan_mark("before point chains", tmark);
   // ---- point chains ----
   // adjacency between points from factors with two point slots
   std::vector<std::vector<int32_t>> adj(n);
@@ -203,6 +277,7 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
   for (int c = 0; c < P.n_comp; ++c)
     for (int32_t i = P.comp_start[c]; i < P.comp_start[c + 1]; ++i) comp_of[i] = c;
 
+  plan_mark("before factor types: indices, measurements, arena records", tmark);
   // ---- factor types: indices, measurements, arena records ----
   uint64_t arena = 0;
   for (int t = 0; t < kNTypes; ++t) {
@@ -222,30 +297,46 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
       for (size_t i = 0; i < b->n; ++i) tp.hk[i] = b->huber_k[i];
   }
 
+  plan_mark("before point-pose edges", tmark);
   // ---- point-pose edges ----
   {
-    std::vector<std::pair<int32_t, int32_t>> ep;
-    for (int t = 0; t < kNTypes; ++t) {
-      const TypePlan& tp = P.types[t];
-      const int nk = kNKeys[t];
-      for (int i = 0; i < tp.n; ++i)
-        for (int sa = 0; sa < nk; ++sa)
-          if (kSlotKind[t][sa] == 1)
-            for (int sb = 0; sb < nk; ++sb)
-              if (kSlotKind[t][sb] == 0) ep.emplace_back(tp.idx[i * nk + sa], tp.idx[i * nk + sb]);
+    // bucket (point, pose) incidences by point, then sort + unique each
+    // point's (short) pose list: the (point, pose)-sorted unique edge list
+    std::vector<int32_t> cnt(P.n_pt + 1, 0);
+    auto each = [&](auto&& fn) {
+      for (int t = 0; t < kNTypes; ++t) {
+        const TypePlan& tp = P.types[t];
+        const int nk = kNKeys[t];
+        for (int i = 0; i < tp.n; ++i)
+          for (int sa = 0; sa < nk; ++sa)
+            if (kSlotKind[t][sa] == 1)
+              for (int sb = 0; sb < nk; ++sb)
+                if (kSlotKind[t][sb] == 0) fn(tp.idx[i * nk + sa], tp.idx[i * nk + sb]);
+      }
+    };
+    each([&](int32_t pt, int32_t) { cnt[pt + 1]++; });
+    for (int i = 0; i < P.n_pt; ++i) cnt[i + 1] += cnt[i];
+    std::vector<int32_t> poses(cnt[P.n_pt]);
+    {
+      std::vector<int32_t> cur(cnt.begin(), cnt.end() - 1);
+      each([&](int32_t pt, int32_t pose) { poses[cur[pt]++] = pose; });
     }
-    std::sort(ep.begin(), ep.end());
-    ep.erase(std::unique(ep.begin(), ep.end()), ep.end());
-    P.n_edge = static_cast<int>(ep.size());
-    P.edge_pt.resize(ep.size());
-    P.edge_pose.resize(ep.size());
     P.pt_edge_start.assign(P.n_pt + 1, 0);
-    for (size_t e = 0; e < ep.size(); ++e) {
-      P.edge_pt[e] = ep[e].first;
-      P.edge_pose[e] = ep[e].second;
-      P.pt_edge_start[ep[e].first + 1]++;
+    P.edge_pt.clear();
+    P.edge_pose.clear();
+    P.edge_pt.reserve(poses.size());
+    P.edge_pose.reserve(poses.size());
+    for (int pt = 0; pt < P.n_pt; ++pt) {
+      auto b = poses.begin() + cnt[pt], e = poses.begin() + cnt[pt + 1];
+      std::sort(b, e);
+      e = std::unique(b, e);
+      for (auto it = b; it != e; ++it) {
+        P.edge_pt.push_back(pt);
+        P.edge_pose.push_back(*it);
+      }
+      P.pt_edge_start[pt + 1] = static_cast<int32_t>(P.edge_pose.size());
     }
-    for (int i = 0; i < P.n_pt; ++i) P.pt_edge_start[i + 1] += P.pt_edge_start[i];
+    P.n_edge = static_cast<int>(P.edge_pose.size());
   }
   auto find_edge = [&](int32_t pt, int32_t pose) -> int32_t {
     auto b = P.edge_pose.begin() + P.pt_edge_start[pt];
@@ -254,6 +345,7 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
     return static_cast<int32_t>(it - P.edge_pose.begin());
   };
 
+  plan_mark("before arena layout", tmark);
   // ---- arena layout ----
   // every region starts at an even offset (16-byte aligned), so blocks at
   // even offsets inside it can be read with 16-byte loads
@@ -266,6 +358,7 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
   align2();
   P.off_W = arena; arena += 18ull * P.n_edge;
 
+  plan_mark("before component neighbour poses and Y layout", tmark);
   // ---- component neighbour poses and Y layout ----
   P.comp_nb_start.assign(1, 0);
   P.comp_y_base.resize(P.n_comp);
@@ -303,108 +396,186 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
   P.arena_size = arena;
   if (arena >= (1ull << 32)) { err = "graph too large for 32-bit arena offsets"; return DYNOHIP_ESTRUCT; }
 
-  // ---- point-side gathers ----
+  plan_mark("before point-side gathers", tmark);
+  // ---- point-side gathers (CSR builds run on worker threads) ----
+  std::vector<std::thread> workers;
+  bool chain_ok = true;
   {
-    std::vector<std::pair<int32_t, GEntry>> pD, pE, pG, pW;
-    for (int t = 0; t < kNTypes; ++t) {
-      const TypePlan& tp = P.types[t];
-      const int nk = kNKeys[t], d = kDim[t];
-      for (int i = 0; i < tp.n; ++i) {
-        int pslot[2], np = 0;
-        for (int s = 0; s < nk; ++s) {
-          if (kSlotKind[t][s] != 1) continue;
-          pslot[np++] = s;
-          const int32_t pt = tp.idx[i * nk + s];
-          const uint32_t J = block_off(tp, t, i, s);
-          pD.push_back({pt, GEntry{J, J, d, 1}});
-          pG.push_back({pt, GEntry{J, b_off(tp, t, i), d, 1}});
-          for (int sb = 0; sb < nk; ++sb)
-            if (kSlotKind[t][sb] == 0)
-              pW.push_back({find_edge(pt, tp.idx[i * nk + sb]), GEntry{J, block_off(tp, t, i, sb), d, 1}});
-        }
-        if (np == 2) {
-          int sa = pslot[0], sb = pslot[1];
-          int32_t pa = tp.idx[i * nk + sa], pb = tp.idx[i * nk + sb];
-          if (pa > pb) { std::swap(pa, pb); std::swap(sa, sb); }
-          if (pb != pa + 1 || comp_of[pa] != comp_of[pb]) { err = "internal: chain link not adjacent"; return DYNOHIP_ESTRUCT; }
-          // E_pa = C_{pa+1, pa} = J_{pb}^T J_{pa}
-          pE.push_back({pa, GEntry{block_off(tp, t, i, sb), block_off(tp, t, i, sa), d, 1}});
+    // enumerates the point-side entries in factor order; `which` selects
+    // D (0), E (1), g_p (2) or W (3)
+    auto emit_point = [&](int which, auto&& fn) {
+      for (int t = 0; t < kNTypes; ++t) {
+        const TypePlan& tp = P.types[t];
+        const int nk = kNKeys[t], d = kDim[t];
+        for (int i = 0; i < tp.n; ++i) {
+          int pslot[2], np = 0;
+          for (int s = 0; s < nk; ++s) {
+            if (kSlotKind[t][s] != 1) continue;
+            pslot[np++] = s;
+            const int32_t pt = tp.idx[i * nk + s];
+            const uint32_t J = block_off(tp, t, i, s);
+            if (which == 0) fn(pt, GEntry{J, J, d, 1});
+            if (which == 2) fn(pt, GEntry{J, b_off(tp, t, i), d, 1});
+            if (which == 3)
+              for (int sb = 0; sb < nk; ++sb)
+                if (kSlotKind[t][sb] == 0) fn(find_edge(pt, tp.idx[i * nk + sb]), GEntry{J, block_off(tp, t, i, sb), d, 1});
+          }
+          if (which == 1 && np == 2) {
+            int sa = pslot[0], sb = pslot[1];
+            int32_t pa = tp.idx[i * nk + sa], pb = tp.idx[i * nk + sb];
+            if (pa > pb) { std::swap(pa, pb); std::swap(sa, sb); }
+            if (pb != pa + 1 || comp_of[pa] != comp_of[pb]) { chain_ok = false; continue; }
+            // E_pa = C_{pa+1, pa} = J_{pb}^T J_{pa}
+            fn(pa, GEntry{block_off(tp, t, i, sb), block_off(tp, t, i, sa), d, 1});
+          }
         }
       }
-    }
-    to_csr(P.n_pt, pD, P.gD);
-    to_csr(P.n_pt, pE, P.gE);
-    to_csr(P.n_pt, pG, P.gGp);
-    to_csr(P.n_edge, pW, P.gW);
-  }
-
-  // ---- reduced system targets ----
-  {
-    std::unordered_map<uint64_t, int32_t> tmap;
-    std::vector<std::pair<int32_t, int32_t>> tgt;  // (A, B)
-    auto target = [&](int32_t A, int32_t B) -> int32_t {
-      const uint64_t k = (static_cast<uint64_t>(A) << 32) | static_cast<uint32_t>(B);
-      auto it = tmap.find(k);
-      if (it != tmap.end()) return it->second;
-      const int32_t id = static_cast<int32_t>(tgt.size());
-      tmap.emplace(k, id);
-      tgt.emplace_back(A, B);
-      return id;
     };
-    for (int32_t A = 0; A < P.n_pose; ++A) target(A, A);  // every diagonal (damping)
-    std::vector<std::pair<int32_t, GEntry>> pr, pg;
-    for (int t = 0; t < kNTypes; ++t) {
-      const TypePlan& tp = P.types[t];
-      const int nk = kNKeys[t], d = kDim[t];
-      for (int i = 0; i < tp.n; ++i)
-        for (int sa = 0; sa < nk; ++sa) {
-          if (kSlotKind[t][sa] != 0) continue;
-          const int32_t A = tp.idx[i * nk + sa];
-          pg.push_back({A, GEntry{block_off(tp, t, i, sa), b_off(tp, t, i), d, 1}});
-          for (int sb = 0; sb < nk; ++sb) {
-            if (kSlotKind[t][sb] != 0) continue;
-            const int32_t B = tp.idx[i * nk + sb];
-            if (A < B) continue;
-            pr.push_back({target(A, B), GEntry{block_off(tp, t, i, sa), block_off(tp, t, i, sb), d, 1}});
+    for (int which = 0; which < 4; ++which)
+      workers.emplace_back([&P, &emit_point, which] {
+        GatherList& out = which == 0 ? P.gD : which == 1 ? P.gE : which == 2 ? P.gGp : P.gW;
+        csr_two_pass(which == 3 ? P.n_edge : P.n_pt, [&](auto&& fn) { emit_point(which, fn); }, out);
+      });
+    for (auto& w : workers) w.join();
+    workers.clear();
+  }
+  if (!chain_ok) { err = "internal: chain link not adjacent"; return DYNOHIP_ESTRUCT; }
+
+  plan_mark("before reduced system targets", tmark);
+  // ---- reduced system targets ----
+  // Pose-pair blocks (A >= B) of the reduced system: every diagonal (for the
+  // damping), the pose pairs of every factor and the neighbour-pose pairs of
+  // every point component. Targets are numbered in (B, A) order (band column
+  // order); each target's entries keep the enumeration order below.
+  {
+    auto emit_pairs = [&](auto&& pair_fn) {  // pair_fn(A, B, entry)
+      for (int t = 0; t < kNTypes; ++t) {
+        const TypePlan& tp = P.types[t];
+        const int nk = kNKeys[t], d = kDim[t];
+        for (int i = 0; i < tp.n; ++i)
+          for (int sa = 0; sa < nk; ++sa) {
+            if (kSlotKind[t][sa] != 0) continue;
+            const int32_t A = tp.idx[i * nk + sa];
+            for (int sb = 0; sb < nk; ++sb) {
+              if (kSlotKind[t][sb] != 0) continue;
+              const int32_t B = tp.idx[i * nk + sb];
+              if (A < B) continue;
+              pair_fn(A, B, GEntry{block_off(tp, t, i, sa), block_off(tp, t, i, sb), d, 1});
+            }
           }
-        }
-    }
-    for (int c = 0; c < P.n_comp; ++c) {
-      const int32_t nb0 = P.comp_nb_start[c], m = P.comp_nb_start[c + 1] - nb0;
-      for (int a = 0; a < m; ++a) {
-        const int32_t A = P.nb_pose[nb0 + a];
-        for (int32_t q = P.nbedge_start[nb0 + a]; q < P.nbedge_start[nb0 + a + 1]; ++q)
-          pg.push_back({A, GEntry{P.nbedge_w[q], static_cast<uint32_t>(P.off_v + 3ull * (P.comp_start[c] + P.nbedge_pt[q])), 3, -1}});
-        for (int b = 0; b <= a; ++b) {
-          const int32_t B = P.nb_pose[nb0 + b];
-          const int32_t tid = target(A, B);
-          for (int32_t q = P.nbedge_start[nb0 + a]; q < P.nbedge_start[nb0 + a + 1]; ++q) {
-            const int i = P.nbedge_pt[q];
-            const uint32_t y = static_cast<uint32_t>(P.comp_y_base[c] + 18ll * (static_cast<int64_t>(i) * m + b));
-            pr.push_back({tid, GEntry{P.nbedge_w[q], y, 3, -1}});
+      }
+      for (int c = 0; c < P.n_comp; ++c) {
+        const int32_t nb0 = P.comp_nb_start[c], m = P.comp_nb_start[c + 1] - nb0;
+        for (int a = 0; a < m; ++a) {
+          const int32_t A = P.nb_pose[nb0 + a];
+          for (int b = 0; b <= a; ++b) {
+            const int32_t B = P.nb_pose[nb0 + b];
+            for (int32_t q = P.nbedge_start[nb0 + a]; q < P.nbedge_start[nb0 + a + 1]; ++q) {
+              const int i = P.nbedge_pt[q];
+              const uint32_t y = static_cast<uint32_t>(P.comp_y_base[c] + 18ll * (static_cast<int64_t>(i) * m + b));
+              pair_fn(A, B, GEntry{P.nbedge_w[q], y, 3, -1});
+            }
           }
         }
       }
+    };
+    // gradient gathers per pose: J_A^T b per factor, then -W_A v per component
+    auto emit_grad = [&](auto&& fn) {
+      for (int t = 0; t < kNTypes; ++t) {
+        const TypePlan& tp = P.types[t];
+        const int nk = kNKeys[t], d = kDim[t];
+        for (int i = 0; i < tp.n; ++i)
+          for (int sa = 0; sa < nk; ++sa)
+            if (kSlotKind[t][sa] == 0) fn(tp.idx[i * nk + sa], GEntry{block_off(tp, t, i, sa), b_off(tp, t, i), d, 1});
+      }
+      for (int c = 0; c < P.n_comp; ++c) {
+        const int32_t nb0 = P.comp_nb_start[c], m = P.comp_nb_start[c + 1] - nb0;
+        for (int a = 0; a < m; ++a)
+          for (int32_t q = P.nbedge_start[nb0 + a]; q < P.nbedge_start[nb0 + a + 1]; ++q)
+            fn(P.nb_pose[nb0 + a], GEntry{P.nbedge_w[q], static_cast<uint32_t>(P.off_v + 3ull * (P.comp_start[c] + P.nbedge_pt[q])), 3, -1});
+      }
+    };
+    // pair index: dense rows of width (max A - B) + 1 when that is small,
+    // a hash map otherwise. The distinct pairs are the factor pose pairs and
+    // the (a, b) neighbour pairs of every component (each neighbour pose has
+    // at least one edge), so marking does not walk the edge lists.
+    auto each_distinct = [&](auto&& fn) {
+      for (int t = 0; t < kNTypes; ++t) {
+        const TypePlan& tp = P.types[t];
+        const int nk = kNKeys[t];
+        if (kNPoseSlots[t] < 2) continue;
+        for (int i = 0; i < tp.n; ++i)
+          for (int sa = 0; sa < nk; ++sa)
+            if (kSlotKind[t][sa] == 0)
+              for (int sb = 0; sb < nk; ++sb)
+                if (kSlotKind[t][sb] == 0 && tp.idx[i * nk + sa] >= tp.idx[i * nk + sb])
+                  fn(tp.idx[i * nk + sa], tp.idx[i * nk + sb]);
+      }
+      for (int c = 0; c < P.n_comp; ++c) {
+        const int32_t nb0 = P.comp_nb_start[c], m = P.comp_nb_start[c + 1] - nb0;
+        for (int a = 0; a < m; ++a)
+          for (int b = 0; b <= a; ++b) fn(P.nb_pose[nb0 + a], P.nb_pose[nb0 + b]);
+      }
+    };
+    int32_t W = 0;
+    for (int t = 0; t < kNTypes; ++t) {
+      const TypePlan& tp = P.types[t];
+      const int nk = kNKeys[t];
+      if (kNPoseSlots[t] < 2) continue;
+      for (int i = 0; i < tp.n; ++i)
+        for (int sa = 0; sa < nk; ++sa)
+          for (int sb = 0; sb < nk; ++sb)
+            if (kSlotKind[t][sa] == 0 && kSlotKind[t][sb] == 0)
+              W = std::max(W, tp.idx[i * nk + sa] - tp.idx[i * nk + sb]);
     }
-    // renumber targets in (B, A) order (band column order)
-    std::vector<int32_t> order(tgt.size());
-    std::iota(order.begin(), order.end(), 0);
-    std::sort(order.begin(), order.end(), [&](int32_t x, int32_t y) {
-      if (tgt[x].second != tgt[y].second) return tgt[x].second < tgt[y].second;
-      return tgt[x].first < tgt[y].first;
-    });
-    std::vector<int32_t> rank(tgt.size());
-    for (size_t r = 0; r < order.size(); ++r) rank[order[r]] = static_cast<int32_t>(r);
-    for (auto& p : pr) p.first = rank[p.first];
-    P.red_A.resize(tgt.size());
-    P.red_B.resize(tgt.size());
-    for (size_t r = 0; r < order.size(); ++r) {
-      P.red_A[r] = tgt[order[r]].first;
-      P.red_B[r] = tgt[order[r]].second;
+    for (int c = 0; c < P.n_comp; ++c) {  // nb poses are sorted per component
+      const int32_t nb0 = P.comp_nb_start[c], nb1 = P.comp_nb_start[c + 1];
+      if (nb1 > nb0) W = std::max(W, P.nb_pose[nb1 - 1] - P.nb_pose[nb0]);
     }
-    to_csr(tgt.size(), pr, P.gRed);
-    to_csr(P.n_pose, pg, P.gGred);
+    const int64_t span = static_cast<int64_t>(W) + 1;
+    const bool dense = static_cast<int64_t>(P.n_pose) * span <= (int64_t{1} << 26);
+    std::vector<int32_t> id_dense;
+    std::unordered_map<uint64_t, int32_t> id_map;
+    auto pkey = [](int32_t A, int32_t B) { return (static_cast<uint64_t>(B) << 32) | static_cast<uint32_t>(A); };
+    if (dense) id_dense.assign(static_cast<size_t>(P.n_pose) * span, -1);
+    auto mark = [&](int32_t A, int32_t B) {
+      if (dense) id_dense[static_cast<size_t>(A) * span + (A - B)] = 0;
+      else id_map.emplace(pkey(A, B), 0);
+    };
+    for (int32_t A = 0; A < P.n_pose; ++A) mark(A, A);
+    each_distinct(mark);
+    P.red_A.clear();
+    P.red_B.clear();
+    if (dense) {
+      for (int32_t B = 0; B < P.n_pose; ++B)
+        for (int32_t A = B; A < P.n_pose && A - B < span; ++A) {
+          int32_t& id = id_dense[static_cast<size_t>(A) * span + (A - B)];
+          if (id < 0) continue;
+          id = static_cast<int32_t>(P.red_A.size());
+          P.red_A.push_back(A);
+          P.red_B.push_back(B);
+        }
+    } else {
+      std::vector<uint64_t> ks;
+      ks.reserve(id_map.size());
+      for (const auto& kv : id_map) ks.push_back(kv.first);
+      std::sort(ks.begin(), ks.end());  // (B, A) order
+      for (uint64_t k : ks) {
+        id_map[k] = static_cast<int32_t>(P.red_A.size());
+        P.red_A.push_back(static_cast<int32_t>(k & 0xffffffffu));
+        P.red_B.push_back(static_cast<int32_t>(k >> 32));
+      }
+    }
+    auto tid = [&](int32_t A, int32_t B) -> int32_t {
+      return dense ? id_dense[static_cast<size_t>(A) * span + (A - B)] : id_map.at(pkey(A, B));
+    };
+    std::thread grad([&] { csr_two_pass(P.n_pose, emit_grad, P.gGred); });
+    csr_two_pass(P.red_A.size(),
+                 [&](auto&& fn) { emit_pairs([&](int32_t A, int32_t B, const GEntry& e) { fn(tid(A, B), e); }); },
+                 P.gRed);
+    grad.join();
   }
+  plan_mark("reduced system targets", tmark);
 
   // ---- band layout ----
   P.n_red = 6 * P.n_pose;
@@ -423,10 +594,12 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
     P.band_D[j] = rlow[j] - j;
     P.max_D = std::max(P.max_D, P.band_D[j]);
   }
+  plan_mark("band", tmark);
   if (with_schedule && !build_tile_schedule(P)) {
     err = "graph too short in time for " + std::to_string(nranks) + " partitions";
     return DYNOHIP_ESTRUCT;
   }
+  plan_mark("tile schedule", tmark);
   return DYNOHIP_OK;
 }
 

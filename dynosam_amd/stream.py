@@ -93,13 +93,16 @@ def generate(cfg=StreamConfig()):
     starts = rng.integers(0, F - Ls + 1, size=S)
     local = np.stack([rng.normal(0, 6.0, S), rng.normal(0, 3.0, S), 12.0 + rng.normal(0, 4.0, S)], axis=1)
     static_world = np.zeros((S, 3))
-    for i in range(S):
-        Xm = X[starts[i] + Ls // 2]
-        p = Xm[:3, :3] @ local[i] + Xm[:3, 3]
-        static_world[i] = p
-        for k in range(starts[i], starts[i] + Ls):
-            z = X[k][:3, :3].T @ (p - X[k][:3, 3]) + rng.normal(0, cfg.meas_noise, 3)
-            meas[k]["static"].append((i, 0, z))
+    Xs = np.stack(X)                                        # F x 4 x 4
+    mid = Xs[starts + Ls // 2]
+    static_world = np.einsum("nij,nj->ni", mid[:, :3, :3], local) + mid[:, :3, 3]
+    noise = rng.normal(0, cfg.meas_noise, (S, Ls, 3))
+    for off in range(Ls):
+        ks = starts + off
+        Xk = Xs[ks]
+        z = np.einsum("nji,nj->ni", Xk[:, :3, :3], static_world - Xk[:, :3, 3]) + noise[:, off]
+        for i in range(S):
+            meas[int(ks[i])]["static"].append((i, 0, z[i]))
     next_trk = S
     for j in range(cfg.single_obs_static):
         k = int(rng.integers(0, F))

@@ -274,6 +274,35 @@ dynob_formulation* dynob_module_formulation(dynob_module* m);
 int dynob_module_last_problem(dynob_module* m, dynohip_graph_view* g, const uint64_t** keys, const uint8_t** kinds,
                               const double** initial, const double** optimised, size_t* n, size_t* n_doubles);
 
+/* ------------------------------------------------------------------ */
+/* Frontend-output replay (BSON)                                       */
+/* ------------------------------------------------------------------ */
+/* The file RGBDInstanceFrontendModule writes with
+   JsonConverter::WriteOutJson(std::map<FrameId, RGBDInstanceOutputPacket>)
+   (RGBDInstanceFrontendModule.cc:80, Logger.hpp:170-230): nlohmann BSON of
+   {"data": [[frame_id, packet], ...]} with the packet layout of
+   JsonUtils.cc:68-118. The reader decodes what RGBDBackendModule::updateMap
+   reads (landmark+keypoint pairs, checked as
+   collectLandmarkKeypointMeasurementsHelper does; frontend camera pose;
+   estimated motions) plus the optional ground truth. Parse errors (a failed
+   nlohmann get / a CHECK in the reference) return DYNOHIP_EINVAL; the handle
+   is still returned so the message can be read, and must be destroyed. */
+typedef struct dynob_replay dynob_replay;
+
+int dynob_replay_open(const char* path, dynob_replay** out);
+int dynob_replay_parse(const uint8_t* data, size_t n, dynob_replay** out);
+void dynob_replay_destroy(dynob_replay* r);
+const char* dynob_replay_last_error(const dynob_replay* r);
+size_t dynob_replay_num_packets(const dynob_replay* r);
+/* Packet i (ascending frame order) as the module's input; the pointers stay
+   valid while the replay handle lives. */
+int dynob_replay_packet(const dynob_replay* r, size_t i, dynob_input_packet* out);
+/* GroundTruthInputPacket of packet i: returns 1 and fills X_world and up to
+   `cap` objects (L_world_, prev_H_current_world_ or NaN when absent), 0 when
+   the packet has none. *n_objects = the packet's object count. */
+int dynob_replay_ground_truth(const dynob_replay* r, size_t i, double* X_world12, int32_t* object_ids,
+                              double* L_world12, double* prev_H12, size_t cap, size_t* n_objects);
+
 #ifdef __cplusplus
 }
 #endif
