@@ -9,3 +9,5 @@ timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun
 timeout -k 10 300 python -u bench.py > gpurun_out/bench_c2.log 2>&1 || exit 3
 timeout -k 10 300 python -u bench.py --config NS --no-cpu-baseline > gpurun_out/bench_ns.log 2>&1 || exit 4
 bash tools/prof_run.sh gpurun_out/prof_c2 bench.py --steps 3 --no-cpu-baseline > gpurun_out/prof_c2.txt 2>&1 || exit 5
+timeout -k 10 300 python -u bench.py --mode stream --steps 2 --warmup 1 > gpurun_out/bench_stream_sw.log 2>&1 || exit 6
+timeout -k 10 300 python -u bench.py --mode stream --full-batch --steps 2 --warmup 1 > gpurun_out/bench_stream_fb.log 2>&1 || exit 7
