@@ -261,3 +261,43 @@ class GroundTruth(C.Structure):
         ("L_world12", C.POINTER(C.c_double)),
         ("prev_H_current_world12", C.POINTER(C.c_double)),
     ]
+
+
+# ---- include/dynorefine.h --------------------------------------------------
+class RefineBatch(C.Structure):
+    _fields_ = [
+        ("n_problems", C.c_size_t),
+        ("track_start", C.POINTER(C.c_int32)),
+        ("X_k_1", C.POINTER(C.c_double)),
+        ("X_k", C.POINTER(C.c_double)),
+        ("H_init", C.POINTER(C.c_double)),
+        ("calibration", C.POINTER(C.c_double)),
+        ("kp_k_1", C.POINTER(C.c_double)),
+        ("kp_k", C.POINTER(C.c_double)),
+        ("m_k_1", C.POINTER(C.c_double)),
+        ("m_k", C.POINTER(C.c_double)),
+        ("X_k_1_init", C.POINTER(C.c_double)),
+        ("X_k_init", C.POINTER(C.c_double)),
+    ]
+
+
+class RefineParams(C.Structure):
+    _fields_ = [
+        ("landmark_motion_sigma", C.c_double),
+        ("projection_sigma", C.c_double),
+        ("k_huber", C.c_double),
+        ("prior_sigma", C.c_double),
+        ("outlier_reject", C.c_int),
+        ("reserved", C.c_int),
+    ]
+
+
+class RefineResult(C.Structure):
+    _fields_ = [
+        ("iterations", C.c_int),
+        ("inner_iterations", C.c_int),
+        ("status", C.c_int),
+        ("n_outliers", C.c_int),
+        ("error_before", C.c_double),
+        ("error_after", C.c_double),
+    ]

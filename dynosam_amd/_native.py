@@ -155,6 +155,16 @@ def _declare(name, lib):
             ("dynob_replay_num_packets", [vp_], C.c_size_t),
             ("dynob_replay_packet", [vp_, C.c_size_t, P(_abi.InputPacket)], C.c_int),
             ("dynob_replay_ground_truth", [vp_, C.c_size_t, D, I32_, D, D, C.c_size_t, SZ], C.c_int),
+            ("dynorefine_params_default", [P(_abi.RefineParams)], None),
+            ("dynorefine_create", [C.c_int, P(vp_)], C.c_int),
+            ("dynorefine_destroy", [vp_], None),
+            ("dynorefine_last_error", [vp_], C.c_char_p),
+            ("dynorefine_upload", [vp_, P(_abi.RefineBatch)], C.c_int),
+            ("dynorefine_solve", [vp_, P(_abi.RefineParams), P(_abi.LMParams)], C.c_int),
+            ("dynorefine_download", [vp_, D, U8, P(_abi.RefineResult)], C.c_int),
+            ("dynorefine_run", [vp_, P(_abi.RefineBatch), P(_abi.RefineParams), P(_abi.LMParams), D, U8,
+                                P(_abi.RefineResult)], C.c_int),
+            ("dynorefine_last_solve_ms", [vp_], C.c_double),
             ("dynob_module_params_default", [P(_abi.ModuleParams)], None),
             ("dynob_module_create", [P(_abi.BackendParams), P(_abi.ModuleParams), P(vp_)], C.c_int),
             ("dynob_module_destroy", [vp_], None),

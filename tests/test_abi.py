@@ -72,3 +72,13 @@ def test_backend_struct_sizes():
     assert C.sizeof(_abi.InputPacket) == 8 + 8 + 96 + 8 * 7
     assert C.sizeof(_abi.ModuleParams) == 4 + 4 + 8 + 4 * 6 + C.sizeof(_abi.LMParams)
     assert C.sizeof(_abi.SpinResult) == 4 * 4 + 8 * 6
+
+
+def test_dynorefine_exports_every_declared_symbol():
+    lib = C.CDLL(_native.lib_path("libdynohip.so"))
+    names = declared("dynorefine.h", "dynorefine_")
+    assert len(names) >= 9
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    assert C.sizeof(_abi.RefineBatch) == 8 + 11 * 8
+    assert C.sizeof(_abi.RefineResult) == 4 * 4 + 2 * 8

@@ -8,5 +8,5 @@ out=$(realpath -m "$1"); shift
 mkdir -p "$out"
 cd "$root/dynosam_amd/csrc"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wall "$@" -o "$out/libdynohip.so" \
-  kernels.hip tilechol.hip solver.cpp plan.cpp tiles.cpp partition.cpp keys.cpp driver.cpp backend.cpp replay.cpp
+  kernels.hip tilechol.hip solver.cpp plan.cpp tiles.cpp partition.cpp keys.cpp driver.cpp backend.cpp replay.cpp refine.hip
 cp "$root/dynosam_amd/lib/libdynosynth.so" "$out/"
