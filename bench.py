@@ -47,10 +47,11 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default=None, help="C2 (windows mode default) / C5 (partitioned default) / ...")
-    ap.add_argument("--mode", default="windows", choices=("windows", "partitioned", "stream"),
+    ap.add_argument("--mode", default="windows", choices=("windows", "partitioned", "stream", "refine"),
                     help="windows: one independent graph per rank (weak scaling); partitioned: one graph split "
                          "over the ranks (strong scaling); stream: the backend module replays a synthetic "
                          "frontend stream per rank (graph construction + sliding-window LM, weak scaling)")
+    ap.add_argument("--problems", type=int, default=4096, help="refine mode: (object, frame pair) problems per batch")
     ap.add_argument("--full-batch", action="store_true", help="stream mode: one full-batch solve at the last frame "
                                                              "instead of the sliding window (shipped flags)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample (s)")
@@ -168,6 +169,76 @@ def stream_main(args, world, rank, local_rank, dist):
         dist.destroy_process_group()
 
 
+def refine_main(args, world, rank, local_rank, dist):
+    """--mode refine: the batched frontend object-motion refinement
+    (dynosam_amd.refine). One step = one batch of
+    `--problems` MotionOnlyRefinementOptimizer problems (20-60 tracklets
+    each, device-resident inputs) solved in one launch; value = problems
+    solved per second over all ranks (each rank its own batch). The CPU
+    baseline is the numpy restatement (oracle/refine.py, dense solve, one
+    thread) on a bounded sample of the same problems."""
+    import torch
+    from dynosam_amd import refine
+
+    batch = refine.synthetic_batch(args.problems, tracks=(20, 60), seed=42 + rank)
+    opt = refine.MotionOnlyRefinementOptimizer(device=local_rank)
+    opt.upload(batch)
+    for _ in range(args.warmup):
+        opt.solve()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    kernel_ms = 0.0
+    for _ in range(args.steps):
+        kernel_ms += opt.solve()
+    barrier()
+    dt = time.perf_counter() - t0
+    H, flags, res = opt.download()
+    iters = sum(r["iterations"] for r in res)
+    inner = sum(r["inner_iterations"] for r in res)
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    n_total = args.problems * args.steps * world
+    if rank == 0:
+        out = {
+            "metric": "object-motion refinements/s (MotionOnlyRefinementOptimizer, batched)",
+            "value": n_total / dt, "unit": "problems/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": 1e3 * dt / args.steps,
+            "kernel_ms_per_step": kernel_ms / args.steps,
+            "lm_iterations_per_problem": iters / args.problems, "inner_iterations_per_problem": inner / args.problems,
+            "lm_iterations_per_s": iters * args.steps * world / dt,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (dynosam_amd.refine.synthetic_batch, seed 42 + rank)",
+            "config": {"workload": f"{args.problems} problems x 20-60 tracklets, ProjectionError, default params",
+                       "tracklets": int(batch.track_start[-1])},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import refine as orf  # test infrastructure: the checker, timed as the CPU baseline
+            R = orf.Refiner()
+            t0 = time.perf_counter()
+            n = 0
+            while time.perf_counter() - t0 < args.cpu_seconds and n < batch.n:
+                d = batch.problem(n)
+                R.refine(orf.Problem(d["X_k_1"], d["X_k"], d["H"], d["K"], d["kp_k_1"], d["kp_k"], d["m_k_1"],
+                                     d["m_k"]))
+                n += 1
+            cdt = time.perf_counter() - t0
+            out["cpu_baseline"] = {"value": n / cdt, "unit": "problems/s", "cores": 1, "kind": "port",
+                                   "sample": f"first {n} problems of the batch, numpy restatement (oracle/refine.py, "
+                                             f"dense solve), {cdt:.1f} s"}
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     if args.config is None:
@@ -185,6 +256,8 @@ def main():
         dist.init_process_group(backend="nccl")
     if args.mode == "stream":
         return stream_main(args, world, rank, local_rank, dist)
+    if args.mode == "refine":
+        return refine_main(args, world, rank, local_rank, dist)
     from dynosam_amd import synth
     from dynosam_amd.optimizer import Solver
 
