@@ -108,6 +108,36 @@ void csr_two_pass(size_t ntargets, Emit&& emit, GatherList& out) {
   emit([&](int32_t t, const GEntry& e) { out.ent[cur[t]++] = e; });
 }
 
+// CSR over `nranges` contiguous pieces of one enumeration: emit_range(r, fn)
+// enumerates piece r; the pieces are counted and filled on worker threads,
+// and every target's entries keep the order of the whole enumeration
+template <typename EmitRange>
+void csr_ranges(size_t ntargets, int nranges, EmitRange&& emit_range, GatherList& out) {
+  std::vector<std::vector<int64_t>> cur(nranges, std::vector<int64_t>(ntargets, 0));
+  auto parallel = [&](auto&& body) {
+    std::vector<std::thread> th;
+    for (int r = 1; r < nranges; ++r) th.emplace_back([&, r] { body(r); });
+    body(0);
+    for (auto& t : th) t.join();
+  };
+  parallel([&](int r) { emit_range(r, [&](int32_t t, const GEntry&) { cur[r][t]++; }); });
+  out.start.assign(ntargets + 1, 0);
+  for (size_t t = 0; t < ntargets; ++t) {
+    int64_t off = out.start[t];
+    for (int r = 0; r < nranges; ++r) {
+      const int64_t c = cur[r][t];
+      cur[r][t] = off;
+      off += c;
+    }
+    out.start[t + 1] = off;
+  }
+  out.ent.resize(out.start[ntargets]);
+  parallel([&](int r) {
+    auto& c = cur[r];
+    emit_range(r, [&](int32_t t, const GEntry& e) { out.ent[c[t]++] = e; });
+  });
+}
+
 void to_csr(size_t ntargets, std::vector<std::pair<int32_t, GEntry>>& pairs, GatherList& out) {
   out.start.assign(ntargets + 1, 0);
   for (auto& p : pairs) out.start[p.first + 1]++;
@@ -448,23 +478,33 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
   // every point component. Targets are numbered in (B, A) order (band column
   // order); each target's entries keep the enumeration order below.
   {
-    auto emit_pairs = [&](auto&& pair_fn) {  // pair_fn(A, B, entry)
-      for (int t = 0; t < kNTypes; ++t) {
-        const TypePlan& tp = P.types[t];
-        const int nk = kNKeys[t], d = kDim[t];
-        for (int i = 0; i < tp.n; ++i)
-          for (int sa = 0; sa < nk; ++sa) {
-            if (kSlotKind[t][sa] != 0) continue;
-            const int32_t A = tp.idx[i * nk + sa];
-            for (int sb = 0; sb < nk; ++sb) {
-              if (kSlotKind[t][sb] != 0) continue;
-              const int32_t B = tp.idx[i * nk + sb];
-              if (A < B) continue;
-              pair_fn(A, B, GEntry{block_off(tp, t, i, sa), block_off(tp, t, i, sb), d, 1});
+    // the pair enumeration in pieces: piece 0 = the factors, pieces 1.. =
+    // contiguous component ranges (comp_cut)
+    const int n_pieces = 1 + std::max(1, std::min(7, P.n_comp / 2048));
+    std::vector<int> comp_cut(n_pieces);
+    for (int r = 1; r < n_pieces; ++r)
+      comp_cut[r - 1] = static_cast<int>(static_cast<int64_t>(P.n_comp) * (r - 1) / (n_pieces - 1));
+    comp_cut[n_pieces - 1] = P.n_comp;
+    auto emit_pairs_piece = [&](int piece, auto&& pair_fn) {  // pair_fn(A, B, entry)
+      if (piece == 0) {
+        for (int t = 0; t < kNTypes; ++t) {
+          const TypePlan& tp = P.types[t];
+          const int nk = kNKeys[t], d = kDim[t];
+          for (int i = 0; i < tp.n; ++i)
+            for (int sa = 0; sa < nk; ++sa) {
+              if (kSlotKind[t][sa] != 0) continue;
+              const int32_t A = tp.idx[i * nk + sa];
+              for (int sb = 0; sb < nk; ++sb) {
+                if (kSlotKind[t][sb] != 0) continue;
+                const int32_t B = tp.idx[i * nk + sb];
+                if (A < B) continue;
+                pair_fn(A, B, GEntry{block_off(tp, t, i, sa), block_off(tp, t, i, sb), d, 1});
+              }
             }
-          }
+        }
+        return;
       }
-      for (int c = 0; c < P.n_comp; ++c) {
+      for (int c = comp_cut[piece - 1]; c < comp_cut[piece]; ++c) {
         const int32_t nb0 = P.comp_nb_start[c], m = P.comp_nb_start[c + 1] - nb0;
         for (int a = 0; a < m; ++a) {
           const int32_t A = P.nb_pose[nb0 + a];
@@ -478,6 +518,9 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
           }
         }
       }
+    };
+    auto emit_pairs = [&](auto&& pair_fn) {
+      for (int r = 0; r < n_pieces; ++r) emit_pairs_piece(r, pair_fn);
     };
     // gradient gathers per pose: J_A^T b per factor, then -W_A v per component
     auto emit_grad = [&](auto&& fn) {
@@ -570,9 +613,11 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
       return dense ? id_dense[static_cast<size_t>(A) * span + (A - B)] : id_map.at(pkey(A, B));
     };
     std::thread grad([&] { csr_two_pass(P.n_pose, emit_grad, P.gGred); });
-    csr_two_pass(P.red_A.size(),
-                 [&](auto&& fn) { emit_pairs([&](int32_t A, int32_t B, const GEntry& e) { fn(tid(A, B), e); }); },
-                 P.gRed);
+    csr_ranges(P.red_A.size(), n_pieces,
+               [&](int piece, auto&& fn) {
+                 emit_pairs_piece(piece, [&](int32_t A, int32_t B, const GEntry& e) { fn(tid(A, B), e); });
+               },
+               P.gRed);
     grad.join();
   }
   plan_mark("reduced system targets", tmark);

@@ -11,3 +11,5 @@ timeout -k 10 300 python -u bench.py --config NS --no-cpu-baseline > gpurun_out/
 bash tools/prof_run.sh gpurun_out/prof_c2 bench.py --steps 3 --no-cpu-baseline > gpurun_out/prof_c2.txt 2>&1 || exit 5
 timeout -k 10 300 python -u bench.py --mode stream --steps 2 --warmup 1 > gpurun_out/bench_stream_sw.log 2>&1 || exit 6
 timeout -k 10 300 python -u bench.py --mode stream --full-batch --steps 2 --warmup 1 > gpurun_out/bench_stream_fb.log 2>&1 || exit 7
+timeout -k 10 300 python -u bench.py --mode refine --steps 3 --warmup 1 --cpu-seconds 10 > gpurun_out/bench_refine.log 2>&1 || exit 8
+bash tools/prof_run.sh gpurun_out/prof_refine bench.py --mode refine --steps 2 --no-cpu-baseline > gpurun_out/prof_refine.txt 2>&1 || exit 9
