@@ -15,9 +15,10 @@
 // 64). The damped normal equations are solved through the Schur complement
 // of every tracklet's 6x6 point block: a lane factors its C_i + lambda I in
 // registers, forms Y_i = C_i^-1 W_i, and the wave sums B_i - W_i^T Y_i into
-// the 18x18 (X_{k-1}, X_k, H) system with butterfly shuffles in a fixed
-// order (bit-reproducible). The 18x18 system is factored in LDS, then every
-// lane back-substitutes its points. The whole LM loop (linearise, tryLambda,
+// the 18x18 (X_{k-1}, X_k, H) system through an LDS transpose (64 entries at
+// a time, each summed by one lane in lane order: bit-reproducible). The
+// 18x18 system is factored in registers (lane = row, readlane broadcasts),
+// then every lane back-substitutes its points. The whole LM loop (linearise, tryLambda,
 // accept / reject, convergence, outlier rounds) runs inside the kernel: one
 // launch per batch, no host round trip per iteration.
 #include <hip/hip_runtime.h>
@@ -34,6 +35,8 @@ namespace {
 
 constexpr int kWave = 64;
 constexpr int kLin = 80;  // linearisation scratch per tracklet (doubles)
+constexpr int kWin = 63;  // reduction window: 57 system entries + 6 gradient entries
+constexpr int kRedLd = kWave + 1;
 constexpr double kChi2_3_099 = 11.344866730144373;  // boost chi_squared quantile(3, 0.99)
 
 struct Pose {
@@ -241,6 +244,14 @@ __device__ double ternary(const double* p1, const double* p2, const Pose& H, dou
   return huber_rho(e, hk);
 }
 
+// lane `src`'s v (src wave-uniform), through two v_readlane_b32
+__device__ __forceinline__ double read_lane(double v, int src) {
+  const unsigned long long u = __double_as_longlong(v);
+  const unsigned lo = __builtin_amdgcn_readlane(static_cast<unsigned>(u), src);
+  const unsigned hi = __builtin_amdgcn_readlane(static_cast<unsigned>(u >> 32), src);
+  return __longlong_as_double((static_cast<unsigned long long>(hi) << 32) | lo);
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
@@ -295,6 +306,21 @@ __device__ __forceinline__ void point_solve(const double* C, double* x) {
   }
 }
 
+// x <- L^-1 x (the forward half of point_solve)
+__device__ __forceinline__ void lower_solve(const double* C, double* x) {
+  for (int i = 0; i < 6; ++i) {
+    double s = x[i];
+    for (int m = 0; m < i; ++m) s -= C[6 * i + m] * x[m];
+    x[i] = s / C[7 * i];
+  }
+}
+__device__ __forceinline__ double dot6(const double* a, const double* b) {
+  return ((a[0] * b[0] + a[1] * b[1]) + (a[2] * b[2] + a[3] * b[3])) + (a[4] * b[4] + a[5] * b[5]);
+}
+__device__ __forceinline__ double dot3(const double* a, const double* b) {
+  return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2];
+}
+
 // W(:, c): point rows (6) of pose column c in [X1 (0-5) | X2 (6-11) | H (12-17)]
 __device__ __forceinline__ void w_column(const double* L, int c, double* w) {
   const double* A1 = L;
@@ -308,6 +334,20 @@ __device__ __forceinline__ void w_column(const double* L, int c, double* w) {
   } else if (L[79] != 0.0) {
     for (int i = 0; i < 6; ++i)
       w[i] = At[i] * At[c - 6] + At[12 + i] * At[c + 6] + At[24 + i] * At[c + 18];
+  }
+}
+// z = L^-1 W(:, c); z_column_bot: rows 3-5 of z for an X_k column (c in
+// 6-11), whose rows 0-2 are zero
+__device__ __forceinline__ void z_column(const double* L, const double* C, int c, double* z) {
+  w_column(L, c, z);
+  lower_solve(C, z);
+}
+__device__ __forceinline__ void z_column_bot(const double* L, const double* C, int c, double* z) {
+  const double* A2 = L + 20;
+  for (int i = 0; i < 3; ++i) {
+    double s = A2[6 + i] * A2[c - 6] + A2[15 + i] * A2[c + 3];
+    for (int m = 0; m < i; ++m) s -= C[6 * (3 + i) + 3 + m] * z[m];
+    z[i] = s / C[7 * (3 + i)];
   }
 }
 __device__ __forceinline__ void point_grad(const double* L, double* g) {
@@ -372,7 +412,7 @@ struct Shared {
   double g[18];
   double dx[18];
   double bprior[12];
-  int fail;
+  double red[kWave * kRedLd];  // cross-lane reduction of S: [entry][lane]
 };
 
 __device__ double total_error(const Batch& B, const Shared& sh, const double* Kp, int pb, int pt, int t0, int t1,
@@ -402,7 +442,11 @@ __device__ double total_error(const Batch& B, const Shared& sh, const double* Kp
   return e;
 }
 
-__global__ __launch_bounds__(kWave) void k_refine(Batch B) {
+#ifndef DYNOREFINE_WAVES_PER_EU
+#define DYNOREFINE_WAVES_PER_EU 1
+#endif
+__global__ __launch_bounds__(kWave, DYNOREFINE_WAVES_PER_EU)
+void k_refine(Batch B) {
   __shared__ Shared sh;
   const int prob = blockIdx.x;
   const int lane = threadIdx.x;
@@ -475,110 +519,187 @@ __global__ __launch_bounds__(kWave) void k_refine(Batch B) {
 
         // ---- tryLambda until accepted, gave up or stopped ----
         for (;;) {
-          // reduced system: sum_i (B_i - W_i^T C_i^-1 W_i), g_pose - W_i^T C_i^-1 g_i
-          if (lane == 0) {
-            for (int i = 0; i < 18 * 18; ++i) sh.S[i] = 0.0;
-            for (int i = 0; i < 18; ++i) sh.g[i] = 0.0;
-          }
+          // reduced system: sum_i (B_i - W_i^T C_i^-1 W_i), g_pose - W_i^T C_i^-1 g_i,
+          // with C_i = L_i L_i^T: entry (a, b) = B_i(a, b) - z_a . z_b where
+          // z_c = L_i^-1 W_i(:, c). W_i is block sparse (X_{k-1} columns touch
+          // m_{k-1} only, X_k columns m_k only), so z of an X_k column has its
+          // top three rows zero. The 171 entries + 18 gradient entries are
+          // emitted in three windows of 63 (whole block pairs each, so that
+          // only two z blocks are live at a time) and reduced through LDS:
+          // every lane stores its contribution (red[entry][lane]), then lane
+          // e sums row e in lane order (fixed order: bit-reproducible).
+          double acc[3] = {0.0, 0.0, 0.0};
           bool solved = true;
+          auto flush = [&](int grp) {
+            __syncthreads();
+            if (lane < kWin) {
+              const double* row = sh.red + lane * kRedLd;
+              double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+#pragma unroll
+              for (int j = 0; j < kWave; j += 4) {
+                s0 += row[j];
+                s1 += row[j + 1];
+                s2 += row[j + 2];
+                s3 += row[j + 3];
+              }
+              acc[grp] += (s0 + s1) + (s2 + s3);
+            }
+            __syncthreads();
+          };
           for (int base = t0; base < t1; base += kWave) {
             const int t = base + lane;
             const bool have = t < t1;
             const double* L = B.lin + static_cast<int64_t>(have ? t : t0) * kLin;
             double C[36];
-            const bool lok = have ? point_block(L, lambda, C) : true;
+            const bool lok = point_block(L, lambda, C) || !have;
             if (__any(!lok)) {
               solved = false;
               break;
             }
-            double Y[6][18];
+            auto put = [&](int idx, double v) { sh.red[idx * kRedLd + lane] = have ? v : 0.0; };
+            double zg[6];
+            point_grad(L, zg);
+            lower_solve(C, zg);
+            double Z2[6][6], Z0[6][6];
 #pragma unroll
-            for (int a = 0; a < 18; ++a) {
-              double w[6];
-              if (have) {
-                w_column(L, a, w);
-                point_solve(C, w);
+            for (int c = 0; c < 6; ++c) {
+              z_column(L, C, 12 + c, Z2[c]);
+              z_column(L, C, c, Z0[c]);
+            }
+            // window 0: (H, H), (H, X_{k-1}), g_H
+#pragma unroll
+            for (int i = 0; i < 6; ++i)
+#pragma unroll
+              for (int j = 0; j <= i; ++j) put(i * (i + 1) / 2 + j, pose_entry(L, 12 + i, 12 + j) - dot6(Z2[i], Z2[j]));
+#pragma unroll
+            for (int i = 0; i < 6; ++i)
+#pragma unroll
+              for (int j = 0; j < 6; ++j) put(21 + 6 * i + j, -dot6(Z2[i], Z0[j]));
+#pragma unroll
+            for (int i = 0; i < 6; ++i) put(57 + i, pose_grad(L, 12 + i) - dot6(Z2[i], zg));
+            flush(0);
+            // window 1: (X_{k-1}, X_{k-1}), g_{X_{k-1}}, (H, X_k)
+#pragma unroll
+            for (int i = 0; i < 6; ++i)
+#pragma unroll
+              for (int j = 0; j <= i; ++j) put(i * (i + 1) / 2 + j, pose_entry(L, i, j) - dot6(Z0[i], Z0[j]));
+#pragma unroll
+            for (int i = 0; i < 6; ++i) put(57 + i, pose_grad(L, i) - dot6(Z0[i], zg));
+            double Z1[6][3];
+#pragma unroll
+            for (int c = 0; c < 6; ++c) z_column_bot(L, C, 6 + c, Z1[c]);
+#pragma unroll
+            for (int i = 0; i < 6; ++i)
+#pragma unroll
+              for (int j = 0; j < 6; ++j) put(21 + 6 * i + j, -dot3(Z2[i] + 3, Z1[j]));
+            flush(1);
+            // window 2: (X_k, X_{k-1}), (X_k, X_k), g_{X_k}; z of the
+            // X_{k-1} columns recomputed rather than kept live
+            double Z0b[6][6];
+#pragma unroll
+            for (int c = 0; c < 6; ++c) z_column(L, C, c, Z0b[c]);
+#pragma unroll
+            for (int i = 0; i < 6; ++i)
+#pragma unroll
+              for (int j = 0; j < 6; ++j) put(6 * i + j, -dot3(Z1[i], Z0b[j] + 3));
+#pragma unroll
+            for (int i = 0; i < 6; ++i)
+#pragma unroll
+              for (int j = 0; j <= i; ++j) put(36 + i * (i + 1) / 2 + j, pose_entry(L, 6 + i, 6 + j) - dot3(Z1[i], Z1[j]));
+#pragma unroll
+            for (int i = 0; i < 6; ++i) put(57 + i, pose_grad(L, 6 + i) - dot3(Z1[i], zg + 3));
+            flush(2);
+          }
+          if (solved) {
+#pragma unroll
+            for (int grp = 0; grp < 3; ++grp) {
+              if (lane >= kWin) continue;
+              int a, b;
+              if (lane >= 57) {
+                sh.g[(grp == 0 ? 12 : grp == 1 ? 0 : 6) + lane - 57] = acc[grp];
+                continue;
+              }
+              if (grp == 2 && lane < 36) {
+                a = 6 + lane / 6;
+                b = lane % 6;
+              } else if (grp < 2 && lane >= 21) {
+                a = 12 + (lane - 21) / 6;
+                b = (grp == 0 ? 0 : 6) + (lane - 21) % 6;
               } else {
-#pragma unroll
-                for (int i = 0; i < 6; ++i) w[i] = 0.0;
+                const int k = grp == 2 ? lane - 36 : lane;
+                const int r = static_cast<int>((sqrt(8.0 * k + 1.0) - 1.0) * 0.5);
+                const int off = grp == 0 ? 12 : grp == 1 ? 0 : 6;
+                a = off + r;
+                b = off + k - r * (r + 1) / 2;
               }
-#pragma unroll
-              for (int i = 0; i < 6; ++i) Y[i][a] = w[i];
-            }
-            double yg[6] = {0, 0, 0, 0, 0, 0};
-            if (have) {
-              point_grad(L, yg);
-              point_solve(C, yg);
-            }
-#pragma unroll
-            for (int a = 0; a < 18; ++a) {
-              double wa[6] = {0, 0, 0, 0, 0, 0};
-              if (have) w_column(L, a, wa);
-#pragma unroll
-              for (int b = 0; b < 18; ++b) {
-                if (b > a) continue;
-                double v = 0.0;
-                if (have) {
-                  v = pose_entry(L, a, b);
-#pragma unroll
-                  for (int i = 0; i < 6; ++i) v -= wa[i] * Y[i][b];
-                }
-                v = wave_sum(v);
-                if (lane == 0) sh.S[18 * a + b] += v;
-              }
-              double v = 0.0;
-              if (have) {
-                v = pose_grad(L, a);
-#pragma unroll
-                for (int i = 0; i < 6; ++i) v -= wa[i] * yg[i];
-              }
-              v = wave_sum(v);
-              if (lane == 0) sh.g[a] += v;
+              sh.S[18 * a + b] = acc[grp];
             }
           }
           __syncthreads();
-          if (solved && lane == 0) {
-            // priors (J = I / sigma) and damping, then Cholesky of the 18x18
+          // priors (J = I / sigma) and damping, then the 18x18 Cholesky in
+          // registers: lane i < 18 holds row i; column k is broadcast with
+          // readlane. Solves: forward on the rows, backward on the columns
+          // (read back from LDS).
+          if (solved) {
+            const int i = lane < 18 ? lane : 17;
+            double r[18];
+#pragma unroll
+            for (int j = 0; j < 18; ++j) r[j] = j <= i ? sh.S[18 * i + j] : 0.0;
+            double gi = sh.g[i];
             const double ip2 = B.isig_prior * B.isig_prior;
-            for (int i = 0; i < 12; ++i) {
-              sh.S[19 * i] += ip2;
-              sh.g[i] += B.isig_prior * sh.bprior[i];
-            }
-            for (int i = 0; i < 18; ++i) sh.S[19 * i] += lambda;
-            int fail = 0;
-            for (int k = 0; k < 18 && !fail; ++k) {
-              double d = sh.S[19 * k];
-              for (int m = 0; m < k; ++m) d -= sh.S[18 * k + m] * sh.S[18 * k + m];
+#pragma unroll
+            for (int j = 0; j < 18; ++j)
+              if (j == lane) {
+                if (j < 12) {
+                  r[j] += ip2;
+                  gi += B.isig_prior * sh.bprior[j];
+                }
+                r[j] += lambda;
+              }
+            bool fail = false;
+#pragma unroll
+            for (int k = 0; k < 18; ++k) {
+              const double d = read_lane(r[k], k);
               if (!(d > 0.0)) {
-                fail = 1;
+                fail = true;
                 break;
               }
-              d = sqrt(d);
-              sh.S[19 * k] = d;
-              for (int i = k + 1; i < 18; ++i) {
-                double s = sh.S[18 * i + k];
-                for (int m = 0; m < k; ++m) s -= sh.S[18 * i + m] * sh.S[18 * k + m];
-                sh.S[18 * i + k] = s / d;
+              const double ld = sqrt(d);
+              r[k] = lane == k ? ld : r[k] / ld;
+#pragma unroll
+              for (int j = k + 1; j < 18; ++j) {
+                const double ljk = read_lane(r[k], j);
+                if (lane >= j) r[j] -= r[k] * ljk;
               }
             }
-            if (!fail) {
-              double x[18];
-              for (int i = 0; i < 18; ++i) {
-                double s = sh.g[i];
-                for (int m = 0; m < i; ++m) s -= sh.S[18 * i + m] * x[m];
-                x[i] = s / sh.S[19 * i];
+            if (fail) {
+              solved = false;
+            } else {
+#pragma unroll
+              for (int k = 0; k < 18; ++k) {
+                if (lane == k) gi = gi / r[k];
+                const double yk = read_lane(gi, k);
+                if (lane > k) gi -= r[k] * yk;
               }
-              for (int i = 17; i >= 0; --i) {
-                double s = x[i];
-                for (int m = i + 1; m < 18; ++m) s -= sh.S[18 * m + i] * x[m];
-                x[i] = s / sh.S[19 * i];
+              if (lane < 18) {
+#pragma unroll
+                for (int j = 0; j < 18; ++j)
+                  if (j <= lane) sh.S[18 * lane + j] = r[j];
               }
-              for (int i = 0; i < 18; ++i) sh.dx[i] = x[i];
+              __syncthreads();
+              double ct[18];  // column `lane` of L
+#pragma unroll
+              for (int m = 0; m < 18; ++m) ct[m] = (m >= i) ? sh.S[18 * m + i] : 0.0;
+#pragma unroll
+              for (int m = 17; m >= 0; --m) {
+                if (lane == m) gi = gi / ct[m];
+                const double xm = read_lane(gi, m);
+                if (lane < m) gi -= ct[m] * xm;
+              }
+              if (lane < 18) sh.dx[lane] = gi;
             }
-            sh.fail = fail;
           }
           __syncthreads();
-          if (solved && sh.fail) solved = false;
           // back-substitution, linearised error at delta, candidate points
           double newLin = 0.0;
           if (solved) {
