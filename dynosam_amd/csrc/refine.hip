@@ -23,7 +23,9 @@
 // launch per batch, no host round trip per iteration.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cfloat>
+#include <cstdio>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -36,7 +38,8 @@ namespace {
 constexpr int kWave = 64;
 constexpr int kLin = 80;  // linearisation scratch per tracklet (doubles)
 constexpr int kWin = 63;  // reduction window: 57 system entries + 6 gradient entries
-constexpr int kRedLd = kWave + 1;
+constexpr int kQuads = kWave / 4;  // reduction columns: quad sums
+constexpr int kRedLd = kQuads + 1;
 constexpr double kChi2_3_099 = 11.344866730144373;  // boost chi_squared quantile(3, 0.99)
 
 struct Pose {
@@ -252,6 +255,20 @@ __device__ __forceinline__ double read_lane(double v, int src) {
   return __longlong_as_double((static_cast<unsigned long long>(hi) << 32) | lo);
 }
 
+// v from the lane given by the DPP quad permutation CTRL
+template <int CTRL>
+__device__ __forceinline__ double quad_perm(double v) {
+  const unsigned long long u = __double_as_longlong(v);
+  const unsigned lo = __builtin_amdgcn_mov_dpp(static_cast<int>(u), CTRL, 0xF, 0xF, false);
+  const unsigned hi = __builtin_amdgcn_mov_dpp(static_cast<int>(u >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double((static_cast<unsigned long long>(hi) << 32) | lo);
+}
+// (v0 + v1) + (v2 + v3) over the lane's quad, identical on its four lanes
+__device__ __forceinline__ double quad_sum(double v) {
+  v += quad_perm<0xB1>(v);     // [1, 0, 3, 2]
+  return v + quad_perm<0x4E>(v);  // [2, 3, 0, 1]
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
@@ -399,6 +416,7 @@ struct Batch {
   uint8_t* active;  // the tracklet's ternary factor is in the graph
   uint8_t* outlier;
   double* H_out;
+  long long* prof;  // DYNOREFINE_PROFILE builds: 8 phase tick counters per problem
   dynorefine_result* res;
   double isig_proj, isig_motion, hk, isig_prior;
   int outlier_reject;
@@ -412,7 +430,7 @@ struct Shared {
   double g[18];
   double dx[18];
   double bprior[12];
-  double red[kWave * kRedLd];  // cross-lane reduction of S: [entry][lane]
+  double red[kWin * kRedLd];  // cross-lane reduction of S: [entry][quad]
 };
 
 __device__ double total_error(const Batch& B, const Shared& sh, const double* Kp, int pb, int pt, int t0, int t1,
@@ -471,7 +489,22 @@ void k_refine(Batch B) {
   }
   __syncthreads();
   int pb = 0, pt = 0;  // current pose / point buffers
+#ifdef DYNOREFINE_PROFILE
+  long long pt_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  long long pt_t = clock64();
+#define RPROF(k)                  \
+  do {                            \
+    const long long n_ = clock64(); \
+    pt_acc[k] += n_ - pt_t;       \
+    pt_t = n_;                    \
+  } while (0)
+#else
+#define RPROF(k) \
+  do {           \
+  } while (0)
+#endif
   double err = total_error(B, sh, Kp, pb, pt, t0, t1, lane);
+  RPROF(0);
   const double err0 = err;
   int it_total = 0, inner_total = 0, status = DYNOREFINE_OK, n_outliers = 0;
   const double lambda_f = prm.lambda_factor;
@@ -517,6 +550,7 @@ void k_refine(Batch B) {
         __syncthreads();
         for (int i = 0; i < 12; ++i) oldLin += 0.5 * sh.bprior[i] * sh.bprior[i];
 
+        RPROF(1);
         // ---- tryLambda until accepted, gave up or stopped ----
         for (;;) {
           // reduced system: sum_i (B_i - W_i^T C_i^-1 W_i), g_pose - W_i^T C_i^-1 g_i,
@@ -525,9 +559,9 @@ void k_refine(Batch B) {
           // m_{k-1} only, X_k columns m_k only), so z of an X_k column has its
           // top three rows zero. The 171 entries + 18 gradient entries are
           // emitted in three windows of 63 (whole block pairs each, so that
-          // only two z blocks are live at a time) and reduced through LDS:
-          // every lane stores its contribution (red[entry][lane]), then lane
-          // e sums row e in lane order (fixed order: bit-reproducible).
+          // only two z blocks are live at a time) and reduced in two stages:
+          // quad sums by DPP, stored to LDS (red[entry][quad]), then lane e
+          // sums row e in quad order (fixed order: bit-reproducible).
           double acc[3] = {0.0, 0.0, 0.0};
           bool solved = true;
           auto flush = [&](int grp) {
@@ -536,7 +570,7 @@ void k_refine(Batch B) {
               const double* row = sh.red + lane * kRedLd;
               double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
 #pragma unroll
-              for (int j = 0; j < kWave; j += 4) {
+              for (int j = 0; j < kQuads; j += 4) {
                 s0 += row[j];
                 s1 += row[j + 1];
                 s2 += row[j + 2];
@@ -556,7 +590,10 @@ void k_refine(Batch B) {
               solved = false;
               break;
             }
-            auto put = [&](int idx, double v) { sh.red[idx * kRedLd + lane] = have ? v : 0.0; };
+            auto put = [&](int idx, double v) {
+              v = quad_sum(have ? v : 0.0);
+              if ((lane & 3) == 0) sh.red[idx * kRedLd + (lane >> 2)] = v;
+            };
             double zg[6];
             point_grad(L, zg);
             lower_solve(C, zg);
@@ -636,6 +673,7 @@ void k_refine(Batch B) {
             }
           }
           __syncthreads();
+          RPROF(2);
           // priors (J = I / sigma) and damping, then the 18x18 Cholesky in
           // registers: lane i < 18 holds row i; column k is broadcast with
           // readlane. Solves: forward on the rows, backward on the columns
@@ -700,6 +738,7 @@ void k_refine(Batch B) {
             }
           }
           __syncthreads();
+          RPROF(3);
           // back-substitution, linearised error at delta, candidate points
           double newLin = 0.0;
           if (solved) {
@@ -761,7 +800,9 @@ void k_refine(Batch B) {
                 store_pose(sh.X[1 - pb][lane], Tn);
               }
               __syncthreads();
+              RPROF(4);
               newErr = total_error(B, sh, Kp, 1 - pb, 1 - pt, t0, t1, lane);
+              RPROF(5);
               const double costChange = err - newErr;
               if (linChange > DBL_EPSILON * oldLin) step_ok = costChange / linChange > prm.min_model_fidelity;
               if (fabs(costChange) < prm.relative_error_tol * err) stop = true;
@@ -841,6 +882,15 @@ void k_refine(Batch B) {
     __syncthreads();
     err = total_error(B, sh, Kp, pb, pt, t0, t1, lane);
   }
+  RPROF(6);
+#ifdef DYNOREFINE_PROFILE
+  if (lane < 8) {
+    long long v = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v = lane == k ? pt_acc[k] : v;
+    B.prof[8 * prob + lane] = v;
+  }
+#endif
   if (lane < 12) B.H_out[12 * prob + lane] = sh.X[pb][2][lane];
   if (lane == 0) {
     dynorefine_result r;
@@ -1032,6 +1082,12 @@ int dynorefine_solve(dynorefine_solver* s, const dynorefine_params* p, const dyn
   B.outlier = s->outlier.p;
   B.H_out = s->Hout.p;
   B.res = s->res.p;
+  B.prof = nullptr;
+#ifdef DYNOREFINE_PROFILE
+  DevBuf<long long> prof;
+  RCHK(s, prof.alloc(8 * s->n_prob));
+  B.prof = prof.p;
+#endif
   B.isig_proj = 1.0 / prm.projection_sigma;
   B.isig_motion = 1.0 / prm.landmark_motion_sigma;
   B.hk = prm.k_huber;
@@ -1044,6 +1100,19 @@ int dynorefine_solve(dynorefine_solver* s, const dynorefine_params* p, const dyn
   RCHK(s, hipEventRecord(s->ev[1], s->stream));
   RCHK(s, hipEventSynchronize(s->ev[1]));
   RCHK(s, hipEventElapsedTime(&s->last_ms, s->ev[0], s->ev[1]));
+#ifdef DYNOREFINE_PROFILE
+  {
+    std::vector<long long> h(8 * s->n_prob);
+    RCHK(s, hipMemcpy(h.data(), prof.p, h.size() * sizeof(long long), hipMemcpyDeviceToHost));
+    double tot[8] = {0};
+    for (size_t p = 0; p < s->n_prob; ++p)
+      for (int k = 0; k < 8; ++k) tot[k] += static_cast<double>(h[8 * p + k]);
+    std::fprintf(stderr, "[refine profile] mean clock64 ticks per problem:");
+    const char* names[8] = {"init_error", "linearize", "schur", "solve18", "backsub", "new_error", "rest", "-"};
+    for (int k = 0; k < 7; ++k) std::fprintf(stderr, " %s=%.0f", names[k], tot[k] / std::max<size_t>(1, s->n_prob));
+    std::fprintf(stderr, "\n");
+  }
+#endif
   s->solved = true;
   return DYNOHIP_OK;
 }
