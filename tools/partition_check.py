@@ -5,12 +5,27 @@ Launch one process per rank:
       --master-port P tools/partition_check.py --config C2 [--backend gloo|nccl]
 
 Ranks use GPU local_rank % device_count, so N ranks may share one GPU (then
-use --backend gloo: RCCL does not put two ranks on one device). Every rank
-runs the partitioned optimize(); rank 0 then runs the ordinary single-handle
-optimize() on the same graph and prints one JSON line comparing them: LM
-iteration counts, the per-attempt trace (lambda, errors, accept flags) and
-the final values (relative Frobenius norm). Exit code 1 on a mismatch beyond
---tol.
+use --backend gloo: RCCL does not put two ranks on one device).
+
+Two comparisons, both against the ordinary single-handle solve of the same
+graph on rank 0:
+
+* conditioned (the north-star bar, "1e-6 relative Frobenius per LM
+  iteration"): before every outer iteration every handle is put on the
+  single handle's values and lambda, runs ONE iterate(), and the resulting
+  values are compared. This isolates one linearise + damped solve + retract
+  per comparison, so rounding drift cannot accumulate. A control handle (the
+  single-GPU solver with a different nested-dissection tile ordering, i.e.
+  the same arithmetic in a different summation order) is run the same way:
+  it measures how much of any difference is summation order alone.
+* free-running: every rank runs optimize(); LM iteration counts, the accept
+  sequence and the final values are compared. On ill-conditioned graphs
+  (prior sigma 1e-4, ternary sigma 1e-5, Huber k 1e-4) trajectories drift
+  apart in the last bits; the control handle's free run shows the size of
+  that drift for a pure reordering.
+
+Prints one JSON line (rank 0); exit code 1 when the conditioned comparison
+misses --tol or the free run changes iteration counts / accept sequence.
 """
 import argparse
 import json
@@ -24,20 +39,29 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def rel(a, b):
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="C2")
     ap.add_argument("--backend", default="gloo")
     ap.add_argument("--tol", type=float, default=1e-6)
     ap.add_argument("--max-iterations", type=int, default=100)
+    ap.add_argument("--conditioned", type=int, default=-1,
+                    help="outer iterations of the conditioned comparison (-1: as many as the free run)")
+    ap.add_argument("--control-leaf", type=int, default=2,
+                    help="nested-dissection leaf size of the control handle's tile ordering")
+    ap.add_argument("--no-free", action="store_true", help="skip the free-running comparison")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     import torch
     import torch.distributed as dist
 
     from dynosam_amd import _abi, synth
-    from dynosam_amd.optimizer import LevenbergMarquardtOptimizer
-    from dynosam_amd.partitioned import PartitionedLevenbergMarquardtOptimizer
+    from dynosam_amd.optimizer import Solver, set_tile_ordering
+    from dynosam_amd.partitioned import PartitionedSolver, TorchAllReduce
 
     dist.init_process_group(backend=args.backend)
     rank, world = dist.get_rank(), dist.get_world_size()
@@ -46,48 +70,143 @@ def main():
     graph, values, _ = synth.generate(args.config)
     params = _abi.LMParams.gtsam_default()
     params.max_iterations = args.max_iterations
+
+    def lm_params(lam):
+        p = _abi.LMParams.gtsam_default()
+        p.max_iterations = args.max_iterations
+        p.lambda_initial = lam
+        return p
+
     t0 = time.perf_counter()
-    opt = PartitionedLevenbergMarquardtOptimizer(graph, values, params, device=dev)
+    ar = TorchAllReduce(dev)
+    part = PartitionedSolver(dev, world, rank, ar)
+    part.set_graph(graph)
+    part.set_values(values)
     t1 = time.perf_counter()
-    out = opt.optimize()
-    t2 = time.perf_counter()
-    owner, xdoubles = opt.solver.value_owner()
-    trace = opt.trace()
-    summ = opt.summary()
-    local_factors = None
-    st = opt.solver.stats()
-    local_factors = st.get("n_factor")
-    counts = [None] * world
-    dist.all_gather_object(counts, {"rank": rank, "factors": local_factors, "points": st.get("n_point"),
-                                    "calls": opt.allreduce.calls, "doubles": opt.allreduce.doubles})
-    ok = True
+    res = {"config": args.config, "ranks": world, "backend": args.backend, "s_setup": t1 - t0}
+    ref = ctrl = None
     if rank == 0:
-        ref_opt = LevenbergMarquardtOptimizer(graph, values, params, device=dev)
+        ref = Solver(dev)
+        ref.set_graph(graph)
+        ref.set_values(values)
+        set_tile_ordering(args.control_leaf)
+        ctrl = Solver(dev)
+        ctrl.set_graph(graph)
+        ctrl.set_values(values)
+        set_tile_ordering(-1)
+
+    # ---- free-running ----
+    ok_free = True
+    if not args.no_free:
+        t2 = time.perf_counter()
+        sp = part.optimize(params)
         t3 = time.perf_counter()
-        ref = ref_opt.optimize()
-        t4 = time.perf_counter()
-        rtrace = ref_opt.trace()
-        rel = float(np.linalg.norm(out.data - ref.data) / np.linalg.norm(ref.data))
-        n = min(len(trace), len(rtrace))
-        # the error trajectory: accepted steps (a rejected trial point at a
-        # small lambda is far from the solution and its error is as
-        # ill-conditioned as the step; reported separately)
-        def rel_err(acc):
-            return max((abs(a["new_error"] - b["new_error"]) / max(abs(b["new_error"]), 1e-300)
-                        for a, b in zip(trace[:n], rtrace[:n])
-                        if np.isfinite(b["new_error"]) and (b["accepted"] or not acc)), default=0.0)
-        err_rel = rel_err(True)
-        err_rel_all = rel_err(False)
-        same_accepts = [a["accepted"] for a in trace] == [b["accepted"] for b in rtrace]
-        ok = (summ.iterations == ref_opt.iterations() and same_accepts and rel < args.tol and err_rel < args.tol)
-        res = {"config": args.config, "ranks": world, "backend": args.backend, "ok": bool(ok),
-               "iterations": [summ.iterations, ref_opt.iterations()],
-               "inner": [summ.inner_iterations, ref_opt.getInnerIterations()],
-               "final_error": [summ.final_error, ref_opt.summary().final_error],
-               "values_rel_frobenius": rel, "trace_error_rel_max": err_rel, "trial_error_rel_max": err_rel_all, "same_accept_sequence": same_accepts,
-               "exchange_doubles_per_solve": int(xdoubles),
-               "replicated_values": int((owner < 0).sum()), "per_rank": counts,
-               "s_setup": t1 - t0, "s_optimize_partitioned": t2 - t1, "s_optimize_single": t4 - t3}
+        out = part.gathered_values_data()
+        trace = part.trace()
+        if rank == 0:
+            t4 = time.perf_counter()
+            sr = ref.optimize(params)
+            t5 = time.perf_counter()
+            sc = ctrl.optimize(params)
+            rtrace, ctrace = ref.trace(), ctrl.trace()
+            rv, cv = ref.values_data(), ctrl.values_data()
+
+            def err_rel(a_tr, b_tr):
+                n = min(len(a_tr), len(b_tr))
+                return max((abs(a["new_error"] - b["new_error"]) / max(abs(b["new_error"]), 1e-300)
+                            for a, b in zip(a_tr[:n], b_tr[:n]) if np.isfinite(b["new_error"]) and b["accepted"]),
+                           default=0.0)
+
+            same_acc = [a["accepted"] for a in trace] == [b["accepted"] for b in rtrace]
+            ok_free = sp.iterations == sr.iterations and sp.inner_iterations == sr.inner_iterations and same_acc
+            res["free"] = {
+                "iterations": [sp.iterations, sr.iterations, sc.iterations],
+                "inner": [sp.inner_iterations, sr.inner_iterations, sc.inner_iterations],
+                "final_error": [sp.final_error, sr.final_error, sc.final_error],
+                "same_accept_sequence": same_acc,
+                "values_rel_frobenius": rel(out, rv),
+                "accepted_error_rel_max": err_rel(trace, rtrace),
+                "control_values_rel_frobenius": rel(cv, rv),
+                "control_accepted_error_rel_max": err_rel(ctrace, rtrace),
+                "control_same_accept_sequence": [a["accepted"] for a in ctrace] == [b["accepted"] for b in rtrace],
+                "s_optimize_partitioned": t3 - t2, "s_optimize_single": t5 - t4,
+                "order": "[partitioned, single, control]"}
+
+    # ---- conditioned per outer iteration ----
+    ok_cond = True
+    n_cond = args.conditioned
+    if n_cond != 0:
+        if n_cond < 0:
+            n_cond = res.get("free", {}).get("iterations", [0, 0])[1] or 10
+            n_cond = int(torch.tensor([n_cond]).item())
+        nb = torch.tensor([n_cond], dtype=torch.int64)
+        dist.broadcast(nb, 0)
+        n_cond = int(nb.item())
+        state = torch.from_numpy(values.data.copy())
+        lam = 1e-5
+        rows = []
+        for it in range(n_cond):
+            dist.broadcast(state, 0)
+            lt = torch.tensor([lam], dtype=torch.float64)
+            dist.broadcast(lt, 0)
+            lam = float(lt.item())
+            v_it = values.with_data(state.numpy().copy())
+            part.set_values(v_it)
+            part.reset(lm_params(lam))
+            sp = part.iterate()
+            pv = part.gathered_values_data()
+            if rank == 0:
+                row = {"it": it, "lambda": lam}
+                outs = {}
+                for name, h in (("single", ref), ("control", ctrl)):
+                    h.set_values(v_it)
+                    h.reset(lm_params(lam))
+                    s = h.iterate()
+                    outs[name] = (s, h.values_data())
+                sr, rv = outs["single"]
+                sc, cv = outs["control"]
+                step = np.linalg.norm(rv - v_it.data)
+                row.update({
+                    "inner": [sp.inner_iterations, sr.inner_iterations, sc.inner_iterations],
+                    "accepted": [sp.iterations, sr.iterations, sc.iterations],
+                    "error": [sp.final_error, sr.final_error, sc.final_error],
+                    "values_rel": rel(pv, rv), "control_values_rel": rel(cv, rv),
+                    "step_rel": rel(pv - v_it.data, rv - v_it.data) if step > 0 else 0.0,
+                    "control_step_rel": rel(cv - v_it.data, rv - v_it.data) if step > 0 else 0.0,
+                    "error_rel": abs(sp.final_error - sr.final_error) / max(abs(sr.final_error), 1e-300)})
+                rows.append(row)
+                state = torch.from_numpy(rv.copy())
+                lam = sr.final_lambda
+                if sr.iterations == 0:   # no accepted step: LM stops here
+                    n_stop = torch.tensor([1])
+                else:
+                    n_stop = torch.tensor([0])
+            else:
+                n_stop = torch.tensor([0])
+            dist.broadcast(n_stop, 0)
+            if int(n_stop.item()):
+                break
+        if rank == 0:
+            vmax = max((r["values_rel"] for r in rows), default=0.0)
+            cmax = max((r["control_values_rel"] for r in rows), default=0.0)
+            same = all(r["inner"][0] == r["inner"][1] and r["accepted"][0] == r["accepted"][1] for r in rows)
+            ok_cond = same and vmax < args.tol
+            res["conditioned"] = {"iterations": len(rows), "values_rel_max": vmax,
+                                  "control_values_rel_max": cmax,
+                                  "step_rel_max": max((r["step_rel"] for r in rows), default=0.0),
+                                  "control_step_rel_max": max((r["control_step_rel"] for r in rows), default=0.0),
+                                  "error_rel_max": max((r["error_rel"] for r in rows), default=0.0),
+                                  "same_inner_and_accepts": same, "rows": rows}
+    owner, xdoubles = part.value_owner()
+    st = part.stats()
+    counts = [None] * world
+    dist.all_gather_object(counts, {"rank": rank, "factors": st.get("n_factor"), "points": st.get("n_point"),
+                                    "calls": ar.calls, "doubles": ar.doubles})
+    ok = ok_free and ok_cond
+    if rank == 0:
+        res.update({"ok": bool(ok), "ok_conditioned": bool(ok_cond), "ok_free_counts": bool(ok_free),
+                    "tol": args.tol, "exchange_doubles_per_solve": int(xdoubles),
+                    "replicated_values": int((owner < 0).sum()), "per_rank": counts})
         line = json.dumps(res)
         print(line, flush=True)
         if args.out:
