@@ -115,6 +115,8 @@ class Stats(C.Structure):
         ("ms_retract_error", C.c_double),
         ("n_linearize", C.c_int64),
         ("n_solves", C.c_int64),
+        ("lin_bytes_read", C.c_double),
+        ("lin_bytes_impl", C.c_double),
     ]
 
     def as_dict(self):

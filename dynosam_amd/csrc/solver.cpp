@@ -443,10 +443,12 @@ int enqueue_try(dynohip_solver* s, double lambda) {
                         s->side, s->ev_main, s->ev_side);
     launch_tile_backward(s->bd, s->sd, P.bplevel, s->linv.p, y, x, s->failp, st);
   } else {
-    launch_tile_cholesky_solve(s->bd, s->sd, P.flevel, P.fpanels, P.bplevel, s->linv.p, s->gred.p, s->contrib.p, y,
-                               x, s->failp, st, s->side, s->ev_main, s->ev_side);
+    launch_tile_forward(s->bd, s->sd, P.flevel, P.fpanels, s->linv.p, s->gred.p, s->contrib.p, y, s->failp, st,
+                        s->side, s->ev_main, s->ev_side);
+    if (timed) (void)hipEventRecord(s->ev[5], st);
+    launch_tile_backward(s->bd, s->sd, P.bplevel, s->linv.p, y, x, s->failp, st);
   }
-  if (timed) (void)hipEventRecord(s->ev[5], st);
+  if (timed && s->nranks > 1) (void)hipEventRecord(s->ev[5], st);
   if (timed) (void)hipEventRecord(s->ev[6], st);
   // pose deltas are x[0 .. 6 n_pose) in pose-index order
   launch_backsub(s->cd, P.n_edge, A, x, s->wdx.p, s->dpt.p, st);
@@ -475,15 +477,36 @@ void compute_base_stats(dynohip_solver* s) {
   st.chol_levels = P.flevel.empty() ? 0 : static_cast<int64_t>(P.flevel.size()) - 1;
   st.back_levels = P.blevel.empty() ? 0 : static_cast<int64_t>(P.blevel.size()) - 1;
   st.nd_leaf = P.nd_leaf;
-  double lin = 0.0;
+  // SURVEY.md §8(d) B_A: what one Jacobian assembly must read and write
+  double rd = 96.0 * P.n_pose + 24.0 * P.n_pt, impl = 0.0;
+  std::vector<uint64_t> pp;   // distinct pose-pose pairs of multi-pose factors
   for (int t = 0; t < kNTypes; ++t) {
     const TypePlan& tp = P.types[t];
     st.n_factor += tp.n;
-    double per = 4.0 * kNKeys[t] + 8.0 * kMeasDim[t] + 8.0 * kDim[t] + 8.0 + 8.0 * tp.stride;
+    rd += (4.0 * kNKeys[t] + 8.0 * kMeasDim[t]) * tp.n;
+    // the record implementation: indices, measurement, 1/sigma and Huber k
+    // and the slot values read, the J | b record written, then re-read by
+    // the point-side gathers
+    double per = 4.0 * kNKeys[t] + 8.0 * kMeasDim[t] + 8.0 * kDim[t] + 8.0 + 2.0 * 8.0 * tp.stride;
     for (int sl = 0; sl < kNKeys[t]; ++sl) per += kSlotKind[t][sl] == 0 ? 96.0 : 24.0;
-    lin += per * tp.n;
+    impl += per * tp.n;
+    for (int i = 0; i < tp.n; ++i)
+      for (int a = 0; a < kNKeys[t]; ++a)
+        for (int b = a + 1; b < kNKeys[t]; ++b)
+          if (kSlotKind[t][a] == 0 && kSlotKind[t][b] == 0) {
+            const uint64_t x = static_cast<uint32_t>(tp.idx[static_cast<size_t>(i) * kNKeys[t] + a]);
+            const uint64_t y = static_cast<uint32_t>(tp.idx[static_cast<size_t>(i) * kNKeys[t] + b]);
+            pp.push_back(x < y ? (x << 32 | y) : (y << 32 | x));
+          }
   }
-  st.lin_bytes = lin;
+  std::sort(pp.begin(), pp.end());
+  const double n_pp = static_cast<double>(std::unique(pp.begin(), pp.end()) - pp.begin());
+  const double wr = 8.0 * (9.0 * P.n_pt + 18.0 * P.n_edge + 9.0 * P.gE.ntargets() + 27.0 * P.n_pose + 36.0 * n_pp);
+  st.lin_bytes = rd + wr;
+  st.lin_bytes_read = rd;
+  // point-side block outputs (D, E, g_p, W) written by the gathers
+  impl += 8.0 * (9.0 * P.n_pt + 9.0 * P.gE.ntargets() + 3.0 * P.n_pt + 18.0 * P.n_edge);
+  st.lin_bytes_impl = impl;
   double asmb = 0.0;
   for (const GEntry& e : P.gRed.ent) asmb += 16.0 + 8.0 * e.k * 12.0;
   for (const GEntry& e : P.gGred.ent) asmb += 16.0 + 8.0 * e.k * 7.0;

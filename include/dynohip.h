@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define DYNOHIP_ABI_VERSION 1
+#define DYNOHIP_ABI_VERSION 2
 
 typedef enum {
   DYNOHIP_OK = 0,
@@ -207,16 +207,27 @@ typedef struct {
   int64_t chol_levels;       /* launches of the tile factorisation          */
   int64_t back_levels;       /* launches of the backward substitution       */
   int64_t nd_leaf;           /* nested-dissection leaf (tiles; 0 = none)    */
-  double lin_bytes;          /* algorithmic HBM bytes of one linearisation
-                                (factor records + values read, J|b written) */
+  double lin_bytes;          /* SURVEY.md §8(d) B_A: algorithmic HBM bytes of
+                                one Jacobian assembly (Phase A) = keys (4 B
+                                each) + measurements of every factor, every
+                                value once (96 B per pose, 24 B per point),
+                                and the block outputs (H_ll + g_l per point,
+                                H_lc per point-pose edge, m-m block per
+                                chain link, H_cc + g per pose, 6x6 per
+                                pose-pose pair)                              */
   double assembly_bytes;     /* algorithmic bytes of one reduced assembly
                                 (gather lists + blocks read, band written)  */
   double chol_flops;         /* algorithmic flops of one envelope Cholesky  */
   double chol_tile_flops;    /* flops actually issued by the tile algorithm */
-  /* accumulated device time (ms, HIP events) and counts since lm_reset */
+  /* accumulated device time (ms, HIP events) and counts since lm_reset.
+     ms_cholesky: the factorisation with the fused forward substitution
+     (k_factor_persist); ms_solve: the backward substitution. */
   double ms_linearize, ms_schur, ms_assembly, ms_cholesky, ms_solve,
          ms_backsub, ms_retract_error;
   int64_t n_linearize, n_solves;
+  double lin_bytes_read;     /* the read part of lin_bytes                  */
+  double lin_bytes_impl;     /* bytes the current Phase A kernels move by
+                                construction (records written and re-read) */
 } dynohip_stats;
 
 int dynohip_get_stats(dynohip_solver* s, dynohip_stats* out);

@@ -2,9 +2,18 @@
  * oracle.c — CPU restatement of the DynoSAM backend hot path (see oracle.h).
  *
  * TEST INFRASTRUCTURE ONLY: the parity checker, never the product.
- * Plain C99, FP64, single thread, no external libraries.
+ * Plain C99, FP64, no external libraries. Single thread by default; with
+ * oracle_set_threads(p, n > 1) the same LM runs its linearisation, errors
+ * and Schur + envelope-Cholesky solve on n POSIX threads (the all-cores CPU
+ * baseline of bench.py, SURVEY.md §8(d) "CPU baseline"): the same
+ * operations, with the reductions split into fixed chunks and the envelope
+ * Cholesky blocked right-looking, so results agree with the single-thread
+ * path to rounding.
  */
+#define _POSIX_C_SOURCE 200809L
 #include "oracle.h"
+
+#include <pthread.h>
 
 #include <float.h>
 #include <math.h>
@@ -505,6 +514,11 @@ struct oracle_problem {
   int converged;
   dynohip_trace_entry* trace;
   size_t ntrace, captrace;
+  /* threaded solve (oracle_set_threads) */
+  int nthreads;
+  struct pool_t* pool;
+  size_t* comp_f_start;   /* factors touching each component (CSR) */
+  int* comp_f;
 };
 
 static void set_err(oracle_problem* p, const char* fmt, ...) {
@@ -809,6 +823,8 @@ void oracle_destroy(oracle_problem* p) {
   }
   free(p->comps); free(p->first); free(p->rowoff); free(p->sky); free(p->gc);
   free(p->trace);
+  oracle_set_threads(p, 1);
+  free(p->comp_f_start); free(p->comp_f);
   free(p);
 }
 
@@ -839,7 +855,9 @@ static double factor_error(const oracle_problem* p, const double* data, const fa
   return 0.5 * d2;
 }
 
+static double graph_error_mt(const oracle_problem* p, const double* data);
 static double graph_error(const oracle_problem* p, const double* data) {
+  if (p->nthreads > 1) return graph_error_mt(p, data);
   double s = 0.0;
   for (size_t f = 0; f < p->nf; ++f) s += factor_error(p, data, &p->f[f]);
   return s;
@@ -847,32 +865,36 @@ static double graph_error(const oracle_problem* p, const double* data) {
 double oracle_error(oracle_problem* p) { return graph_error(p, p->data); }
 
 /* NoiseModelFactor::linearize: b = -r, whiten, Huber block reweight */
-static void linearize_all(oracle_problem* p) {
-  for (size_t f = 0; f < p->nf; ++f) {
-    const factor_t* F = &p->f[f];
-    const double* v[4];
-    factor_vars(p, p->data, F, v);
-    const int d = kDim[F->type], cols = oracle_factor_cols(F->type);
-    double* A = p->A + p->foffA[f];
-    double* b = p->b + p->foffb[f];
-    double r[6];
-    eval_factor(F->type, v, F->meas, r, A);
-    double n2 = 0.0;
+static void linearize_one(oracle_problem* p, size_t f) {
+  const factor_t* F = &p->f[f];
+  const double* v[4];
+  factor_vars(p, p->data, F, v);
+  const int d = kDim[F->type], cols = oracle_factor_cols(F->type);
+  double* A = p->A + p->foffA[f];
+  double* b = p->b + p->foffb[f];
+  double r[6];
+  eval_factor(F->type, v, F->meas, r, A);
+  double n2 = 0.0;
+  for (int i = 0; i < d; ++i) {
+    b[i] = -r[i] * F->inv_sigma[i];
+    for (int j = 0; j < cols; ++j) A[i * cols + j] *= F->inv_sigma[i];
+    n2 += b[i] * b[i];
+  }
+  if (F->huber_k > 0.0) {
+    const double e = sqrt(n2);
+    const double w = e <= F->huber_k ? 1.0 : F->huber_k / e;
+    const double sw = sqrt(w);
     for (int i = 0; i < d; ++i) {
-      b[i] = -r[i] * F->inv_sigma[i];
-      for (int j = 0; j < cols; ++j) A[i * cols + j] *= F->inv_sigma[i];
-      n2 += b[i] * b[i];
-    }
-    if (F->huber_k > 0.0) {
-      const double e = sqrt(n2);
-      const double w = e <= F->huber_k ? 1.0 : F->huber_k / e;
-      const double sw = sqrt(w);
-      for (int i = 0; i < d; ++i) {
-        b[i] *= sw;
-        for (int j = 0; j < cols; ++j) A[i * cols + j] *= sw;
-      }
+      b[i] *= sw;
+      for (int j = 0; j < cols; ++j) A[i * cols + j] *= sw;
     }
   }
+}
+
+static void linearize_all_mt(oracle_problem* p);
+static void linearize_all(oracle_problem* p) {
+  if (p->nthreads > 1) { linearize_all_mt(p); return; }
+  for (size_t f = 0; f < p->nf; ++f) linearize_one(p, f);
 }
 
 size_t oracle_linearize_size(const oracle_problem* p) {
@@ -897,7 +919,29 @@ int oracle_linearize(oracle_problem* p, double* out, size_t n_doubles) {
 
 /* JacobianFactor::error summed: 0.5 * || A delta - b ||^2 ; delta per
    variable in value-data layout (6 per pose, 3 per point) via doff */
+/* the squared residual rows e_i^2 of factor f (at rows[foffb[f]..]) */
+static void linear_error_rows(const oracle_problem* p, size_t f, const double* delta, const size_t* doff,
+                              double* rows) {
+  const factor_t* F = &p->f[f];
+  const int d = kDim[F->type], cols = oracle_factor_cols(F->type);
+  const double* A = p->A + p->foffA[f];
+  const double* b = p->b + p->foffb[f];
+  for (int i = 0; i < d; ++i) {
+    double acc = 0.0;
+    if (delta) {
+      int c = 0;
+      for (int sl = 0; sl < kNKeys[F->type]; ++sl) {
+        const double* dv = delta + doff[F->var[sl]];
+        for (int j = 0; j < slot_dim(F->type, sl); ++j, ++c) acc += A[i * cols + c] * dv[j];
+      }
+    }
+    const double e = acc - b[i];
+    rows[p->foffb[f] + i] = e * e;
+  }
+}
+static double linear_error_mt(const oracle_problem* p, const double* delta, const size_t* doff);
 static double linear_error(const oracle_problem* p, const double* delta, const size_t* doff) {
+  if (p->nthreads > 1) return linear_error_mt(p, delta, doff);
   double s = 0.0;
   for (size_t f = 0; f < p->nf; ++f) {
     const factor_t* F = &p->f[f];
@@ -1150,8 +1194,10 @@ static size_t make_doff(const oracle_problem* p, size_t* doff) {
   return o;
 }
 
+static int solve_schur_mt(oracle_problem* p, double lambda, double* delta, const size_t* doff);
 static int solve_system(oracle_problem* p, double lambda, double* delta, const size_t* doff, size_t N) {
   if (p->dense) return solve_dense(p, lambda, delta, doff, N);
+  if (p->nthreads > 1) return solve_schur_mt(p, lambda, delta, doff);
   return solve_schur(p, lambda, delta, doff);
 }
 
@@ -1327,4 +1373,455 @@ int oracle_get_trace(const oracle_problem* p, dynohip_trace_entry* out, size_t c
   if (out && n) memcpy(out, p->trace, n * sizeof(dynohip_trace_entry));
   if (n_out) *n_out = p->ntrace;
   return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* Threaded LM (oracle_set_threads): the all-cores CPU baseline.       */
+/* Every parallel phase writes disjoint data; the sums that cross      */
+/* threads are formed from per-factor / per-row terms added in the     */
+/* serial order, and the envelope Cholesky subtracts its terms in the  */
+/* serial order too, so the trajectory is bit-identical to the single- */
+/* thread path.                                                        */
+/* ------------------------------------------------------------------ */
+typedef void (*task_fn)(void* ctx, int tid, int nt);
+struct pool_t {
+  int n;
+  pthread_t* th;
+  pthread_barrier_t start, end;
+  task_fn fn;
+  void* ctx;
+  int quit;
+};
+typedef struct { struct pool_t* pool; int tid; } worker_arg;
+
+static void* pool_worker(void* a) {
+  worker_arg* w = (worker_arg*)a;
+  struct pool_t* P = w->pool;
+  const int tid = w->tid;
+  free(w);
+  for (;;) {
+    pthread_barrier_wait(&P->start);
+    if (P->quit) break;
+    P->fn(P->ctx, tid, P->n);
+    pthread_barrier_wait(&P->end);
+  }
+  return NULL;
+}
+
+static void pool_run(struct pool_t* P, task_fn fn, void* ctx) {
+  P->fn = fn;
+  P->ctx = ctx;
+  pthread_barrier_wait(&P->start);
+  fn(ctx, 0, P->n);
+  pthread_barrier_wait(&P->end);
+}
+
+int oracle_set_threads(oracle_problem* p, int n) {
+  if (!p) return DYNOHIP_EINVAL;
+  if (p->pool) {
+    struct pool_t* P = p->pool;
+    P->quit = 1;
+    pthread_barrier_wait(&P->start);
+    for (int t = 1; t < P->n; ++t) pthread_join(P->th[t], NULL);
+    pthread_barrier_destroy(&P->start);
+    pthread_barrier_destroy(&P->end);
+    free(P->th);
+    free(P);
+    p->pool = NULL;
+  }
+  p->nthreads = n > 1 ? n : 1;
+  if (p->nthreads == 1) return 0;
+  struct pool_t* P = (struct pool_t*)calloc(1, sizeof(struct pool_t));
+  P->n = p->nthreads;
+  P->th = (pthread_t*)calloc((size_t)P->n, sizeof(pthread_t));
+  pthread_barrier_init(&P->start, NULL, (unsigned)P->n);
+  pthread_barrier_init(&P->end, NULL, (unsigned)P->n);
+  for (int t = 1; t < P->n; ++t) {
+    worker_arg* w = (worker_arg*)malloc(sizeof(worker_arg));
+    w->pool = P;
+    w->tid = t;
+    pthread_create(&P->th[t], NULL, pool_worker, w);
+  }
+  p->pool = P;
+  /* factors touching each component (a factor's points share one) */
+  if (!p->comp_f_start) {
+    p->comp_f_start = (size_t*)calloc((size_t)p->ncomp + 1, sizeof(size_t));
+    int* fc = (int*)malloc((p->nf ? p->nf : 1) * sizeof(int));
+    for (size_t f = 0; f < p->nf; ++f) {
+      const factor_t* F = &p->f[f];
+      fc[f] = -1;
+      for (int sl = 0; sl < kNKeys[F->type]; ++sl)
+        if (kSlotKind[F->type][sl] == 1) fc[f] = p->comp_of[F->var[sl]];
+      if (fc[f] >= 0) p->comp_f_start[fc[f] + 1]++;
+    }
+    for (int c = 0; c < p->ncomp; ++c) p->comp_f_start[c + 1] += p->comp_f_start[c];
+    p->comp_f = (int*)malloc((p->comp_f_start[p->ncomp] ? p->comp_f_start[p->ncomp] : 1) * sizeof(int));
+    size_t* fill = (size_t*)malloc(((size_t)p->ncomp + 1) * sizeof(size_t));
+    memcpy(fill, p->comp_f_start, ((size_t)p->ncomp + 1) * sizeof(size_t));
+    for (size_t f = 0; f < p->nf; ++f)
+      if (fc[f] >= 0) p->comp_f[fill[fc[f]]++] = (int)f;
+    free(fill);
+    free(fc);
+  }
+  return 0;
+}
+
+static void chunk(size_t n, int tid, int nt, size_t* lo, size_t* hi) {
+  *lo = n * (size_t)tid / (size_t)nt;
+  *hi = n * (size_t)(tid + 1) / (size_t)nt;
+}
+
+typedef struct {
+  oracle_problem* p;
+  const double* data;
+  const double* delta;
+  const size_t* doff;
+  double* terms;
+  double lambda;
+  int* tfail;
+  size_t j0, j1, ilo, ihi;
+} mt_ctx;
+
+static void t_linearize(void* c, int tid, int nt) {
+  mt_ctx* x = (mt_ctx*)c;
+  size_t lo, hi;
+  chunk(x->p->nf, tid, nt, &lo, &hi);
+  for (size_t f = lo; f < hi; ++f) linearize_one(x->p, f);
+}
+static void linearize_all_mt(oracle_problem* p) {
+  mt_ctx x;
+  memset(&x, 0, sizeof(x));
+  x.p = p;
+  pool_run(p->pool, t_linearize, &x);
+}
+
+static void t_error(void* c, int tid, int nt) {
+  mt_ctx* x = (mt_ctx*)c;
+  size_t lo, hi;
+  chunk(x->p->nf, tid, nt, &lo, &hi);
+  for (size_t f = lo; f < hi; ++f) x->terms[f] = factor_error(x->p, x->data, &x->p->f[f]);
+}
+static double graph_error_mt(const oracle_problem* p, const double* data) {
+  mt_ctx x;
+  memset(&x, 0, sizeof(x));
+  x.p = (oracle_problem*)p;
+  x.data = data;
+  x.terms = (double*)malloc((p->nf ? p->nf : 1) * sizeof(double));
+  pool_run(p->pool, t_error, &x);
+  double s = 0.0;
+  for (size_t f = 0; f < p->nf; ++f) s += x.terms[f];
+  free(x.terms);
+  return s;
+}
+
+static void t_linerr(void* c, int tid, int nt) {
+  mt_ctx* x = (mt_ctx*)c;
+  size_t lo, hi;
+  chunk(x->p->nf, tid, nt, &lo, &hi);
+  for (size_t f = lo; f < hi; ++f) linear_error_rows(x->p, f, x->delta, x->doff, x->terms);
+}
+static double linear_error_mt(const oracle_problem* p, const double* delta, const size_t* doff) {
+  size_t nrows = 0;
+  for (size_t f = 0; f < p->nf; ++f) nrows += (size_t)kDim[p->f[f].type];
+  mt_ctx x;
+  memset(&x, 0, sizeof(x));
+  x.p = (oracle_problem*)p;
+  x.delta = delta;
+  x.doff = doff;
+  x.terms = (double*)malloc((nrows ? nrows : 1) * sizeof(double));
+  pool_run(p->pool, t_linerr, &x);
+  double s = 0.0;
+  for (size_t r = 0; r < nrows; ++r) s += x.terms[r];
+  free(x.terms);
+  return 0.5 * s;
+}
+
+static int nb_index(const comp_t* C, int red) {
+  int lo = 0, hi = C->nnb - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (C->nb[mid] < red) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+/* zero the normal equations; each component's C, W, g_p from its own factors */
+static void t_comp_accumulate(void* c, int tid, int nt) {
+  mt_ctx* x = (mt_ctx*)c;
+  oracle_problem* p = x->p;
+  size_t lo, hi;
+  chunk(p->rowoff[p->ndim_red], tid, nt, &lo, &hi);
+  memset(p->sky + lo, 0, (hi - lo) * sizeof(double));
+  chunk(p->ndim_red, tid, nt, &lo, &hi);
+  memset(p->gc + lo, 0, (hi - lo) * sizeof(double));
+  for (int cc = tid; cc < p->ncomp; cc += nt) {
+    comp_t* C = &p->comps[cc];
+    const size_t n3 = 3 * (size_t)C->npts, m6 = 6 * (size_t)C->nnb;
+    memset(C->C, 0, n3 * n3 * sizeof(double));
+    memset(C->W, 0, n3 * m6 * sizeof(double));
+    memset(C->gp, 0, n3 * sizeof(double));
+    for (size_t q = p->comp_f_start[cc]; q < p->comp_f_start[cc + 1]; ++q) {
+      const size_t f = (size_t)p->comp_f[q];
+      const factor_t* F = &p->f[f];
+      const int d = kDim[F->type], cols = oracle_factor_cols(F->type), nk = kNKeys[F->type];
+      const double* A = p->A + p->foffA[f];
+      const double* b = p->b + p->foffb[f];
+      int c0 = 0;
+      for (int sa = 0; sa < nk; ++sa) {
+        const int da = slot_dim(F->type, sa);
+        if (kSlotKind[F->type][sa] != 1) { c0 += da; continue; }
+        int la = 0;
+        while (C->pts[la] != F->var[sa]) ++la;
+        for (int ia = 0; ia < da; ++ia) {
+          double s = 0.0;
+          for (int r = 0; r < d; ++r) s += A[r * cols + c0 + ia] * b[r];
+          C->gp[3 * la + ia] += s;
+        }
+        int c1 = 0;
+        for (int sb = 0; sb < nk; ++sb) {
+          const int db = slot_dim(F->type, sb);
+          const int vb = F->var[sb];
+          const int pb = kSlotKind[F->type][sb] == 1;
+          size_t lb = 0;
+          if (pb) { while (C->pts[lb] != vb) ++lb; }
+          else lb = (size_t)nb_index(C, p->red_of[vb]);
+          for (int ia = 0; ia < da; ++ia)
+            for (int ib = 0; ib < db; ++ib) {
+              double s = 0.0;
+              for (int r = 0; r < d; ++r) s += A[r * cols + c0 + ia] * A[r * cols + c1 + ib];
+              if (pb) C->C[(3 * (size_t)la + ia) * n3 + 3 * lb + ib] += s;
+              else C->W[(3 * (size_t)la + ia) * m6 + 6 * lb + ib] += s;
+            }
+          c1 += db;
+        }
+        c0 += da;
+      }
+    }
+  }
+}
+
+/* pose-side gradient and pose-pose blocks: thread t owns a range of
+   reduced poses (rows), every thread scans the factors in order */
+static void pose_range(const oracle_problem* p, int tid, int nt, int* lo, int* hi) {
+  size_t a, b;
+  chunk((size_t)p->npose, tid, nt, &a, &b);
+  *lo = (int)a;
+  *hi = (int)b;
+}
+static void t_pose_accumulate(void* c, int tid, int nt) {
+  mt_ctx* x = (mt_ctx*)c;
+  oracle_problem* p = x->p;
+  int plo, phi;
+  pose_range(p, tid, nt, &plo, &phi);
+  for (size_t f = 0; f < p->nf; ++f) {
+    const factor_t* F = &p->f[f];
+    const int d = kDim[F->type], cols = oracle_factor_cols(F->type), nk = kNKeys[F->type];
+    int mine = 0;
+    for (int sa = 0; sa < nk; ++sa)
+      if (kSlotKind[F->type][sa] == 0 && p->red_of[F->var[sa]] >= plo && p->red_of[F->var[sa]] < phi) mine = 1;
+    if (!mine) continue;
+    const double* A = p->A + p->foffA[f];
+    const double* b = p->b + p->foffb[f];
+    int c0 = 0;
+    for (int sa = 0; sa < nk; ++sa) {
+      const int da = slot_dim(F->type, sa);
+      const int va = F->var[sa];
+      if (kSlotKind[F->type][sa] != 0 || p->red_of[va] < plo || p->red_of[va] >= phi) { c0 += da; continue; }
+      for (int ia = 0; ia < da; ++ia) {
+        double s = 0.0;
+        for (int r = 0; r < d; ++r) s += A[r * cols + c0 + ia] * b[r];
+        p->gc[6 * (size_t)p->red_of[va] + ia] += s;
+      }
+      int c1 = 0;
+      for (int sb = 0; sb < nk; ++sb) {
+        const int db = slot_dim(F->type, sb);
+        const int vb = F->var[sb];
+        if (kSlotKind[F->type][sb] == 0)
+          for (int ia = 0; ia < da; ++ia)
+            for (int ib = 0; ib < db; ++ib) {
+              const size_t gi = 6 * (size_t)p->red_of[va] + ia, gj = 6 * (size_t)p->red_of[vb] + ib;
+              if (gi < gj) continue;
+              double s = 0.0;
+              for (int r = 0; r < d; ++r) s += A[r * cols + c0 + ia] * A[r * cols + c1 + ib];
+              *sky_at(p, gi, gj) += s;
+            }
+        c1 += db;
+      }
+      c0 += da;
+    }
+  }
+  for (size_t i = 6 * (size_t)plo; i < 6 * (size_t)phi; ++i) *sky_at(p, i, i) += x->lambda;
+}
+
+static void t_comp_factor(void* c, int tid, int nt) {
+  mt_ctx* x = (mt_ctx*)c;
+  oracle_problem* p = x->p;
+  for (int cc = tid; cc < p->ncomp; cc += nt) {
+    comp_t* C = &p->comps[cc];
+    const size_t n3 = 3 * (size_t)C->npts, m6 = 6 * (size_t)C->nnb;
+    for (size_t i = 0; i < n3; ++i) C->C[i * n3 + i] += x->lambda;
+    if (!chol_dense(C->C, n3)) { x->tfail[tid] = 1; continue; }
+    memcpy(C->Y, C->W, n3 * m6 * sizeof(double));
+    chol_solve(C->C, n3, C->Y, m6);
+    memcpy(C->v, C->gp, n3 * sizeof(double));
+    chol_solve(C->C, n3, C->v, 1);
+  }
+}
+
+/* Schur terms into the rows this thread owns, components in order */
+static void t_schur(void* c, int tid, int nt) {
+  mt_ctx* x = (mt_ctx*)c;
+  oracle_problem* p = x->p;
+  int plo, phi;
+  pose_range(p, tid, nt, &plo, &phi);
+  for (int cc = 0; cc < p->ncomp; ++cc) {
+    comp_t* C = &p->comps[cc];
+    const size_t n3 = 3 * (size_t)C->npts, m6 = 6 * (size_t)C->nnb;
+    for (int a = 0; a < C->nnb; ++a) {
+      if (C->nb[a] < plo || C->nb[a] >= phi) continue;
+      for (int ia = 0; ia < 6; ++ia) {
+        const size_t gi = 6 * (size_t)C->nb[a] + ia;
+        double s = 0.0;
+        for (size_t k = 0; k < n3; ++k) s += C->W[k * m6 + 6 * a + ia] * C->v[k];
+        p->gc[gi] -= s;
+        for (int bb = 0; bb <= a; ++bb)
+          for (int ib = 0; ib < 6; ++ib) {
+            const size_t gj = 6 * (size_t)C->nb[bb] + ib;
+            if (gj > gi) continue;
+            double t = 0.0;
+            for (size_t k = 0; k < n3; ++k) t += C->W[k * m6 + 6 * a + ia] * C->Y[k * m6 + 6 * bb + ib];
+            *sky_at(p, gi, gj) -= t;
+          }
+      }
+    }
+  }
+}
+
+/* blocked right-looking envelope Cholesky, rows [ilo, ihi) of block [j0, j1):
+   panel entries (columns of the block), then the trailing update; the terms
+   of every entry are subtracted in ascending k, as the serial row form does */
+static void t_chol_panel(void* c, int tid, int nt) {
+  mt_ctx* x = (mt_ctx*)c;
+  oracle_problem* p = x->p;
+  for (size_t i = x->ilo + (size_t)tid; i < x->ihi; i += (size_t)nt) {
+    const size_t fi = p->first[i];
+    if (fi >= x->j1) continue;
+    for (size_t j = fi > x->j0 ? fi : x->j0; j < x->j1; ++j) {
+      const size_t fj = p->first[j];
+      size_t k0 = fi > fj ? fi : fj;
+      if (k0 < x->j0) k0 = x->j0;
+      double s = *sky_at(p, i, j);
+      for (size_t k = k0; k < j; ++k) s -= *sky_at(p, i, k) * *sky_at(p, j, k);
+      *sky_at(p, i, j) = s / *sky_at(p, j, j);
+    }
+  }
+}
+static void t_chol_update(void* c, int tid, int nt) {
+  mt_ctx* x = (mt_ctx*)c;
+  oracle_problem* p = x->p;
+  for (size_t i = x->ilo + (size_t)tid; i < x->ihi; i += (size_t)nt) {
+    const size_t fi = p->first[i];
+    if (fi >= x->j1) continue;
+    for (size_t j = fi > x->j1 ? fi : x->j1; j <= i; ++j) {
+      const size_t fj = p->first[j];
+      if (fj >= x->j1) continue;
+      size_t k0 = fi > fj ? fi : fj;
+      if (k0 < x->j0) k0 = x->j0;
+      double s = *sky_at(p, i, j);
+      for (size_t k = k0; k < x->j1; ++k) s -= *sky_at(p, i, k) * *sky_at(p, j, k);
+      *sky_at(p, i, j) = s;
+    }
+  }
+}
+
+static void t_backsub(void* c, int tid, int nt) {
+  mt_ctx* x = (mt_ctx*)c;
+  oracle_problem* p = x->p;
+  double* delta = (double*)x->delta;
+  for (int cc = tid; cc < p->ncomp; cc += nt) {
+    comp_t* C = &p->comps[cc];
+    const size_t n3 = 3 * (size_t)C->npts, m6 = 6 * (size_t)C->nnb;
+    double* rhs = (double*)malloc((n3 ? n3 : 1) * sizeof(double));
+    for (size_t k = 0; k < n3; ++k) {
+      double s = C->gp[k];
+      for (int a = 0; a < C->nnb; ++a)
+        for (int ia = 0; ia < 6; ++ia)
+          s -= C->W[k * m6 + 6 * a + ia] * delta[x->doff[p->pose_var[C->nb[a]]] + ia];
+      rhs[k] = s;
+    }
+    chol_solve(C->C, n3, rhs, 1);
+    for (int k = 0; k < C->npts; ++k)
+      for (int j = 0; j < 3; ++j) delta[x->doff[C->pts[k]] + j] = rhs[3 * k + j];
+    free(rhs);
+  }
+}
+
+static int solve_schur_mt(oracle_problem* p, double lambda, double* delta, const size_t* doff) {
+  const size_t nd = p->ndim_red;
+  const int nt = p->nthreads;
+  mt_ctx x;
+  memset(&x, 0, sizeof(x));
+  x.p = p;
+  x.lambda = lambda;
+  x.doff = doff;
+  x.delta = delta;
+  x.tfail = (int*)calloc((size_t)nt, sizeof(int));
+  pool_run(p->pool, t_comp_accumulate, &x);
+  pool_run(p->pool, t_pose_accumulate, &x);
+  pool_run(p->pool, t_comp_factor, &x);
+  int ok = 1;
+  for (int t = 0; t < nt; ++t) ok = ok && !x.tfail[t];
+  free(x.tfail);
+  if (!ok) return 0;
+  pool_run(p->pool, t_schur, &x);
+  /* envelope Cholesky, 64-column blocks */
+  const size_t B = 64;
+  for (size_t j0 = 0; j0 < nd; j0 += B) {
+    const size_t j1 = j0 + B < nd ? j0 + B : nd;
+    /* the diagonal block, serially (its rows, its columns) */
+    for (size_t i = j0; i < j1; ++i) {
+      const size_t fi = p->first[i];
+      for (size_t j = fi > j0 ? fi : j0; j <= i; ++j) {
+        const size_t fj = p->first[j];
+        size_t k0 = fi > fj ? fi : fj;
+        if (k0 < j0) k0 = j0;
+        double s = *sky_at(p, i, j);
+        for (size_t k = k0; k < j; ++k) s -= *sky_at(p, i, k) * *sky_at(p, j, k);
+        if (j == i) {
+          if (!(s > 0.0) || !isfinite(s)) return 0;
+          *sky_at(p, i, i) = sqrt(s);
+        } else {
+          *sky_at(p, i, j) = s / *sky_at(p, j, j);
+        }
+      }
+    }
+    size_t ihi = j1;
+    for (size_t i = j1; i < nd; ++i)
+      if (p->first[i] < j1) ihi = i + 1;
+    if (ihi > j1) {
+      x.j0 = j0;
+      x.j1 = j1;
+      x.ilo = j1;
+      x.ihi = ihi;
+      pool_run(p->pool, t_chol_panel, &x);
+      pool_run(p->pool, t_chol_update, &x);
+    }
+  }
+  /* forward / backward substitution */
+  double* y = (double*)malloc((nd ? nd : 1) * sizeof(double));
+  for (size_t i = 0; i < nd; ++i) {
+    double s = p->gc[i];
+    for (size_t k = p->first[i]; k < i; ++k) s -= *sky_at(p, i, k) * y[k];
+    y[i] = s / *sky_at(p, i, i);
+  }
+  for (size_t ii = nd; ii-- > 0;) {
+    y[ii] /= *sky_at(p, ii, ii);
+    const double xi = y[ii];
+    for (size_t k = p->first[ii]; k < ii; ++k) y[k] -= *sky_at(p, ii, k) * xi;
+  }
+  for (int r = 0; r < p->npose; ++r)
+    for (int k = 0; k < 6; ++k) delta[doff[p->pose_var[r]] + k] = y[6 * (size_t)r + k];
+  free(y);
+  pool_run(p->pool, t_backsub, &x);
+  return 1;
 }

@@ -48,6 +48,9 @@ void oracle_destroy(oracle_problem* p);
 const char* oracle_last_error(const oracle_problem* p);
 /* 0 = Schur + skyline (default), 1 = dense full-system Cholesky */
 void oracle_set_dense(oracle_problem* p, int dense);
+/* threads of the Schur + skyline LM (default 1); the trajectory is
+   bit-identical for every thread count (the all-cores CPU baseline) */
+int oracle_set_threads(oracle_problem* p, int nthreads);
 
 double oracle_error(oracle_problem* p);
 int oracle_lm_reset(oracle_problem* p, const dynohip_lm_params* prm);

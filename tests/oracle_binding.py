@@ -29,6 +29,8 @@ def lib():
         L.oracle_last_error.argtypes = [vp]
         L.oracle_last_error.restype = C.c_char_p
         L.oracle_set_dense.argtypes = [vp, C.c_int]
+        L.oracle_set_threads.argtypes = [vp, C.c_int]
+        L.oracle_set_threads.restype = C.c_int
         L.oracle_error.argtypes = [vp]
         L.oracle_error.restype = C.c_double
         L.oracle_lm_reset.argtypes = [vp, P(_abi.LMParams)]
@@ -68,7 +70,7 @@ def dptr(a):
 class Oracle:
     """CPU restatement of LevenbergMarquardtOptimizer(graph, values).optimize()."""
 
-    def __init__(self, graph, values, dense=False):
+    def __init__(self, graph, values, dense=False, threads=1):
         L = lib()
         self.graph = graph
         self.values = values
@@ -85,6 +87,8 @@ class Oracle:
             self.h = None
             raise ValueError(f"oracle_create: {rc} {msg}")
         L.oracle_set_dense(self.h, 1 if dense else 0)
+        if threads > 1:
+            L.oracle_set_threads(self.h, int(threads))
         self.ndata = data.shape[0]
 
     def __del__(self):

@@ -106,3 +106,17 @@ def test_indefinite_system_fails_step():
     g, v, _ = synth.generate("T1")
     ok, _ = Oracle(g, v).solve_damped(0.0)
     assert ok in (0, 1)
+
+
+@pytest.mark.parametrize("name", ["T2", "C1"])
+def test_threaded_oracle_bit_identical(name):
+    """The all-cores CPU baseline (oracle_set_threads) runs the same LM
+    trajectory as the single-thread restatement, bit for bit."""
+    g, v, _ = synth.generate(name)
+    out = []
+    for th in (1, 4):
+        o = Oracle(g, v, threads=th)
+        s = o.optimize()
+        out.append((s.iterations, s.inner_iterations, s.final_error, o.values_data()))
+    assert out[0][:3] == out[1][:3]
+    assert np.array_equal(out[0][3], out[1][3])
