@@ -173,6 +173,9 @@ def _declare(name, lib):
             ("dynob_module_map", [vp_], vp_),
             ("dynob_module_formulation", [vp_], vp_),
             ("dynob_module_last_problem", [vp_, P(_abi.GraphView), P(U64), P(U8), P(D), P(D), SZ, SZ], C.c_int),
+            ("dynob_module_write_statistics", [vp_, C.c_char_p, C.c_char_p], C.c_int),
+            ("dynob_module_statistics", [vp_, C.c_char_p, P(C.c_double), C.c_size_t, P(C.c_size_t)], C.c_int),
+            ("dynob_module_statistics_labels", [vp_, C.c_char_p, C.c_size_t, P(C.c_size_t)], C.c_int),
         ]:
             f = getattr(lib, fn)
             f.argtypes = args

@@ -16,16 +16,24 @@ void dynohip_sliding_window_init(dynohip_sliding_window* w, int window, int over
   w->first_frame = -1;
 }
 
+// The reference aborts (glog CHECK_GE) on a first frame that does not fit an
+// int and on a triggered window that starts before the first frame
+// (RGBDBackendModule.hpp:121-124, 139-141); here both return DYNOHIP_EINVAL
+// after the same state updates.
 int dynohip_sliding_window_check(dynohip_sliding_window* w, uint64_t frame_k, uint64_t* starting_frame,
                                  uint64_t* ending_frame) {
   if (!w) return DYNOHIP_EINVAL;
-  if (w->first_frame == -1) w->first_frame = static_cast<int>(frame_k);
+  if (w->first_frame == -1) {
+    w->first_frame = static_cast<int>(frame_k);
+    if (w->first_frame < 0) return DYNOHIP_EINVAL;   // CHECK_GE(first_frame, 0)
+  }
   const int frame = static_cast<int>(frame_k) - w->first_frame;
   const bool condition = (w->previous_trigger_frame - (frame - w->sliding_window)) == w->overlap_size;
   if (condition) w->previous_trigger_frame = frame;
   if (ending_frame) *ending_frame = frame_k;
   const int starting = static_cast<int>(frame_k) - w->sliding_window;
   if (starting_frame) *starting_frame = static_cast<uint64_t>(starting);
+  if (condition && starting < w->first_frame) return DYNOHIP_EINVAL;   // CHECK_GE(starting_frame, first_frame)
   return condition ? 1 : 0;
 }
 

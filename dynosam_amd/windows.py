@@ -29,7 +29,16 @@ class SlidingWindow:
     def check(self, frame_k):
         s, e = C.c_uint64(), C.c_uint64()
         cond = self._lib.dynohip_sliding_window_check(C.byref(self._st), int(frame_k), C.byref(s), C.byref(e))
+        if cond < 0:
+            # the reference's CHECK_GE (RGBDBackendModule.hpp:121-124, 139-141)
+            raise ValueError(f"SlidingWindow::check({frame_k}): window start {ctypes_int(s.value)} before the "
+                             f"first frame {self._st.first_frame}")
         return bool(cond), int(s.value), int(e.value)
+
+
+def ctypes_int(u):
+    """uint64 -> the int it was cast from."""
+    return u - (1 << 64) if u >= (1 << 63) else u
 
 
 def full_batch_trigger(full_batch_frame, frame_k):

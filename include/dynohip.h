@@ -318,7 +318,10 @@ typedef struct {
 void dynohip_sliding_window_init(dynohip_sliding_window* w, int window,
                                  int overlap);
 /* SlidingWindow::check(frame_k): returns the condition (1/0) and writes the
-   window [frame_k - window, frame_k] bounds. */
+   window [frame_k - window, frame_k] bounds. DYNOHIP_EINVAL where the
+   reference's CHECK_GE aborts (RGBDBackendModule.hpp:121-124, 139-141): a
+   first frame beyond INT_MAX, or a triggered window starting before the
+   first frame (e.g. overlap >= window, or a negative start). */
 int dynohip_sliding_window_check(dynohip_sliding_window* w, uint64_t frame_k,
                                  uint64_t* starting_frame,
                                  uint64_t* ending_frame);

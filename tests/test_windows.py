@@ -219,3 +219,18 @@ def test_configs3_eight_c2_windows_sharded_on_gpu(gpu_available, tmp_path):
 def synth_key_x(frame):
     from dynosam_amd.keys import camera_pose_key
     return camera_pose_key(frame)
+
+
+def test_sliding_window_check_errors():
+    """The reference's CHECK_GEs (RGBDBackendModule.hpp:121-124, 139-141)
+    become DYNOHIP_EINVAL (ValueError here) instead of an abort."""
+    sw = SlidingWindow(10, 4)
+    with pytest.raises(ValueError):
+        sw.check(1 << 31)          # first frame does not fit an int
+    # a window triggered by an earlier frame after a later one starts
+    # before the first frame (overlap 5 > window 3)
+    sw = SlidingWindow(3, 5)
+    for k in range(10, 14):
+        sw.check(k)                # triggers at 13: [10, 13]
+    with pytest.raises(ValueError):
+        sw.check(11)               # condition holds, start 8 < first 10
