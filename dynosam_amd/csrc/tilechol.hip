@@ -84,6 +84,39 @@ __device__ __forceinline__ double rsqrt_nr(double x) {
   return y;
 }
 
+#ifdef DYNOHIP_TASK_CLOCK
+// per-task timestamps of the last k_factor_persist launch (s_memrealtime,
+// 100 MHz): dequeue, dependencies met, factor start, factor end, done; and
+// the worker; sub-phases and the factorisation's block steps (tools/task_clock.py)
+__device__ unsigned long long g_tclk[32][32768];
+#define TCLK(idx, q, v) \
+  do {                  \
+    if (threadIdx.x == 0 && (q) < 32768) g_tclk[idx][q] = (v); \
+  } while (0)
+// lane 0 of the calling wave (s_memtime: shader clock cycles)
+#define TCLKW(idx, q) \
+  do {                  \
+    if ((threadIdx.x & 63) == 0 && (q) < 32768) g_tclk[idx][q] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define TCLKW(idx, q) \
+  do {                  \
+  } while (0)
+#define TCLK(idx, q, v) \
+  do {                  \
+  } while (0)
+#endif
+__device__ __forceinline__ unsigned long long rtc() { return __builtin_amdgcn_s_memrealtime(); }
+
+// 1/x: hardware estimate + two Newton steps (full FP64 accuracy); four
+// dependent FMAs, half the chain of the reciprocal square root
+__device__ __forceinline__ double rcp_nr(double x) {
+  double y = __builtin_amdgcn_rcp(x);
+  y = __builtin_fma(__builtin_fma(-x, y, 1.0), y, y);
+  y = __builtin_fma(__builtin_fma(-x, y, 1.0), y, y);
+  return y;
+}
+
 __device__ __forceinline__ double* slot_ptr(const TileDev& b, int32_t slot) {
   return b.slots + static_cast<int64_t>(slot) * T * T;
 }
@@ -130,29 +163,36 @@ __device__ __forceinline__ double read_lane(double v, int lane) {
 // trailing update runs unmasked on the registers that still hold rows > p.
 // W is updated unscaled (W~[c][i] -= W~[c][p] U[p][i] / U[p][p]) and each
 // column is scaled by its 1/U[j][j] once at the end.
-__device__ __forceinline__ void factor16_wave(v4d& B, v4d& W, int l, bool& ok) {
+// dscr: 16 doubles of LDS scratch for the pivots. The column masks come from
+// a per-lane counter made opaque every pivot, so the compiler cannot hoist
+// sixteen of them into (spilled) scalar registers.
+__device__ __forceinline__ void factor16_wave(v4d& B, v4d& W, int l, bool& ok, double* dscr) {
   const int j = l & 15;
-  double myrs = 1.0;
-  bool good = true;
+  int jd = j;   // j - p at pivot p
 #pragma unroll
   for (int p = 0; p < 16; ++p) {
     const int rp = p >> 2, gp = p & 3;
     const double d = read_lane(B[rp], 16 * gp + p);
-    good = good && (d > 0.0) && (d < 1e300);
     const double rowp = pull_lane(B[rp], j + 16 * gp);  // B[p][j]
-    const double rs = rsqrt_nr(d);
-    const double f = rowp * (rs * rs);                   // U[p][j] / U[p][p]
-    const double fm = j > p ? f : 0.0;
-    myrs = j == p ? rs : myrs;
+    const double f = rowp * rcp_nr(d);                   // U[p][j] / U[p][p]
+    asm volatile("" : "+v"(jd));
+    const double fm = jd > 0 ? f : 0.0;
+    jd -= 1;
+    dscr[p] = d;   // every lane, same value
+
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       if (4 * r + 3 > p) B[r] -= bcast_row_lane(B[r], p) * f;     // rows g+4r > p
       if (4 * r <= p) W[r] -= bcast_row_lane(W[r], p) * fm;      // W~[c][p] != 0 only for c <= p
     }
   }
+  asm volatile("" ::: "memory");   // read back through LDS, not a 16-way select
+  const double dj = dscr[j];   // this lane's column scale 1/U[j][j] = 1/sqrt(d_j)
+  const double myrs = rsqrt_nr(dj);
 #pragma unroll
   for (int r = 0; r < 4; ++r) W[r] *= myrs;
-  ok = ok && good;
+  // every pivot positive and finite (NaN fails both tests), checked once
+  ok = ok && __all((dj > 0.0) && (dj < 1e300));
 }
 
 // acc (+)= Y^T Z for 16x16 blocks Y, Z in accumulator layout (K = 16)
@@ -175,16 +215,17 @@ __device__ __forceinline__ v4d mfma_tn(const v4d& Y, const v4d& Z, v4d acc, bool
 // The inverse work thus runs on waves that would otherwise wait, and only
 // the last inverse row follows the final barrier. Each wave keeps its
 // previous U block and its own W in registers.
-// xch: 2 x 4 blocks x 256 doubles of LDS.
-// Hooks use otherwise idle waves: idle0() runs on waves 1-3 while wave 0
-// factors block 0 (before the first barrier), idle1() on wave 0 during step 1.
+// xch: 2 x 4 blocks x 256 doubles of LDS; dscr: 16 doubles per wave.
+// idle(KB) runs at the top of block step KB on every wave but the factoring
+// one (wave KB): the caller spreads its independent MFMA work (pending
+// updates) over the periods in which a wave would otherwise wait.
 struct NoHook {
-  __device__ void operator()() const {}
+  __device__ void operator()(int) const {}
 };
 
-template <class Idle0 = NoHook, class Idle1 = NoHook>
-__device__ bool factor_tile_blk(v4d (&accA)[4], v4d (&accX)[4], int w, int l, double* xch, Idle0&& idle0 = Idle0(),
-                                Idle1&& idle1 = Idle1()) {
+template <int w, class Idle = NoHook>
+__device__ bool factor_tile_blk_w(v4d (&accA)[4], v4d (&accX)[4], int l, double* xch, double* dscr, Idle&& idle,
+                                  int q) {
   bool ok = true;
   v4d Wmine = v4d{0.0, 0.0, 0.0, 0.0};   // W of this wave's diagonal block
   v4d Uprev = v4d{0.0, 0.0, 0.0, 0.0};   // U[KB-1][w]
@@ -206,12 +247,13 @@ __device__ bool factor_tile_blk(v4d (&accA)[4], v4d (&accX)[4], int w, int l, do
   for (int KB = 0; KB < 4; ++KB) {
     double* xb = xch + (KB & 1) * 4 * 256;
     double* xp = xch + ((KB + 1) & 1) * 4 * 256;  // previous step's buffer
-    if (KB == 0 && w != 0) idle0();
-    if (KB == 1 && w == 0) idle1();
+    if (w != KB) idle(KB);
     if (w == KB) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) Wmine[r] = ((l >> 4) + 4 * r == (l & 15)) ? 1.0 : 0.0;
-      factor16_wave(accA[KB], Wmine, l, ok);
+      TCLKW(16 + 4 * KB, q);
+      factor16_wave(accA[KB], Wmine, l, ok, dscr);
+      TCLKW(17 + 4 * KB, q);
 #pragma unroll
       for (int TJ = KB + 1; TJ < 4; ++TJ) {
         v4d z = v4d{0.0, 0.0, 0.0, 0.0};
@@ -220,6 +262,7 @@ __device__ bool factor_tile_blk(v4d (&accA)[4], v4d (&accX)[4], int w, int l, do
         for (int r = 0; r < 4; ++r) xb[TJ * 256 + r * 64 + l] = accA[TJ][r];
       }
     }
+    if (w == KB) TCLKW(18 + 4 * KB, q);
     if (KB >= 1 && w == KB - 1) {
       // final inverse row KB-1 (all its updates from rows < KB-1 applied)
 #pragma unroll
@@ -231,6 +274,8 @@ __device__ bool factor_tile_blk(v4d (&accA)[4], v4d (&accX)[4], int w, int l, do
       }
     }
     __syncthreads();
+    TCLK(12 + KB, q, rtc());
+    if (w == KB) TCLKW(19 + 4 * KB, q);
     if (w > KB) {
       v4d Uv;
 #pragma unroll
@@ -265,6 +310,20 @@ __device__ bool factor_tile_blk(v4d (&accA)[4], v4d (&accX)[4], int w, int l, do
     }
   }
   return ok;
+}
+
+// The wave index is a template parameter of the body above: with a runtime
+// index the compiler merges the four "if (w == KB)" branches into one and
+// addresses accA by w through 16-way select chains.
+template <class Idle = NoHook>
+__device__ __forceinline__ bool factor_tile_blk(v4d (&accA)[4], v4d (&accX)[4], int w, int l, double* xch,
+                                                double* dscr, Idle&& idle = Idle(), int q = 0) {
+  switch (__builtin_amdgcn_readfirstlane(w)) {
+    case 0: return factor_tile_blk_w<0>(accA, accX, l, xch, dscr, idle, q);
+    case 1: return factor_tile_blk_w<1>(accA, accX, l, xch, dscr, idle, q);
+    case 2: return factor_tile_blk_w<2>(accA, accX, l, xch, dscr, idle, q);
+    default: return factor_tile_blk_w<3>(accA, accX, l, xch, dscr, idle, q);
+  }
 }
 
 // y = L^-1 v (64, L^-1 in LDS with stride LD, lower): 4 lanes per row
@@ -440,6 +499,7 @@ __device__ __forceinline__ void own_pending_quadrant(double* As, const double* Q
       for (int rr = 0; rr < 4; ++rr) As[MFMA_ROW(w, l, ti, rr) * LD + MFMA_COL(w, l, tj)] -= acc[ti][tj][rr];
 }
 
+
 struct TaskLds {
   double Ps[T * LD];   // pending diagonal operand L(k, c) -> later L_kk^-1
   double Qs[T * LD];   // pair operand A
@@ -447,26 +507,89 @@ struct TaskLds {
   double As[T * LD];   // own tile (i, k)
   double Xch[2 * 4 * 256];
   double rpart[4][T];
-  double vv[T];
+  double vv[T];        // r_k minus the contributions of eliminated columns
+  double yv[T];        // y_k = L_kk^-1 vv
 };
+
+// Launch-invariant inputs of a panel task: operand slots, the entries of
+// tile row k and r_k. They are fetched before the dependency wait, so that
+// after it a single round trip brings every operand.
+constexpr int kCsMax = 8;   // contribution entries per wave in that round trip
+struct PanelPre {
+  int32_t pd, qa, rb;       // fast path: pending diagonal operand, own pending pair (-1: none)
+  int32_t rbeg, rend;       // entries of tile row k
+  int32_t cs[kCsMax];       // this wave's contribution slots, entries rbeg + w + 4j (-1: none)
+  double rk;                // r_k[lane]
+  bool fast;                // at most one pending pair each
+};
+
+__device__ __forceinline__ PanelPre panel_prefetch(const TileDev& b, const TileTask& tk,
+                                                   const int32_t* __restrict__ pairs, const double* __restrict__ r,
+                                                   int w, int l) {
+  PanelPre p;
+  const bool own = tk.i != tk.k;
+  const int npd = tk.pd_end - tk.pd_beg, npo = own ? tk.po_end - tk.po_beg : 0;
+  p.fast = npd <= 1 && npo <= 1;
+  p.pd = npd == 1 ? pairs[2 * tk.pd_beg] : -1;
+  p.qa = npo == 1 ? pairs[2 * tk.po_beg] : -1;
+  p.rb = npo == 1 ? pairs[2 * tk.po_beg + 1] : -1;
+  p.rbeg = b.row_start[tk.k];
+  p.rend = b.row_start[tk.k + 1];
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+#pragma unroll
+  for (int j = 0; j < kCsMax; ++j) {
+    const int e = p.rbeg + wu + 4 * j;
+    p.cs[j] = (e < p.rend && b.row_col[e] != tk.k) ? b.row_slot[e] : -1;
+  }
+  p.rk = r[static_cast<int64_t>(tk.k) * T + l];
+  return p;
+}
+
+// acc += -P_bi P_bj^T for 16x16 blocks (bi, bj) of a 64x64 LDS operand P,
+// in accumulator layout (the pending update of diagonal block (bi, bj))
+__device__ __forceinline__ v4d pend_block(v4d acc, const double* Ps, int bi, int bj, int l) {
+  const int li = l & 15, lk = l >> 4;
+#pragma unroll 4
+  for (int k0 = 0; k0 < T; k0 += 4)
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-Ps[(16 * bi + li) * LD + k0 + lk], Ps[(16 * bj + li) * LD + k0 + lk],
+                                               acc, 0, 0, 0);
+  return acc;
+}
+
+// sum over the 16 lanes of a row group (lanes with equal l >> 4), with DPP
+// moves only: quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror
+// (a symmetric tree: every lane gets the same, bit-identical sum)
+__device__ __forceinline__ double sum16(double v) {
+  v += __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(v, v, 0x141, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(v, v, 0x140, 0xf, 0xf, false);
+  return v;
+}
+
+// Own-tile pending update A(i,k) -= Q R^T, in four chunks of 16 k per wave
+// (wave w: block row w, all four block columns). The chunks fill the block
+// steps of the diagonal factorisation in which the wave is not factoring:
+// chunk counts per (wave, step), so every wave carries about the same MFMA
+// load per step (wave 0 also has its pivots in step 0, waves 1-3 their
+// pending diagonal blocks).
+__constant__ constexpr int8_t kOwnChunks[4][4] = {{0, 3, 1, 0}, {0, 0, 2, 2}, {1, 2, 0, 1}, {2, 1, 1, 0}};
 
 template <bool SC1>
 __device__ __forceinline__ void panel_task(const TileDev& b, const TileTask& tk, const int32_t* __restrict__ pairs,
-                                           double* __restrict__ Linv, const double* __restrict__ r,
-                                           double* __restrict__ contrib, double* __restrict__ y, int* fail,
-                                           TaskLds& S) {
+                                           const PanelPre& p, double* __restrict__ Linv, double* __restrict__ contrib,
+                                           double* __restrict__ y, int* fail, TaskLds& S, int q = 0) {
   double* const Ps = S.Ps;
   double* const Qs = S.Qs;
   double* const Rs = S.Rs;
   double* const As = S.As;
   const int tid = threadIdx.x;
   const int w = tid >> 6, l = tid & 63;
+  const int li = l & 15, lk = l >> 4;
   const bool own = tk.i != tk.k;
-  const int npd = tk.pd_end - tk.pd_beg, npo = own ? tk.po_end - tk.po_beg : 0;
-  const bool fast = npd <= 1 && npo <= 1;
-  // (1) issue everything that is ready at the start of the level together:
-  // the diagonal tile (stored symmetric) into registers, the right-hand side
-  // contributions L(k,c) y_c of eliminated columns, and the operand tiles
+  // (1) one round trip: the diagonal tile (stored symmetric) into registers,
+  // the right-hand side contributions L(k,c) y_c of eliminated columns, and
+  // the operand tiles into LDS
   v4d accA[4], accX[4];
   const double* diag = slot_ptr(b, tk.diag);
 #pragma unroll
@@ -477,21 +600,30 @@ __device__ __forceinline__ void panel_task(const TileDev& b, const TileTask& tk,
       accA[TJ][rr] = TJ >= w ? gld<SC1>(diag + row * T + col) : 0.0;
       accX[TJ][rr] = row == col ? 1.0 : 0.0;
     }
+  double cv[kCsMax];
+#pragma unroll
+  for (int j = 0; j < kCsMax; ++j)
+    cv[j] = p.cs[j] >= 0 ? gld<SC1>(contrib + static_cast<int64_t>(p.cs[j]) * T + l) : 0.0;
+  if (p.fast) {
+    load_tiles_lds<SC1>(p.pd >= 0 ? slot_ptr(b, p.pd) : nullptr, Ps, own ? slot_ptr(b, tk.dst) : nullptr, As,
+                        p.qa >= 0 ? slot_ptr(b, p.qa) : nullptr, Qs,
+                        p.rb >= 0 && p.rb != p.qa && p.rb != p.pd ? slot_ptr(b, p.rb) : nullptr, Rs, tid);
+  }
   {
     double sacc = 0.0;
-    for (int e = b.row_start[tk.k] + w; e < b.row_start[tk.k + 1]; e += 4)
+#pragma unroll
+    for (int j = 0; j < kCsMax; ++j)
+      if (p.cs[j] >= 0) sacc += cv[j];
+    for (int e = p.rbeg + w + 4 * kCsMax; e < p.rend; e += 4)   // long rows (rare)
       if (b.row_col[e] != tk.k) sacc += gld<SC1>(contrib + static_cast<int64_t>(b.row_slot[e]) * T + l);
     S.rpart[w][l] = sacc;
   }
-  if (fast) {
-    load_tiles_lds<SC1>(npd ? slot_ptr(b, pairs[2 * tk.pd_beg]) : nullptr, Ps, own ? slot_ptr(b, tk.dst) : nullptr, As,
-                        npo ? slot_ptr(b, pairs[2 * tk.po_beg]) : nullptr, Qs,
-                        npo ? slot_ptr(b, pairs[2 * tk.po_beg + 1]) : nullptr, Rs, tid);
-  } else {
+  TCLK(6, q, rtc());
+  if (!p.fast) {
     // several pending pairs (rare): apply them one by one before the factor
     if (own) {
       load_tile_lds_t<SC1>(slot_ptr(b, tk.dst), As, tid);
-      if (npo) {
+      if (tk.po_end > tk.po_beg) {
         v4d acc[2][2];
         sum_pairs<SC1>(b, pairs, tk.po_beg, tk.po_end, Qs, Rs, tid, w, l, acc);
 #pragma unroll
@@ -510,68 +642,136 @@ __device__ __forceinline__ void panel_task(const TileDev& b, const TileTask& tk,
     }
   }
   __syncthreads();
-  if (tid < T)
-    S.vv[tid] = r[static_cast<int64_t>(tk.k) * T + tid] -
-                ((S.rpart[0][tid] + S.rpart[1][tid]) + (S.rpart[2][tid] + S.rpart[3][tid]));
-  // (2) pending updates: wave 0's diagonal blocks before the factorisation;
-  // waves 1-3 apply theirs, plus their quadrant of the own tile's update,
-  // while wave 0 factors block 0; wave 0 does its quadrant during step 1
-  const bool dp = fast && npd, op = fast && npo;
-  if (dp && w == 0) diag_pending(accA, Ps, w, l);
-  auto idle0 = [&]() {
-    if (dp) diag_pending(accA, Ps, w, l);
-    if (op) own_pending_quadrant(As, Qs, Rs, w, l);
+  TCLK(7, q, rtc());
+  if (tid < T) S.vv[tid] = p.rk - ((S.rpart[0][tid] + S.rpart[1][tid]) + (S.rpart[2][tid] + S.rpart[3][tid]));
+  // (2) pending diagonal update: block (0,0) by wave 0, blocks (0,v) by
+  // waves v into the second exchange buffer (free until step 1), so wave 0
+  // starts factoring after 16 MFMAs instead of 64
+  const bool dp = p.fast && p.pd >= 0, op = p.fast && p.qa >= 0;
+  if (dp) {
+    if (w == 0) {
+      accA[0] = pend_block(accA[0], Ps, 0, 0, l);
+    } else {
+      const v4d z = pend_block(v4d{0.0, 0.0, 0.0, 0.0}, Ps, 0, w, l);
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) S.Xch[4 * 256 + w * 256 + rr * 64 + l] = z[rr];
+    }
+    __syncthreads();
+    if (w == 0) {
+#pragma unroll
+      for (int TJ = 1; TJ < 4; ++TJ)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) accA[TJ][rr] += S.Xch[4 * 256 + TJ * 256 + rr * 64 + l];
+    }
+  }
+  // the own pair's second operand is L(k,c): usually the pending diagonal
+  // operand already in Ps (read only before Ps receives L_kk^-1)
+  const double* Rop = p.rb == p.qa ? Qs : p.rb == p.pd ? Ps : Rs;
+  v4d ao[4];
+#pragma unroll
+  for (int TJ = 0; TJ < 4; ++TJ) ao[TJ] = v4d{0.0, 0.0, 0.0, 0.0};
+  auto own_chunk = [&](int c) {
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      const int k = 16 * c + 4 * s4 + lk;
+      const double a = Qs[(16 * w + li) * LD + k];
+#pragma unroll
+      for (int TJ = 0; TJ < 4; ++TJ)
+        ao[TJ] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Rop[(16 * TJ + li) * LD + k], ao[TJ], 0, 0, 0);
+    }
   };
-  auto idle1 = [&]() {
-    if (op) own_pending_quadrant(As, Qs, Rs, w, l);
+  auto idle = [&](int KB) {
+    if (KB == 0 && dp) {
+      // this wave's own diagonal blocks (w, TJ >= w), before it factors
+#pragma unroll
+      for (int TJ = 1; TJ < 4; ++TJ)
+        if (TJ >= w) accA[TJ] = pend_block(accA[TJ], Ps, w, TJ, l);
+    }
+    if (op) {
+      int c0 = 0;
+      for (int kb = 0; kb < KB; ++kb) c0 += kOwnChunks[w][kb];
+      const int c1 = c0 + kOwnChunks[w][KB];
+      for (int c = c0; c < c1; ++c) own_chunk(c);
+    }
   };
-  const bool ok = factor_tile_blk(accA, accX, w, l, S.Xch, idle0, idle1);
+  TCLK(2, q, rtc());
+  const bool ok = factor_tile_blk(accA, accX, w, l, S.Xch, &S.rpart[w][0], idle, q);
+  TCLK(3, q, rtc());
   if (!ok && !own && tid == 0) *fail = 1;
-  // L_kk^-1 -> Ps (full square; upper part is exactly zero)
+  if (op) {
+    // wave 3 factors in the last step: its chunks ran before it
 #pragma unroll
-  for (int TJ = 0; TJ < 4; ++TJ)
+    for (int TJ = 0; TJ < 4; ++TJ)
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) Ps[ACC_ROW(w, l, rr) * LD + ACC_COL(TJ, l)] = accX[TJ][rr];
+      for (int rr = 0; rr < 4; ++rr) As[ACC_ROW(w, l, rr) * LD + ACC_COL(TJ, l)] -= ao[TJ][rr];
+  }
+  // L_kk^-1 -> Ps (full square; upper part is exactly zero) and this wave's
+  // rows of y_k = L_kk^-1 vv, reduced across the row groups in registers
+  double yp[4];
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) yp[rr] = 0.0;
+#pragma unroll
+  for (int TJ = 0; TJ < 4; ++TJ) {
+    const double vj = S.vv[16 * TJ + li];
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      Ps[ACC_ROW(w, l, rr) * LD + ACC_COL(TJ, l)] = accX[TJ][rr];
+      if (TJ <= w) yp[rr] += accX[TJ][rr] * vj;
+    }
+  }
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) yp[rr] = sum16(yp[rr]);
+  if (li == 0) {
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) S.yv[ACC_ROW(w, l, rr)] = yp[rr];
+  }
   if (!own) {
     double* dst = Linv + static_cast<int64_t>(tk.k) * T * T;
 #pragma unroll
     for (int TJ = 0; TJ < 4; ++TJ)
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) dst[ACC_ROW(w, l, rr) * T + ACC_COL(TJ, l)] = accX[TJ][rr];
+    if (li == 0) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) y[static_cast<int64_t>(tk.k) * T + ACC_ROW(w, l, rr)] = yp[rr];
+    }
+    return;
   }
   __syncthreads();
-  // y_k = L_kk^-1 r_k
-  const double yrow = lower_gemv4(Ps, S.vv, tid);
-  __syncthreads();
-  if ((tid & 3) == 0) {
-    S.vv[tid >> 2] = yrow;
-    if (!own) y[static_cast<int64_t>(tk.k) * T + (tid >> 2)] = yrow;
+  TCLK(8, q, rtc());
+  TCLK(9, q, rtc());
+  // L(i, k) = A L_kk^-T: wave w forms block row w; block column TJ needs
+  // k < 16 (TJ + 1) only (L_kk^-1 is lower triangular, the rest adds zeros)
+  v4d acc[4];
+#pragma unroll
+  for (int TJ = 0; TJ < 4; ++TJ) acc[TJ] = v4d{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int k0 = 0; k0 < T; k0 += 4) {
+    const double a = As[(16 * w + li) * LD + k0 + lk];
+#pragma unroll
+    for (int TJ = 0; TJ < 4; ++TJ)
+      if (k0 < 16 * (TJ + 1))
+        acc[TJ] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Ps[(16 * TJ + li) * LD + k0 + lk], acc[TJ], 0, 0, 0);
   }
-  if (!own) return;
-  // L(i, k) = A L^-T
-  v4d acc[2][2];
-  mfma_abt(As, Ps, w, l, acc);
-  __syncthreads();
+  TCLK(10, q, rtc());
   double* dst = slot_ptr(b, tk.dst);
+  double cp[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-  for (int ti = 0; ti < 2; ++ti)
+  for (int TJ = 0; TJ < 4; ++TJ) {
+    const double yj = S.yv[16 * TJ + li];
 #pragma unroll
-    for (int tj = 0; tj < 2; ++tj)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int row = MFMA_ROW(w, l, ti, rr), col = MFMA_COL(w, l, tj);
-        gst<SC1>(dst + row * T + col, acc[ti][tj][rr]);
-        As[row * LD + col] = acc[ti][tj][rr];
-      }
-  __syncthreads();
+    for (int rr = 0; rr < 4; ++rr) {
+      gst<SC1>(dst + ACC_ROW(w, l, rr) * T + ACC_COL(TJ, l), acc[TJ][rr]);
+      cp[rr] += acc[TJ][rr] * yj;
+    }
+  }
+  TCLK(11, q, rtc());
   // contribution of this tile to row i's right-hand side: L(i, k) y_k
-  {
-    const int row = tid >> 2, part = tid & 3;
-    double s = 0.0;
-    for (int m = part; m < T; m += 4) s += As[row * LD + m] * S.vv[m];
-    s += __shfl_xor(s, 1);
-    s += __shfl_xor(s, 2);
-    if (part == 0) gst<SC1>(contrib + static_cast<int64_t>(tk.dst) * T + row, s);
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) cp[rr] = sum16(cp[rr]);
+  if (li == 0) {
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) gst<SC1>(contrib + static_cast<int64_t>(tk.dst) * T + ACC_ROW(w, l, rr), cp[rr]);
   }
 }
 
@@ -586,7 +786,8 @@ __global__ __launch_bounds__(256) void k_tasks(TileDev b, const TileTask* __rest
     run_update<false>(b, tk, pairs, S.Qs, S.Rs, tid, tid >> 6, tid & 63);
     return;
   }
-  panel_task<false>(b, tk, pairs, Linv, r, contrib, y, fail, S);
+  const PanelPre p = panel_prefetch(b, tk, pairs, r, tid >> 6, tid & 63);
+  panel_task<false>(b, tk, pairs, p, Linv, contrib, y, fail, S);
 }
 
 // update tasks of a wide level: dst -= sum A B^T, with only the two
@@ -612,6 +813,7 @@ __global__ __launch_bounds__(256) void k_updates(TileDev b, const TileTask* __re
 // drains and the step is rejected.
 constexpr int kSpinLimitF = 1 << 22;
 
+
 __global__ __launch_bounds__(256) void k_factor_persist(TileDev b, const TileTask* __restrict__ tasks, int ntasks,
                                                         const int32_t* __restrict__ pairs,
                                                         const int32_t* __restrict__ dep_start,
@@ -629,6 +831,10 @@ __global__ __launch_bounds__(256) void k_factor_persist(TileDev b, const TileTas
     const int q = __builtin_amdgcn_readfirstlane(s_q);
     if (q >= ntasks) break;
     const TileTask tk = tasks[q];
+    TCLK(0, q, rtc());
+    TCLK(5, q, blockIdx.x);
+    PanelPre p;
+    if (tk.kind == 0) p = panel_prefetch(b, tk, pairs, r, w, l);
     if (w == 0) {
       bool ok = true;
       for (int j = dep_start[q] + l; j < dep_start[q + 1]; j += 64) {
@@ -643,10 +849,12 @@ __global__ __launch_bounds__(256) void k_factor_persist(TileDev b, const TileTas
       if (!ok) atomicOr(fail, 4);
     }
     __syncthreads();
+    TCLK(1, q, rtc());
     if (tk.kind == 1) run_update<true>(b, tk, pairs, S.Qs, S.Rs, tid, w, l);
-    else panel_task<true>(b, tk, pairs, Linv, r, contrib, y, fail, S);
+    else panel_task<true>(b, tk, pairs, p, Linv, contrib, y, fail, S, q);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    TCLK(4, q, rtc());
     if (tid == 0 && (tk.kind == 1 || tk.i != tk.k))
       __hip_atomic_fetch_add(wcnt + tk.dst, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -854,6 +1062,12 @@ __global__ __launch_bounds__(kBackThreads) void k_back_persist(TileDev b, const 
 }
 
 }  // namespace
+
+#ifdef DYNOHIP_TASK_CLOCK
+extern "C" int dynohip_debug_task_clock(unsigned long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tclk), sizeof(unsigned long long) * 32 * 32768) == hipSuccess ? n : -1;
+}
+#endif
 
 void launch_tile_forward(const TileDev& b, const TileSchedDev& sd, const std::vector<int32_t>& flevel,
                          const std::vector<int32_t>& fpanels, double* Linv, const double* r, double* contrib,

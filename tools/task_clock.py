@@ -1,0 +1,108 @@
+"""Critical path of one k_factor_persist launch from per-task timestamps.
+
+Needs a libdynohip.so built with -DDYNOHIP_TASK_CLOCK (tools/build_variant.sh
+<dir> -DDYNOHIP_TASK_CLOCK, then DYNOSAM_AMD_LIB_DIR=<dir>). Runs one LM
+optimisation of a synthetic config, reads the timestamps of the last
+factorisation launch (s_memrealtime, 100 MHz: dequeue, dependencies met,
+factor start, factor end, done) and prints the phase totals and the chain of
+tasks that ends last, each linked to the task that finished last before it
+could start.
+
+usage: python tools/task_clock.py [C2|NS] [out.json]
+"""
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from dynosam_amd import _native, synth  # noqa: E402
+from dynosam_amd.optimizer import LevenbergMarquardtOptimizer, plan_export  # noqa: E402
+
+
+def main():
+    cfg = sys.argv[1] if len(sys.argv) > 1 else "C2"
+    graph, values, _ = synth.generate(cfg)
+    ft = plan_export(graph, values, "ftask").reshape(-1, 10)
+    nt = ft.shape[0]
+    opt = LevenbergMarquardtOptimizer(graph, values, device=0)
+    opt.optimize()
+    lib = _native.load("libdynohip.so")
+    buf = np.zeros((32, 32768), dtype=np.uint64)
+    lib.dynohip_debug_task_clock.argtypes = [C.c_void_p, C.c_int]
+    assert lib.dynohip_debug_task_clock(buf.ctypes.data, nt) >= 0
+    t = buf[:5, :nt].astype(np.int64)
+    t0min = t[0].min()
+    t = (t - t0min) / 100.0               # us
+    sub = (buf[6:12, :nt].astype(np.int64) - t0min) / 100.0
+    bar = (buf[12:16, :nt].astype(np.int64) - t0min) / 100.0
+    worker = buf[5, :nt]
+    kind, kk, ii = ft[:, 0], ft[:, 1], ft[:, 2]
+    span = t[4].max()
+    pan = kind == 0
+    out = {"config": cfg, "tasks": int(nt), "span_us": float(span), "workers": int(worker.max() + 1)}
+    for name, m in (("panel", pan), ("update", ~pan)):
+        out[name] = {"n": int(m.sum()), "wait_us_mean": float((t[1] - t[0])[m].mean()),
+                     "exec_us_mean": float((t[4] - t[1])[m].mean())}
+    own = pan & (kk != ii)
+    # sub-phases: deps -> loads issued+rpart (P0) -> tiles in LDS (P1) -> factor start;
+    # factor end -> Linv in LDS (Q0) -> y (Q1) -> TRSM (Q2) -> stores (Q3) -> done
+    out["panel"]["sub_us_mean"] = {
+        "loads_diag_rhs": float((sub[0] - t[1])[pan].mean()), "tiles_lds": float((sub[1] - sub[0])[pan].mean()),
+        "pending_w0": float((t[2] - sub[1])[pan].mean()), "linv_y_sync": float((sub[2] - t[3])[own].mean()),
+        "y": float((sub[3] - sub[2])[pan].mean()), "trsm": float((sub[4] - sub[3])[own].mean()),
+        "store": float((sub[5] - sub[4])[own].mean()), "contrib_drain": float((t[4] - sub[5])[own].mean())}
+    # factorisation block steps as wave 0 passes each barrier
+    out["panel"]["factor_steps_us_mean"] = [float((bar[0] - t[2])[pan].mean())] + \
+        [float((bar[j] - bar[j - 1])[pan].mean()) for j in range(1, 4)] + [float((t[3] - bar[3])[pan].mean())]
+    # per block step, cycles on the factoring wave: pivots, U row, barrier wait
+    cyc = buf[16:32, :nt].astype(np.int64)
+    steps = []
+    for kb in range(4):
+        a, b_, c, d = cyc[4 * kb:4 * kb + 4]
+        steps.append({"pivots": float((b_ - a)[pan].mean()), "u_row": float((c - b_)[pan].mean()),
+                      "barrier": float((d - c)[pan].mean())})
+    for kb in range(1, 4):
+        steps[kb]["from_prev_barrier"] = float((cyc[4 * kb] - cyc[4 * kb - 1])[pan].mean())
+    out["panel"]["factor_step_cycles"] = steps
+    out["panel"].update({"pre_us_mean": float((t[2] - t[1])[pan].mean()),
+                         "factor_us_mean": float((t[3] - t[2])[pan].mean()),
+                         "post_us_mean": float((t[4] - t[3])[pan].mean())})
+    # chain ending last
+    chain = []
+    cur = int(np.argmax(t[4]))
+    while True:
+        rec = {"q": cur, "kind": int(kind[cur]), "k": int(kk[cur]), "i": int(ii[cur]),
+               "t0": float(t[0, cur]), "wait": float(t[1, cur] - t[0, cur]), "exec": float(t[4, cur] - t[1, cur])}
+        if kind[cur] == 0:
+            rec.update(pre=float(t[2, cur] - t[1, cur]), factor=float(t[3, cur] - t[2, cur]),
+                       post=float(t[4, cur] - t[3, cur]))
+        chain.append(rec)
+        cand = np.where(t[4] <= t[1, cur] + 0.5)[0]
+        cand = cand[cand != cur]
+        if cand.size == 0:
+            break
+        nxt = int(cand[np.argmax(t[4, cand])])
+        if t[4, nxt] < t[0, cur] - 0.5:   # not waiting on anything: queue-bound from here
+            rec["queue_bound"] = True
+            break
+        cur = nxt
+    chain.reverse()
+    out["chain"] = chain
+    tot = {"wait": sum(c["wait"] for c in chain), "pre": sum(c.get("pre", 0) for c in chain),
+           "factor": sum(c.get("factor", 0) for c in chain), "post": sum(c.get("post", 0) for c in chain),
+           "update_exec": sum(c["exec"] for c in chain if c["kind"] == 1)}
+    out["chain_totals_us"] = tot
+    print(json.dumps({k: v for k, v in out.items() if k != "chain"}, indent=1))
+    for c in chain:
+        print(" ".join(f"{k}={v:.1f}" if isinstance(v, float) else f"{k}={v}" for k, v in c.items()))
+    if len(sys.argv) > 2:
+        json.dump(out, open(sys.argv[2], "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
