@@ -8,6 +8,11 @@
 #include <cmath>
 #include <cstring>
 #include <numeric>
+#include <unistd.h>
+
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <unordered_map>
 
@@ -96,57 +101,129 @@ class KeyIndex {
   std::vector<int32_t> vals_;
 };
 
-// CSR by counting: ntargets lists; `emit(fn)` enumerates (target, entry)
-// in list order, and is called twice (count, fill)
-template <typename Emit>
-void csr_two_pass(size_t ntargets, Emit&& emit, GatherList& out) {
-  out.start.assign(ntargets + 1, 0);
-  emit([&](int32_t t, const GEntry&) { out.start[t + 1]++; });
-  for (size_t t = 0; t < ntargets; ++t) out.start[t + 1] += out.start[t];
-  out.ent.resize(out.start[ntargets]);
-  std::vector<int64_t> cur(out.start.begin(), out.start.end() - 1);
-  emit([&](int32_t t, const GEntry& e) { out.ent[cur[t]++] = e; });
-}
-
-// CSR over `nranges` contiguous pieces of one enumeration: emit_range(r, fn)
-// enumerates piece r; the pieces are counted and filled on worker threads,
-// and every target's entries keep the order of the whole enumeration
-template <typename EmitRange>
-void csr_ranges(size_t ntargets, int nranges, EmitRange&& emit_range, GatherList& out) {
-  std::vector<std::vector<int64_t>> cur(nranges, std::vector<int64_t>(ntargets, 0));
-  auto parallel = [&](auto&& body) {
-    std::vector<std::thread> th;
-    for (int r = 1; r < nranges; ++r) th.emplace_back([&, r] { body(r); });
-    body(0);
-    for (auto& t : th) t.join();
-  };
-  parallel([&](int r) { emit_range(r, [&](int32_t t, const GEntry&) { cur[r][t]++; }); });
-  out.start.assign(ntargets + 1, 0);
-  for (size_t t = 0; t < ntargets; ++t) {
-    int64_t off = out.start[t];
-    for (int r = 0; r < nranges; ++r) {
-      const int64_t c = cur[r][t];
-      cur[r][t] = off;
-      off += c;
+// The planner's workers: threads created once per process and reused by
+// every plan (a plan runs a dozen parallel sections; creating 16 threads for
+// each cost milliseconds). run(nw, body) calls body(0..nw-1), body(0) on the
+// calling thread, and returns when all are done. Never destroyed: the threads
+// block on the condition variable until the process exits.
+class PlanPool {
+ public:
+  static PlanPool& get() {
+    // a forked child has none of the parent's threads: it starts its own pool
+    static PlanPool* p = nullptr;
+    static pid_t owner = 0;
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!p || owner != getpid()) {
+      p = new PlanPool();
+      owner = getpid();
     }
-    out.start[t + 1] = off;
+    return *p;
   }
-  out.ent.resize(out.start[ntargets]);
+  int workers() const { return nmax_; }
+  template <typename Body>
+  void run(int nw, Body&& body) {
+    nw = std::max(1, std::min(nw, nmax_));
+    if (nw == 1) {
+      body(0);
+      return;
+    }
+    std::unique_lock<std::mutex> call(call_mu_);   // one parallel section at a time
+    std::function<void(int)> fn = [&body](int r) { body(r); };
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      fn_ = &fn;
+      nw_ = nw;
+      pending_ = nw - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    body(0);
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return pending_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  PlanPool() {
+    const unsigned hc = std::thread::hardware_concurrency();
+    nmax_ = static_cast<int>(std::max(1u, std::min(16u, hc ? hc : 1u)));
+    for (int r = 1; r < nmax_; ++r) std::thread([this, r] { loop(r); }).detach();
+  }
+  void loop(int r) {
+    uint64_t seen = 0;
+    for (;;) {
+      std::function<void(int)>* fn;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (r >= nw_) continue;
+        fn = fn_;
+      }
+      (*fn)(r);
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--pending_ == 0) done_cv_.notify_one();
+    }
+  }
+  int nmax_ = 1;
+  std::mutex call_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  std::function<void(int)>* fn_ = nullptr;
+  int nw_ = 0, pending_ = 0;
+  uint64_t gen_ = 0;
+};
+
+// CSR by target ranges: worker r owns the targets [tcut[r], tcut[r+1]) and
+// runs the enumeration emit(r, fn) itself, keeping only its own targets (the
+// emitter may skip what it knows lies outside range r). Every target keeps
+// the enumeration order of its entries, so the lists equal a single-threaded
+// two-pass build, and each worker fills one contiguous part of the output:
+// cache-local writes instead of one scatter over the whole list.
+template <typename Emit>
+void csr_target_ranges(size_t ntargets, const std::vector<int64_t>& tcut, Emit&& emit, GatherList& out) {
+  const int nr = static_cast<int>(tcut.size()) - 1;
+  auto parallel = [&](auto&& body) { PlanPool::get().run(nr, body); };
+  auto T0 = std::chrono::steady_clock::now();
+  out.start.assign(ntargets + 1, 0);
   parallel([&](int r) {
-    auto& c = cur[r];
-    emit_range(r, [&](int32_t t, const GEntry& e) { out.ent[c[t]++] = e; });
+    const int64_t t0 = tcut[r], t1 = tcut[r + 1];
+    emit(r, [&](int64_t t, const GEntry&) {
+      if (t >= t0 && t < t1) out.start[t + 1]++;
+    });
   });
+  auto T1 = std::chrono::steady_clock::now();
+  for (size_t t = 0; t < ntargets; ++t) out.start[t + 1] += out.start[t];
+  out.ent.resize(out.start[ntargets]);
+  auto T2 = std::chrono::steady_clock::now();
+  parallel([&](int r) {
+    const int64_t t0 = tcut[r], t1 = tcut[r + 1];
+    std::vector<int64_t> cur(out.start.begin() + t0, out.start.begin() + t1);
+    emit(r, [&](int64_t t, const GEntry& e) {
+      if (t >= t0 && t < t1) out.ent[cur[t - t0]++] = e;
+    });
+  });
+  auto T3 = std::chrono::steady_clock::now();
+  if (std::getenv("DYNOHIP_PLAN_TIMING"))
+    std::fprintf(stderr, "  csr nt=%zu nw=%d ent=%zu count %.2f alloc %.2f fill %.2f ms\n", ntargets, nr, out.ent.size(),
+                 std::chrono::duration<double, std::milli>(T1 - T0).count(),
+                 std::chrono::duration<double, std::milli>(T2 - T1).count(),
+                 std::chrono::duration<double, std::milli>(T3 - T2).count());
 }
 
-void to_csr(size_t ntargets, std::vector<std::pair<int32_t, GEntry>>& pairs, GatherList& out) {
-  out.start.assign(ntargets + 1, 0);
-  for (auto& p : pairs) out.start[p.first + 1]++;
-  for (size_t t = 0; t < ntargets; ++t) out.start[t + 1] += out.start[t];
-  out.ent.resize(pairs.size());
-  std::vector<int64_t> cur(out.start.begin(), out.start.end() - 1);
-  for (auto& p : pairs) out.ent[cur[p.first]++] = p.second;
-  pairs.clear();
-  pairs.shrink_to_fit();
+// body(b, e) over [0, n) in contiguous ranges on the planner's workers
+template <typename Body>
+void parallel_for(int64_t n, Body&& body) {
+  const int nw = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(PlanPool::get().workers(), n / 8192 + 1)));
+  PlanPool::get().run(nw, [&](int r) { body(n * r / nw, n * (r + 1) / nw); });
+}
+
+// even cut of [0, n) into the planner's worker count
+std::vector<int64_t> even_cuts(int64_t n) {
+  const int nw = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(PlanPool::get().workers(), n / 64 + 1)));
+  std::vector<int64_t> c(nw + 1);
+  for (int r = 0; r <= nw; ++r) c[r] = n * r / nw;
+  return c;
 }
 
 }  // namespace
@@ -188,6 +265,21 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
       return DYNOHIP_EINVAL;
     }
     fuser[t].resize(b->n * kNKeys[t]);
+    // fast path on the workers; any failure is re-found below, in order, for its message
+    std::vector<uint8_t> bad(1, 0);
+    parallel_for(static_cast<int64_t>(b->n), [&](int64_t i0, int64_t i1) {
+      for (int64_t i = i0; i < i1; ++i)
+        for (int s = 0; s < kNKeys[t]; ++s) {
+          const int32_t u = key_to_user.find(b->keys[i * kNKeys[t] + s]);
+          const int want = kSlotKind[t][s] == 0 ? DYNOHIP_POSE3 : DYNOHIP_POINT3;
+          if (u < 0 || kind[u] != want) {
+            __atomic_store_n(&bad[0], 1, __ATOMIC_RELAXED);
+            return;
+          }
+          fuser[t][i * kNKeys[t] + s] = u;
+        }
+    });
+    if (bad[0])
     for (size_t i = 0; i < b->n; ++i)
       for (int s = 0; s < kNKeys[t]; ++s) {
         const uint64_t key = b->keys[i * kNKeys[t] + s];
@@ -232,8 +324,16 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
 
   plan_mark("before point chains", tmark);
   // ---- point chains ----
-  // adjacency between points from factors with two point slots
-  std::vector<std::vector<int32_t>> adj(n);
+  // adjacency between points from factors with two point slots: at most two
+  // distinct neighbours per point (a chain), held flat
+  std::vector<int32_t> adj(2 * n, -1);
+  std::vector<uint8_t> deg(n, 0);
+  bool too_many = false;
+  auto link = [&](int32_t a, int32_t b) {
+    if (adj[2 * a] == b || adj[2 * a + 1] == b) return;
+    if (deg[a] == 2) { too_many = true; return; }
+    adj[2 * a + deg[a]++] = b;
+  };
   for (int t = 0; t < kNTypes; ++t) {
     const int nk = kNKeys[t];
     int ps[4], np = 0;
@@ -244,62 +344,74 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
     for (size_t i = 0; i < blocks[t]->n; ++i) {
       const int32_t a = fuser[t][i * nk + ps[0]], b = fuser[t][i * nk + ps[1]];
       if (a == b) { err = "factor links a point to itself"; return DYNOHIP_ESTRUCT; }
-      adj[a].push_back(b);
-      adj[b].push_back(a);
+      link(a, b);
+      link(b, a);
     }
   }
-  for (auto& a : adj) {
-    std::sort(a.begin(), a.end());
-    a.erase(std::unique(a.begin(), a.end()), a.end());
-  }
+  if (too_many) { err = "point component is not a chain (degree > 2)"; return DYNOHIP_ESTRUCT; }
   {
     std::vector<char> seen(n, 0);
-    // chains in walk order from the endpoint with the smallest key
-    std::vector<std::vector<int32_t>> chains;
+    // chains in walk order from the endpoint with the smallest key, flat
+    std::vector<int32_t> walks, wstart{0}, comp;
+    walks.reserve(n);
     for (size_t i = 0; i < n; ++i) {
       if (kind[i] != DYNOHIP_POINT3 || seen[i]) continue;
-      // collect component
-      std::vector<int32_t> comp{static_cast<int32_t>(i)};
       seen[i] = 1;
+      if (deg[i] == 0) {   // a lone point (every static landmark)
+        walks.push_back(static_cast<int32_t>(i));
+        wstart.push_back(static_cast<int32_t>(walks.size()));
+        continue;
+      }
+      // collect the component
+      comp.assign(1, static_cast<int32_t>(i));
       size_t nedges2 = 0;
       for (size_t q = 0; q < comp.size(); ++q) {
         const int32_t u = comp[q];
-        nedges2 += adj[u].size();
-        if (adj[u].size() > 2) { err = "point component is not a chain (degree > 2)"; return DYNOHIP_ESTRUCT; }
-        for (int32_t w : adj[u])
+        nedges2 += deg[u];
+        for (int k = 0; k < deg[u]; ++k) {
+          const int32_t w = adj[2 * u + k];
           if (!seen[w]) { seen[w] = 1; comp.push_back(w); }
+        }
       }
       if (nedges2 / 2 != comp.size() - 1) { err = "point component is not a chain (cycle)"; return DYNOHIP_ESTRUCT; }
       int32_t start = -1;
       for (int32_t u : comp)
-        if (adj[u].size() <= 1 && (start < 0 || keys[u] < keys[start])) start = u;
-      std::vector<int32_t> walk;
+        if (deg[u] <= 1 && (start < 0 || keys[u] < keys[start])) start = u;
       int32_t prev = -1, cur = start;
       for (size_t q = 0; q < comp.size(); ++q) {
-        walk.push_back(cur);
+        walks.push_back(cur);
         int32_t nxt = -1;
-        for (int32_t w : adj[cur])
-          if (w != prev) nxt = w;
+        for (int k = 0; k < deg[cur]; ++k)
+          if (adj[2 * cur + k] != prev) nxt = adj[2 * cur + k];
         prev = cur;
         cur = nxt;
       }
-      chains.push_back(std::move(walk));
+      wstart.push_back(static_cast<int32_t>(walks.size()));
     }
-    // longest chains first (stable): the chain kernels run a thread per
-    // chain, so a wave then holds chains of one length and the long ones
-    // start first
-    std::stable_sort(chains.begin(), chains.end(),
-                     [](const std::vector<int32_t>& x, const std::vector<int32_t>& y) { return x.size() > y.size(); });
+    // longest chains first (stable, a counting sort by length): the chain
+    // kernels run a thread per chain, so a wave then holds chains of one
+    // length and the long ones start first
+    const int nchains = static_cast<int>(wstart.size()) - 1;
+    int maxlen = 0;
+    for (int c = 0; c < nchains; ++c) maxlen = std::max(maxlen, wstart[c + 1] - wstart[c]);
+    std::vector<int32_t> lcnt(static_cast<size_t>(maxlen) + 2, 0);
+    for (int c = 0; c < nchains; ++c) lcnt[maxlen - (wstart[c + 1] - wstart[c]) + 1]++;
+    for (int L = 0; L <= maxlen; ++L) lcnt[L + 1] += lcnt[L];
+    std::vector<int32_t> order(nchains);
+    for (int c = 0; c < nchains; ++c) order[lcnt[maxlen - (wstart[c + 1] - wstart[c])]++] = c;
     int32_t next_pt = 0;
+    P.comp_start.reserve(nchains + 1);
+    P.pt_key.reserve(walks.size());
     P.comp_start.push_back(0);
-    for (const auto& walk : chains) {
-      for (int32_t u : walk) {
+    for (int c : order) {
+      for (int32_t q = wstart[c]; q < wstart[c + 1]; ++q) {
+        const int32_t u = walks[q];
         P.user_idx[u] = next_pt++;
         P.pt_key.push_back(keys[u]);
       }
       P.comp_start.push_back(next_pt);
-      P.max_chain = std::max(P.max_chain, static_cast<int>(walk.size()));
     }
+    P.max_chain = maxlen;
     P.n_pt = next_pt;
     P.n_comp = static_cast<int>(P.comp_start.size()) - 1;
   }
@@ -318,10 +430,12 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
     tp.base = arena;
     arena += static_cast<uint64_t>(tp.stride) * tp.n;
     tp.idx.resize(b->n * kNKeys[t]);
-    for (size_t i = 0; i < b->n * kNKeys[t]; ++i) tp.idx[i] = P.user_idx[fuser[t][i]];
     tp.meas.assign(b->measured ? b->measured : nullptr, b->measured ? b->measured + b->n * kMeasDim[t] : nullptr);
     tp.isig.resize(b->n * kDim[t]);
-    for (size_t i = 0; i < b->n * kDim[t]; ++i) tp.isig[i] = 1.0 / b->sigmas[i];
+    parallel_for(static_cast<int64_t>(b->n), [&](int64_t i0, int64_t i1) {
+      for (int64_t i = i0 * kNKeys[t]; i < i1 * kNKeys[t]; ++i) tp.idx[i] = P.user_idx[fuser[t][i]];
+      for (int64_t i = i0 * kDim[t]; i < i1 * kDim[t]; ++i) tp.isig[i] = 1.0 / b->sigmas[i];
+    });
     tp.hk.assign(b->n, 0.0);
     if (b->huber_k)
       for (size_t i = 0; i < b->n; ++i) tp.hk[i] = b->huber_k[i];
@@ -394,8 +508,30 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
   P.comp_y_base.resize(P.n_comp);
   P.off_Y = arena;
   P.nbedge_start.assign(1, 0);
+  P.nb_pose.reserve(P.n_edge);
+  P.nb_comp.reserve(P.n_edge);
+  P.nbedge_pt.reserve(P.n_edge);
+  P.nbedge_w.reserve(P.n_edge);
+  P.nbedge_start.reserve(static_cast<size_t>(P.n_edge) + 1);
+  std::vector<int32_t> nb;
   for (int c = 0; c < P.n_comp; ++c) {
-    std::vector<int32_t> nb;
+    if (P.comp_start[c + 1] - P.comp_start[c] == 1) {
+      // a lone point: its neighbour poses are its (sorted, unique) edges
+      const int32_t i = P.comp_start[c];
+      const int32_t e0 = P.pt_edge_start[i], e1 = P.pt_edge_start[i + 1];
+      P.comp_y_base[c] = static_cast<int64_t>(arena);
+      arena += 18ull * (e1 - e0);
+      for (int32_t e = e0; e < e1; ++e) {
+        P.nb_pose.push_back(P.edge_pose[e]);
+        P.nb_comp.push_back(c);
+        P.nbedge_pt.push_back(0);
+        P.nbedge_w.push_back(static_cast<uint32_t>(P.off_W + 18ull * e));
+        P.nbedge_start.push_back(static_cast<int32_t>(P.nbedge_pt.size()));
+      }
+      P.comp_nb_start.push_back(static_cast<int32_t>(P.nb_pose.size()));
+      continue;
+    }
+    nb.clear();
     for (int32_t i = P.comp_start[c]; i < P.comp_start[c + 1]; ++i)
       for (int32_t e = P.pt_edge_start[i]; e < P.pt_edge_start[i + 1]; ++e) nb.push_back(P.edge_pose[e]);
     std::sort(nb.begin(), nb.end());
@@ -428,48 +564,90 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
 
   plan_mark("before point-side gathers", tmark);
   // ---- point-side gathers (CSR builds run on worker threads) ----
-  std::vector<std::thread> workers;
+  // Point-slot references (type, factor, slot) in enumeration order
+  // (type-major, then factor, then slot), stably sorted by point: a worker
+  // owning a point range walks only its points' references, and every
+  // target still lists its entries in factor order.
   bool chain_ok = true;
   {
-    // enumerates the point-side entries in factor order; `which` selects
-    // D (0), E (1), g_p (2) or W (3)
-    auto emit_point = [&](int which, auto&& fn) {
+    std::vector<int64_t> rstart(static_cast<size_t>(P.n_pt) + 1, 0);
+    for (int t = 0; t < kNTypes; ++t) {
+      const TypePlan& tp = P.types[t];
+      const int nk = kNKeys[t];
+      for (int s = 0; s < nk; ++s)
+        if (kSlotKind[t][s] == 1)
+          for (int i = 0; i < tp.n; ++i) rstart[tp.idx[i * nk + s] + 1]++;
+    }
+    for (int32_t pt = 0; pt < P.n_pt; ++pt) rstart[pt + 1] += rstart[pt];
+    std::vector<uint64_t, default_init_allocator<uint64_t>> refs(rstart[P.n_pt]);
+    {
+      std::vector<int64_t> cur(rstart.begin(), rstart.end() - 1);
       for (int t = 0; t < kNTypes; ++t) {
         const TypePlan& tp = P.types[t];
-        const int nk = kNKeys[t], d = kDim[t];
-        for (int i = 0; i < tp.n; ++i) {
-          int pslot[2], np = 0;
-          for (int s = 0; s < nk; ++s) {
-            if (kSlotKind[t][s] != 1) continue;
-            pslot[np++] = s;
-            const int32_t pt = tp.idx[i * nk + s];
-            const uint32_t J = block_off(tp, t, i, s);
-            if (which == 0) fn(pt, GEntry{J, J, d, 1});
-            if (which == 2) fn(pt, GEntry{J, b_off(tp, t, i), d, 1});
-            if (which == 3)
-              for (int sb = 0; sb < nk; ++sb)
-                if (kSlotKind[t][sb] == 0) fn(find_edge(pt, tp.idx[i * nk + sb]), GEntry{J, block_off(tp, t, i, sb), d, 1});
-          }
-          if (which == 1 && np == 2) {
-            int sa = pslot[0], sb = pslot[1];
-            int32_t pa = tp.idx[i * nk + sa], pb = tp.idx[i * nk + sb];
-            if (pa > pb) { std::swap(pa, pb); std::swap(sa, sb); }
-            if (pb != pa + 1 || comp_of[pa] != comp_of[pb]) { chain_ok = false; continue; }
-            // E_pa = C_{pa+1, pa} = J_{pb}^T J_{pa}
-            fn(pa, GEntry{block_off(tp, t, i, sb), block_off(tp, t, i, sa), d, 1});
+        const int nk = kNKeys[t];
+        for (int i = 0; i < tp.n; ++i)
+          for (int s = 0; s < nk; ++s)
+            if (kSlotKind[t][s] == 1)
+              refs[cur[tp.idx[i * nk + s]]++] = (static_cast<uint64_t>(i) << 8) | (t << 4) | s;
+      }
+    }
+    // a chain link (two point slots) must join consecutive points of one
+    // component; its E entry goes to the lower point
+    for (int t = 0; t < kNTypes; ++t) {
+      const TypePlan& tp = P.types[t];
+      const int nk = kNKeys[t];
+      int ps[2], np = 0;
+      for (int s = 0; s < nk; ++s)
+        if (kSlotKind[t][s] == 1 && np < 2) ps[np++] = s;
+      if (np != 2) continue;
+      for (int i = 0; i < tp.n; ++i) {
+        int32_t pa = tp.idx[i * nk + ps[0]], pb = tp.idx[i * nk + ps[1]];
+        if (pa > pb) std::swap(pa, pb);
+        if (pb != pa + 1 || comp_of[pa] != comp_of[pb]) chain_ok = false;
+      }
+    }
+    if (!chain_ok) { err = "internal: chain link not adjacent"; return DYNOHIP_ESTRUCT; }
+    // the entries of points [p0, p1); `which` selects D (0), E (1), g_p (2) or W (3)
+    auto emit_point = [&](int which, int32_t p0, int32_t p1, auto&& fn) {
+      for (int32_t pt = p0; pt < p1; ++pt)
+        for (int64_t q = rstart[pt]; q < rstart[pt + 1]; ++q) {
+          const uint64_t r = refs[q];
+          const int s = static_cast<int>(r & 15), t = static_cast<int>((r >> 4) & 15);
+          const int i = static_cast<int>(r >> 8);
+          const TypePlan& tp = P.types[t];
+          const int nk = kNKeys[t], d = kDim[t];
+          const uint32_t J = block_off(tp, t, i, s);
+          if (which == 0) fn(pt, GEntry{J, J, d, 1});
+          if (which == 2) fn(pt, GEntry{J, b_off(tp, t, i), d, 1});
+          if (which == 3)
+            for (int sb = 0; sb < nk; ++sb)
+              if (kSlotKind[t][sb] == 0) fn(find_edge(pt, tp.idx[i * nk + sb]), GEntry{J, block_off(tp, t, i, sb), d, 1});
+          if (which == 1) {
+            int so = -1;
+            for (int sb = 0; sb < nk; ++sb)
+              if (kSlotKind[t][sb] == 1 && sb != s) so = sb;
+            // E_pa = C_{pa+1, pa} = J_{pb}^T J_{pa}, once per link (from its lower point)
+            if (so >= 0 && tp.idx[i * nk + so] == pt + 1) fn(pt, GEntry{block_off(tp, t, i, so), J, d, 1});
           }
         }
-      }
     };
-    for (int which = 0; which < 4; ++which)
-      workers.emplace_back([&P, &emit_point, which] {
-        GatherList& out = which == 0 ? P.gD : which == 1 ? P.gE : which == 2 ? P.gGp : P.gW;
-        csr_two_pass(which == 3 ? P.n_edge : P.n_pt, [&](auto&& fn) { emit_point(which, fn); }, out);
-      });
-    for (auto& w : workers) w.join();
-    workers.clear();
+    for (int which = 0; which < 4; ++which) {
+      GatherList& out = which == 0 ? P.gD : which == 1 ? P.gE : which == 2 ? P.gGp : P.gW;
+      const int64_t nt = which == 3 ? P.n_edge : P.n_pt;
+      const std::vector<int64_t> cut = even_cuts(nt);
+      csr_target_ranges(nt, cut,
+                        [&](int r, auto&& fn) {
+                          if (cut[r + 1] <= cut[r]) return;
+                          if (which != 3) {
+                            emit_point(which, static_cast<int32_t>(cut[r]), static_cast<int32_t>(cut[r + 1]), fn);
+                          } else {
+                            emit_point(which, P.edge_pt[cut[r]], P.edge_pt[cut[r + 1] - 1] + 1, fn);
+                          }
+                        },
+                        out);
+    }
   }
-  if (!chain_ok) { err = "internal: chain link not adjacent"; return DYNOHIP_ESTRUCT; }
+
 
   plan_mark("before reduced system targets", tmark);
   // ---- reduced system targets ----
@@ -478,52 +656,42 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
   // every point component. Targets are numbered in (B, A) order (band column
   // order); each target's entries keep the enumeration order below.
   {
-    // the pair enumeration in pieces: piece 0 = the factors, pieces 1.. =
-    // contiguous component ranges (comp_cut)
-    const int n_pieces = 1 + std::max(1, std::min(7, P.n_comp / 2048));
-    std::vector<int> comp_cut(n_pieces);
-    for (int r = 1; r < n_pieces; ++r)
-      comp_cut[r - 1] = static_cast<int>(static_cast<int64_t>(P.n_comp) * (r - 1) / (n_pieces - 1));
-    comp_cut[n_pieces - 1] = P.n_comp;
-    auto emit_pairs_piece = [&](int piece, auto&& pair_fn) {  // pair_fn(A, B, entry)
-      if (piece == 0) {
-        for (int t = 0; t < kNTypes; ++t) {
-          const TypePlan& tp = P.types[t];
-          const int nk = kNKeys[t], d = kDim[t];
-          for (int i = 0; i < tp.n; ++i)
-            for (int sa = 0; sa < nk; ++sa) {
-              if (kSlotKind[t][sa] != 0) continue;
-              const int32_t A = tp.idx[i * nk + sa];
-              for (int sb = 0; sb < nk; ++sb) {
-                if (kSlotKind[t][sb] != 0) continue;
-                const int32_t B = tp.idx[i * nk + sb];
-                if (A < B) continue;
-                pair_fn(A, B, GEntry{block_off(tp, t, i, sa), block_off(tp, t, i, sb), d, 1});
-              }
+    // the pair enumeration: the factors' pose pairs, then every component's
+    // neighbour-pose pairs, components in order
+    auto emit_factor_pairs = [&](auto&& pair_fn) {  // pair_fn(A, B, entry)
+      for (int t = 0; t < kNTypes; ++t) {
+        const TypePlan& tp = P.types[t];
+        const int nk = kNKeys[t], d = kDim[t];
+        for (int i = 0; i < tp.n; ++i)
+          for (int sa = 0; sa < nk; ++sa) {
+            if (kSlotKind[t][sa] != 0) continue;
+            const int32_t A = tp.idx[i * nk + sa];
+            for (int sb = 0; sb < nk; ++sb) {
+              if (kSlotKind[t][sb] != 0) continue;
+              const int32_t B = tp.idx[i * nk + sb];
+              if (A < B) continue;
+              pair_fn(A, B, GEntry{block_off(tp, t, i, sa), block_off(tp, t, i, sb), d, 1});
             }
-        }
-        return;
+          }
       }
-      for (int c = comp_cut[piece - 1]; c < comp_cut[piece]; ++c) {
-        const int32_t nb0 = P.comp_nb_start[c], m = P.comp_nb_start[c + 1] - nb0;
-        for (int a = 0; a < m; ++a) {
-          const int32_t A = P.nb_pose[nb0 + a];
-          for (int b = 0; b <= a; ++b) {
-            const int32_t B = P.nb_pose[nb0 + b];
-            for (int32_t q = P.nbedge_start[nb0 + a]; q < P.nbedge_start[nb0 + a + 1]; ++q) {
-              const int i = P.nbedge_pt[q];
-              const uint32_t y = static_cast<uint32_t>(P.comp_y_base[c] + 18ll * (static_cast<int64_t>(i) * m + b));
-              pair_fn(A, B, GEntry{P.nbedge_w[q], y, 3, -1});
-            }
+    };
+    auto emit_comp_pairs = [&](int c, auto&& pair_fn) {
+      const int32_t nb0 = P.comp_nb_start[c], m = P.comp_nb_start[c + 1] - nb0;
+      for (int a = 0; a < m; ++a) {
+        const int32_t A = P.nb_pose[nb0 + a];
+        for (int b = 0; b <= a; ++b) {
+          const int32_t B = P.nb_pose[nb0 + b];
+          for (int32_t q = P.nbedge_start[nb0 + a]; q < P.nbedge_start[nb0 + a + 1]; ++q) {
+            const int i = P.nbedge_pt[q];
+            const uint32_t y = static_cast<uint32_t>(P.comp_y_base[c] + 18ll * (static_cast<int64_t>(i) * m + b));
+            pair_fn(A, B, GEntry{P.nbedge_w[q], y, 3, -1});
           }
         }
       }
     };
-    auto emit_pairs = [&](auto&& pair_fn) {
-      for (int r = 0; r < n_pieces; ++r) emit_pairs_piece(r, pair_fn);
-    };
-    // gradient gathers per pose: J_A^T b per factor, then -W_A v per component
-    auto emit_grad = [&](auto&& fn) {
+    // gradient gathers per pose: J_A^T b per factor, then -W_A v per
+    // component (components without a neighbour pose in [p0, p1) skipped)
+    auto emit_grad = [&](auto&& fn, int64_t p0, int64_t p1) {
       for (int t = 0; t < kNTypes; ++t) {
         const TypePlan& tp = P.types[t];
         const int nk = kNKeys[t], d = kDim[t];
@@ -533,6 +701,7 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
       }
       for (int c = 0; c < P.n_comp; ++c) {
         const int32_t nb0 = P.comp_nb_start[c], m = P.comp_nb_start[c + 1] - nb0;
+        if (m == 0 || P.nb_pose[nb0 + m - 1] < p0 || P.nb_pose[nb0] >= p1) continue;
         for (int a = 0; a < m; ++a)
           for (int32_t q = P.nbedge_start[nb0 + a]; q < P.nbedge_start[nb0 + a + 1]; ++q)
             fn(P.nb_pose[nb0 + a], GEntry{P.nbedge_w[q], static_cast<uint32_t>(P.off_v + 3ull * (P.comp_start[c] + P.nbedge_pt[q])), 3, -1});
@@ -612,13 +781,26 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
     auto tid = [&](int32_t A, int32_t B) -> int32_t {
       return dense ? id_dense[static_cast<size_t>(A) * span + (A - B)] : id_map.at(pkey(A, B));
     };
-    std::thread grad([&] { csr_two_pass(P.n_pose, emit_grad, P.gGred); });
-    csr_ranges(P.red_A.size(), n_pieces,
-               [&](int piece, auto&& fn) {
-                 emit_pairs_piece(piece, [&](int32_t A, int32_t B, const GEntry& e) { fn(tid(A, B), e); });
-               },
-               P.gRed);
-    grad.join();
+    // per worker, the B range of its targets: a component whose neighbour
+    // poses (sorted) miss it emits nothing there and is skipped whole
+    const std::vector<int64_t> rcut = even_cuts(static_cast<int64_t>(P.red_A.size()));
+    csr_target_ranges(P.red_A.size(), rcut,
+                      [&](int r, auto&& fn) {
+                        if (rcut[r + 1] <= rcut[r]) return;
+                        const int32_t blo = P.red_B[rcut[r]], bhi = P.red_B[rcut[r + 1] - 1];
+                        auto pf = [&](int32_t A, int32_t B, const GEntry& e) {
+                          if (B >= blo && B <= bhi) fn(tid(A, B), e);
+                        };
+                        emit_factor_pairs(pf);
+                        for (int c = 0; c < P.n_comp; ++c) {
+                          const int32_t nb0 = P.comp_nb_start[c], nb1 = P.comp_nb_start[c + 1];
+                          if (nb1 == nb0 || P.nb_pose[nb1 - 1] < blo || P.nb_pose[nb0] > bhi) continue;
+                          emit_comp_pairs(c, pf);
+                        }
+                      },
+                      P.gRed);
+    const std::vector<int64_t> gcut = even_cuts(P.n_pose);
+    csr_target_ranges(P.n_pose, gcut, [&](int r, auto&& fn) { emit_grad(fn, gcut[r], gcut[r + 1]); }, P.gGred);
   }
   plan_mark("reduced system targets", tmark);
 

@@ -23,7 +23,10 @@
 #pragma once
 
 #include <cstdint>
+#include <memory>
 #include <string>
+#include <type_traits>
+#include <utility>
 #include <vector>
 
 #include "../../include/dynohip.h"
@@ -85,9 +88,28 @@ struct BackPart {
 // this many (256 CUs x several 256-thread, few-KB-LDS workgroups each)
 constexpr int kBackPersistMax = 1024;
 
+// resize() leaves new elements uninitialised (large gather lists are filled
+// completely right after; zeroing them first costs a pass of page faults)
+template <typename T, typename A = std::allocator<T>>
+struct default_init_allocator : A {
+  using A::A;
+  template <typename U>
+  struct rebind {
+    using other = default_init_allocator<U, typename std::allocator_traits<A>::template rebind_alloc<U>>;
+  };
+  template <typename U>
+  void construct(U* p) noexcept(std::is_nothrow_default_constructible<U>::value) {
+    ::new (static_cast<void*>(p)) U;
+  }
+  template <typename U, typename... Args>
+  void construct(U* p, Args&&... args) {
+    std::allocator_traits<A>::construct(static_cast<A&>(*this), p, std::forward<Args>(args)...);
+  }
+};
+
 struct GatherList {
   std::vector<int64_t> start;  // ntargets + 1
-  std::vector<GEntry> ent;
+  std::vector<GEntry, default_init_allocator<GEntry>> ent;
   size_t ntargets() const { return start.empty() ? 0 : start.size() - 1; }
 };
 

@@ -26,23 +26,39 @@ using namespace dynohip;
 
 namespace {
 
+// Device buffer that keeps its allocation: a handle re-planned for another
+// graph (the next sliding window, the next full-batch call) reuses it when it
+// is large enough, so only growth pays hipMalloc/hipFree (a device-wide
+// synchronising call). Contents are not preserved across alloc().
 template <typename T>
 struct DevBuf {
   T* p = nullptr;
   size_t n = 0;
+  size_t cap = 0;
   ~DevBuf() { release(); }
   void release() {
     if (p) (void)hipFree(p);
     p = nullptr;
-    n = 0;
+    n = cap = 0;
   }
   hipError_t alloc(size_t count) {
+    if (count <= cap) {
+      n = count;
+      return hipSuccess;
+    }
     release();
+    const size_t c = count + count / 8;   // some headroom for the next graph
+    const hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), c * sizeof(T));
+    if (e != hipSuccess) {
+      p = nullptr;
+      return e;
+    }
     n = count;
-    if (count == 0) return hipSuccess;
-    return hipMalloc(reinterpret_cast<void**>(&p), count * sizeof(T));
+    cap = c;
+    return hipSuccess;
   }
-  hipError_t upload(const std::vector<T>& v, hipStream_t s) {
+  template <class Alloc>
+  hipError_t upload(const std::vector<T, Alloc>& v, hipStream_t s) {
     hipError_t e = alloc(v.size());
     if (e != hipSuccess || v.empty()) return e;
     return hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s);
@@ -144,6 +160,7 @@ struct dynohip_solver {
   double phase_ms[7] = {};   // accumulated: lin, schur, assembly, chol, solve, backsub+linerr, retract+error
   int64_t n_lin = 0, n_solves = 0;
   dynohip_stats base_stats{};
+  bool base_stats_valid = false;   // computed on first dynohip_get_stats after a re-plan
   // partitioned full-batch solve (partition.cpp): this handle is rank
   // `rank` of `nranks`; `comm` sums over ranks
   int nranks = 1, rank = 0;
@@ -785,7 +802,7 @@ int dynohip_set_values(dynohip_solver* s, const uint64_t* keys, const uint8_t* k
     s->value_keys.assign(keys, keys + n);
     s->value_kind.assign(kind, kind + n);
     s->has_plan = true;
-    compute_base_stats(s);
+    s->base_stats_valid = false;
   }
   s->lin_valid = false;
   Plan& P = s->plan;
@@ -963,8 +980,9 @@ int dynohip_values_snapshot(dynohip_solver* s) {
   if (rc) return rc;
   (void)hipSetDevice(s->device);
   const Plan& P = s->plan;
-  if (!s->pose_snap.p && P.n_pose) HIPCHK(s, s->pose_snap.alloc(12ull * P.n_pose));
-  if (!s->pt_snap.p && P.n_pt) HIPCHK(s, s->pt_snap.alloc(3ull * P.n_pt));
+  // sized for the current plan (a re-planned handle may hold a larger graph)
+  if (P.n_pose) HIPCHK(s, s->pose_snap.alloc(12ull * P.n_pose));
+  if (P.n_pt) HIPCHK(s, s->pt_snap.alloc(3ull * P.n_pt));
   if (P.n_pose) HIPCHK(s, hipMemcpyAsync(s->pose_snap.p, s->pose.p, 12ull * P.n_pose * sizeof(double), hipMemcpyDeviceToDevice, s->stream));
   if (P.n_pt) HIPCHK(s, hipMemcpyAsync(s->pt_snap.p, s->pt.p, 3ull * P.n_pt * sizeof(double), hipMemcpyDeviceToDevice, s->stream));
   HIPCHK(s, hipStreamSynchronize(s->stream));
@@ -975,7 +993,8 @@ int dynohip_values_restore(dynohip_solver* s) {
   int rc = ready(s);
   if (rc) return rc;
   const Plan& P = s->plan;
-  if ((P.n_pose && !s->pose_snap.p) || (P.n_pt && !s->pt_snap.p)) return set_err(s, DYNOHIP_ESTATE, "no snapshot");
+  if ((P.n_pose && s->pose_snap.n != 12ull * P.n_pose) || (P.n_pt && s->pt_snap.n != 3ull * P.n_pt))
+    return set_err(s, DYNOHIP_ESTATE, "no snapshot of the current graph's values");
   (void)hipSetDevice(s->device);
   s->lin_valid = false;
   if (P.n_pose) HIPCHK(s, hipMemcpyAsync(s->pose.p, s->pose_snap.p, 12ull * P.n_pose * sizeof(double), hipMemcpyDeviceToDevice, s->stream));
@@ -986,6 +1005,10 @@ int dynohip_values_restore(dynohip_solver* s) {
 
 int dynohip_get_stats(dynohip_solver* s, dynohip_stats* out) {
   if (!s || !out) return DYNOHIP_EINVAL;
+  if (s->has_plan && !s->base_stats_valid) {
+    compute_base_stats(s);
+    s->base_stats_valid = true;
+  }
   *out = s->base_stats;
   out->ms_linearize = s->phase_ms[0];
   out->ms_schur = s->phase_ms[1];
