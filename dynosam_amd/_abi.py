@@ -280,6 +280,7 @@ class RefineBatch(C.Structure):
         ("m_k", C.POINTER(C.c_double)),
         ("X_k_1_init", C.POINTER(C.c_double)),
         ("X_k_init", C.POINTER(C.c_double)),
+        ("ternary_inactive", C.POINTER(C.c_uint8)),
     ]
 
 

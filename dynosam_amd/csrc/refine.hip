@@ -414,6 +414,7 @@ struct Batch {
   double* lin;      // kLin per tracklet
   double* pts;      // 2 buffers x 6 per tracklet: [m_{k-1} | m_k]
   uint8_t* active;  // the tracklet's ternary factor is in the graph
+  const uint8_t* inactive0;  // initial mask (ternary out of the graph at the start)
   uint8_t* outlier;
   double* H_out;
   long long* prof;  // DYNOREFINE_PROFILE builds: 8 phase tick counters per problem
@@ -484,7 +485,7 @@ void k_refine(Batch B) {
       p[i] = B.m1[3 * t + i];
       p[3 + i] = B.m2[3 * t + i];
     }
-    B.active[t] = 1;
+    B.active[t] = B.inactive0[t] ? 0 : 1;
     B.outlier[t] = 0;
   }
   __syncthreads();
@@ -938,7 +939,7 @@ struct dynorefine_solver {
   int64_t n_track = 0;
   DevBuf<int32_t> ts;
   DevBuf<double> X1, X2, X1i, X2i, H0, K, kp1, kp2, m1, m2, lin, pts, Hout;
-  DevBuf<uint8_t> active, outlier;
+  DevBuf<uint8_t> active, outlier, inactive0;
   DevBuf<dynorefine_result> res;
   float last_ms = 0.f;
   bool solved = false;
@@ -1039,6 +1040,11 @@ int dynorefine_upload(dynorefine_solver* s, const dynorefine_batch* b) {
   RCHK(s, s->lin.alloc(static_cast<size_t>(kLin) * (nt ? nt : 1)));
   RCHK(s, s->pts.alloc(12 * static_cast<size_t>(nt ? nt : 1)));
   RCHK(s, s->active.alloc(nt ? nt : 1));
+  RCHK(s, s->inactive0.alloc(nt ? nt : 1));
+  if (b->ternary_inactive && nt)
+    RCHK(s, hipMemcpyAsync(s->inactive0.p, b->ternary_inactive, nt, hipMemcpyHostToDevice, st));
+  else
+    RCHK(s, hipMemsetAsync(s->inactive0.p, 0, nt ? nt : 1, st));
   RCHK(s, s->outlier.alloc(nt ? nt : 1));
   RCHK(s, s->Hout.alloc(12 * (n ? n : 1)));
   RCHK(s, s->res.alloc(n ? n : 1));
@@ -1079,6 +1085,7 @@ int dynorefine_solve(dynorefine_solver* s, const dynorefine_params* p, const dyn
   B.lin = s->lin.p;
   B.pts = s->pts.p;
   B.active = s->active.p;
+  B.inactive0 = s->inactive0.p;
   B.outlier = s->outlier.p;
   B.H_out = s->Hout.p;
   B.res = s->res.p;

@@ -33,6 +33,7 @@ class RefineBatch:
     m_k: np.ndarray           # (T, 3)
     X_k_1_init: np.ndarray = None  # optional initial values (default: the priors)
     X_k_init: np.ndarray = None
+    ternary_inactive: np.ndarray = None  # optional (T,) bool: ternaries out of the graph at the start
 
     @property
     def n(self):
@@ -78,8 +79,14 @@ class MotionOnlyRefinementOptimizer:
         inits = [None if a is None else np.ascontiguousarray(a, dtype=np.float64)
                  for a in (batch.X_k_1_init, batch.X_k_init)]
         self._keep += [a for a in inits if a is not None]
+        inact = None
+        if batch.ternary_inactive is not None:
+            inact = np.ascontiguousarray(batch.ternary_inactive, dtype=np.uint8)
+            assert inact.shape == (int(ts[-1]),)
+            self._keep.append(inact)
         b = _abi.RefineBatch(batch.n, ts.ctypes.data_as(C.POINTER(C.c_int32)), *[_dp(a) for a in self._keep[:8]],
-                             *[C.POINTER(C.c_double)() if a is None else _dp(a) for a in inits])
+                             *[C.POINTER(C.c_double)() if a is None else _dp(a) for a in inits],
+                             C.POINTER(C.c_uint8)() if inact is None else inact.ctypes.data_as(C.POINTER(C.c_uint8)))
         self._check(self._lib.dynorefine_upload(self._h, C.byref(b)))
         self._n, self._nt = batch.n, int(ts[-1])
 

@@ -57,6 +57,10 @@ typedef struct {
      the reference). Lets a test restart the solver from any LM state. */
   const double* X_k_1_init;
   const double* X_k_init;
+  /* Optional, 1 per tracklet: 1 = the tracklet's ternary factor starts out
+     of the graph (null: every ternary present, as in the reference). Lets a
+     test restart the outlier_reject = 2 re-solve from any LM state. */
+  const uint8_t* ternary_inactive;
 } dynorefine_batch;
 
 typedef struct {
