@@ -80,5 +80,5 @@ def test_dynorefine_exports_every_declared_symbol():
     assert len(names) >= 9
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
-    assert C.sizeof(_abi.RefineBatch) == 8 + 11 * 8
+    assert C.sizeof(_abi.RefineBatch) == 8 + 12 * 8
     assert C.sizeof(_abi.RefineResult) == 4 * 4 + 2 * 8
