@@ -326,15 +326,6 @@ __device__ __forceinline__ bool factor_tile_blk(v4d (&accA)[4], v4d (&accX)[4], 
   }
 }
 
-// y = L^-1 v (64, L^-1 in LDS with stride LD, lower): 4 lanes per row
-__device__ __forceinline__ double lower_gemv4(const double* Li, const double* v, int tid) {
-  const int row = tid >> 2, part = tid & 3;
-  double s = 0.0;
-  for (int m = part; m <= row; m += 4) s += Li[row * LD + m] * v[m];
-  s += __shfl_xor(s, 1);
-  s += __shfl_xor(s, 2);
-  return s;
-}
 
 // ---- global memory access of the factorisation --------------------------
 // The level kernels (SC1 = false) read tiles written by earlier launches
@@ -487,28 +478,18 @@ __device__ __forceinline__ void diag_pending(v4d (&accA)[4], const double* Ps, i
   }
 }
 
-// As -= Qs Rs^T on this wave's 32x32 quadrant
-__device__ __forceinline__ void own_pending_quadrant(double* As, const double* Qs, const double* Rs, int w, int l) {
-  v4d acc[2][2];
-  mfma_abt(Qs, Rs, w, l, acc);
-#pragma unroll
-  for (int ti = 0; ti < 2; ++ti)
-#pragma unroll
-    for (int tj = 0; tj < 2; ++tj)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) As[MFMA_ROW(w, l, ti, rr) * LD + MFMA_COL(w, l, tj)] -= acc[ti][tj][rr];
-}
 
 
 struct TaskLds {
-  double Ps[T * LD];   // pending diagonal operand L(k, c) -> later L_kk^-1
+  double Ps[T * LD];   // pending diagonal operand L(k, c) -> later L_kk^-1; second pair operand otherwise
   double Qs[T * LD];   // pair operand A
-  double Rs[T * LD];   // pair operand B
   double As[T * LD];   // own tile (i, k)
   double Xch[2 * 4 * 256];
+  double Ust[16 * 256];  // own panels: W_c = U_cc^-1 at [c][c], U[c][TJ] at [c][TJ] (16x16, accumulator layout)
   double rpart[4][T];
   double vv[T];        // r_k minus the contributions of eliminated columns
   double yv[T];        // y_k = L_kk^-1 vv
+  double tv[4][16];    // forward substitution scratch, per block
 };
 
 // Launch-invariant inputs of a panel task: operand slots, the entries of
@@ -529,10 +510,12 @@ __device__ __forceinline__ PanelPre panel_prefetch(const TileDev& b, const TileT
   PanelPre p;
   const bool own = tk.i != tk.k;
   const int npd = tk.pd_end - tk.pd_beg, npo = own ? tk.po_end - tk.po_beg : 0;
-  p.fast = npd <= 1 && npo <= 1;
   p.pd = npd == 1 ? pairs[2 * tk.pd_beg] : -1;
   p.qa = npo == 1 ? pairs[2 * tk.po_beg] : -1;
   p.rb = npo == 1 ? pairs[2 * tk.po_beg + 1] : -1;
+  // the own pair's second operand L(k,c) must be the first one or the pending
+  // diagonal operand already in Ps (always so in practice); else the slow path
+  p.fast = npd <= 1 && npo <= 1 && (p.rb == p.qa || p.rb == p.pd);
   p.rbeg = b.row_start[tk.k];
   p.rend = b.row_start[tk.k + 1];
   const int wu = __builtin_amdgcn_readfirstlane(w);
@@ -546,14 +529,22 @@ __device__ __forceinline__ PanelPre panel_prefetch(const TileDev& b, const TileT
 }
 
 // acc += -P_bi P_bj^T for 16x16 blocks (bi, bj) of a 64x64 LDS operand P,
-// in accumulator layout (the pending update of diagonal block (bi, bj))
+// in accumulator layout (the pending update of diagonal block (bi, bj)).
+// Four independent accumulator chains (k-steps s mod 4) keep the MFMA pipe
+// busy instead of waiting on one dependent chain of 16; summed in a fixed
+// order.
 __device__ __forceinline__ v4d pend_block(v4d acc, const double* Ps, int bi, int bj, int l) {
   const int li = l & 15, lk = l >> 4;
-#pragma unroll 4
-  for (int k0 = 0; k0 < T; k0 += 4)
-    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-Ps[(16 * bi + li) * LD + k0 + lk], Ps[(16 * bj + li) * LD + k0 + lk],
-                                               acc, 0, 0, 0);
-  return acc;
+  v4d c[4];
+#pragma unroll
+  for (int s4 = 0; s4 < 4; ++s4) c[s4] = v4d{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int k0 = 0; k0 < T; k0 += 16)
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4)
+      c[s4] = __builtin_amdgcn_mfma_f64_16x16x4f64(-Ps[(16 * bi + li) * LD + k0 + 4 * s4 + lk],
+                                                   Ps[(16 * bj + li) * LD + k0 + 4 * s4 + lk], c[s4], 0, 0, 0);
+  return acc + ((c[0] + c[1]) + (c[2] + c[3]));
 }
 
 // sum over the 16 lanes of a row group (lanes with equal l >> 4), with DPP
@@ -567,13 +558,146 @@ __device__ __forceinline__ double sum16(double v) {
   return v;
 }
 
-// Own-tile pending update A(i,k) -= Q R^T, in four chunks of 16 k per wave
-// (wave w: block row w, all four block columns). The chunks fill the block
-// steps of the diagonal factorisation in which the wave is not factoring:
-// chunk counts per (wave, step), so every wave carries about the same MFMA
-// load per step (wave 0 also has its pivots in step 0, waves 1-3 their
-// pending diagonal blocks).
-__constant__ constexpr int8_t kOwnChunks[4][4] = {{0, 3, 1, 0}, {0, 0, 2, 2}, {1, 2, 0, 1}, {2, 1, 1, 0}};
+// ---- own panels (i != k): the factorisation with the TRSM folded in ----
+// L(i,k) = A(i,k) U^-1 (U = L_kk^T) by block forward substitution over the
+// four 16-column blocks c, interleaved with the block steps of the diagonal
+// factorisation: wave w keeps XT[c] = (block (w, c) of L(i,k))^T and forms
+//   XT[c] = W_c^T (A(w,c)^T - sum_{c' < c} U[c'][c]^T XT[c'])
+// as soon as W_c = U_cc^-1 and U[c'][c] are out (the U blocks stay in LDS,
+// Ust). y_k = L_kk^-1 vv is the same substitution on the right-hand side,
+// done by the factoring wave of each step. No explicit L_kk^-1 is formed
+// (the diagonal task stores it for the backward substitution), so there is
+// no inverse row to finish after the last step: one substitution block per
+// wave follows the final barrier instead of the whole TRSM.
+//
+// The own-tile pending update A(i,k) -= Q R^T runs in four column chunks
+// (16 MFMAs each, into As) and the substitution blocks are scheduled per wave
+// into the slots of the factorisation in which the wave would otherwise
+// wait: I<KB> before block step KB (not on the factoring wave), B<KB> after
+// its barrier. A chunk precedes the substitution block of its columns; the
+// wave that factors next does nothing extra after the barrier before its
+// step. y_c = W_c^T (vv_c - sum_{c' < c} U[c'][c]^T y_c') is latency-bound
+// small work: it runs after barrier c (its inputs are out by then), off the
+// factoring wave's path. Actions: 0x10 + c = chunk c, 0x20 + c = substitution
+// block c, 0x30 + c = y_c.
+constexpr int kOwnAct[4][8][4] = {
+    // I0           B0                          I1                  B1                          I2            B2                     I3            B3
+    {{0, 0, 0, 0}, {0x30, 0x10, 0x20, 0x11}, {0, 0, 0, 0}, {0x31, 0x21, 0x12, 0}, {0, 0, 0, 0}, {0x32, 0x22, 0x13, 0}, {0, 0, 0, 0}, {0x23, 0, 0, 0}},
+    {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0x10, 0x20, 0x11, 0x21}, {0, 0, 0, 0}, {0x12, 0x22, 0x13, 0}, {0, 0, 0, 0}, {0x33, 0x23, 0, 0}},
+    {{0x10, 0, 0, 0}, {0x20, 0, 0, 0}, {0x11, 0x12, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0x21, 0x22, 0, 0}, {0x13, 0, 0, 0}, {0x23, 0, 0, 0}},
+    {{0x10, 0x11, 0, 0}, {0x20, 0, 0, 0}, {0x12, 0x13, 0, 0}, {0x21, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0x22, 0x23, 0, 0}},
+};
+
+__device__ __forceinline__ v4d ld_blk(const double* p, int l) {
+  v4d v;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] = p[r * 64 + l];
+  return v;
+}
+__device__ __forceinline__ void st_blk(double* p, const v4d& v, int l) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) p[r * 64 + l] = v[r];
+}
+
+// sum over the four row groups (lanes l, l^16, l^32, l^48)
+__device__ __forceinline__ double sum_groups(double v) {
+  v += __shfl_xor(v, 16);
+  v += __shfl_xor(v, 32);
+  return v;
+}
+
+template <int w, class DiagPend, class Chunk>
+__device__ bool factor_own_w(v4d (&accA)[4], v4d (&XT)[4], int l, TaskLds& S, DiagPend&& diagpend, Chunk&& chunk,
+                             int q) {
+  bool ok = true;
+  const int li = l & 15, g = l >> 4;
+  double* const U = S.Ust;
+  auto Ublk = [&](int c, int tj) { return U + (c * 4 + tj) * 256; };
+  auto subst = [&](int c) {
+    v4d Tm;   // A(w, c)^T: element (j = g + 4r, i = li) = A[16w + i][16c + j]
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Tm[r] = S.As[(16 * w + li) * LD + 16 * c + g + 4 * r];
+    // the c' terms as independent chains, subtracted in order
+    v4d sum[3];
+#pragma unroll
+    for (int cp = 0; cp < 3; ++cp)
+      if (cp < c) sum[cp] = mfma_tn(ld_blk(Ublk(cp, c), l), XT[cp], v4d{0.0, 0.0, 0.0, 0.0}, false);
+#pragma unroll
+    for (int cp = 0; cp < 3; ++cp)
+      if (cp < c) Tm -= sum[cp];
+    XT[c] = mfma_tn(ld_blk(Ublk(c, c), l), Tm, v4d{0.0, 0.0, 0.0, 0.0}, false);
+  };
+  auto ystep = [&](int c) {   // y_c = W_c^T (vv_c - sum_{c' < c} U[c'][c]^T y_c')
+    double part = 0.0;
+#pragma unroll
+    for (int cp = 0; cp < 3; ++cp)
+      if (cp < c) {
+        const v4d u = ld_blk(Ublk(cp, c), l);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) part += u[r] * S.yv[16 * cp + g + 4 * r];
+      }
+    const double t = S.vv[16 * c + li] - sum_groups(part);
+    if (g == 0) S.tv[c][li] = t;
+    const v4d Wc = ld_blk(Ublk(c, c), l);
+    double yp = 0.0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) yp += Wc[r] * S.tv[c][g + 4 * r];
+    yp = sum_groups(yp);
+    if (g == 0) S.yv[16 * c + li] = yp;
+  };
+  auto act = [&](int slot) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int x = kOwnAct[w][slot][a];
+      if (x >= 0x30) ystep(x - 0x30);
+      else if (x >= 0x20) subst(x - 0x20);
+      else if (x >= 0x10) chunk(x - 0x10);
+    }
+  };
+#pragma unroll
+  for (int KB = 0; KB < 4; ++KB) {
+    if (w != KB) {
+      if (KB == 0) diagpend();
+      act(2 * KB);
+    } else {
+      v4d Wm;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Wm[r] = (g + 4 * r == li) ? 1.0 : 0.0;
+      TCLKW(16 + 4 * KB, q);
+      factor16_wave(accA[KB], Wm, l, ok, &S.rpart[w][0]);
+      TCLKW(17 + 4 * KB, q);
+      st_blk(Ublk(KB, KB), Wm, l);
+#pragma unroll
+      for (int TJ = KB + 1; TJ < 4; ++TJ) {
+        accA[TJ] = mfma_tn(Wm, accA[TJ], v4d{0.0, 0.0, 0.0, 0.0}, false);
+        st_blk(Ublk(KB, TJ), accA[TJ], l);
+      }
+      TCLKW(18 + 4 * KB, q);
+    }
+    __syncthreads();
+    TCLK(12 + KB, q, rtc());
+    if (w == KB) TCLKW(19 + 4 * KB, q);
+    if (w > KB) {
+      const v4d Uv = ld_blk(Ublk(KB, w), l);
+#pragma unroll
+      for (int TJ = 0; TJ < 4; ++TJ)
+        if (TJ >= w) accA[TJ] = mfma_tn(Uv, ld_blk(Ublk(KB, TJ), l), accA[TJ], true);
+    }
+    act(2 * KB + 1);
+  }
+  return ok;
+}
+
+template <class DiagPend, class Chunk>
+__device__ __forceinline__ bool factor_own(v4d (&accA)[4], v4d (&XT)[4], int w, int l, TaskLds& S,
+                                           DiagPend&& diagpend, Chunk&& chunk, int q) {
+  switch (__builtin_amdgcn_readfirstlane(w)) {
+    case 0: return factor_own_w<0>(accA, XT, l, S, diagpend, chunk, q);
+    case 1: return factor_own_w<1>(accA, XT, l, S, diagpend, chunk, q);
+    case 2: return factor_own_w<2>(accA, XT, l, S, diagpend, chunk, q);
+    default: return factor_own_w<3>(accA, XT, l, S, diagpend, chunk, q);
+  }
+}
 
 template <bool SC1>
 __device__ __forceinline__ void panel_task(const TileDev& b, const TileTask& tk, const int32_t* __restrict__ pairs,
@@ -581,7 +705,6 @@ __device__ __forceinline__ void panel_task(const TileDev& b, const TileTask& tk,
                                            double* __restrict__ y, int* fail, TaskLds& S, int q = 0) {
   double* const Ps = S.Ps;
   double* const Qs = S.Qs;
-  double* const Rs = S.Rs;
   double* const As = S.As;
   const int tid = threadIdx.x;
   const int w = tid >> 6, l = tid & 63;
@@ -590,7 +713,7 @@ __device__ __forceinline__ void panel_task(const TileDev& b, const TileTask& tk,
   // (1) one round trip: the diagonal tile (stored symmetric) into registers,
   // the right-hand side contributions L(k,c) y_c of eliminated columns, and
   // the operand tiles into LDS
-  v4d accA[4], accX[4];
+  v4d accA[4];
   const double* diag = slot_ptr(b, tk.diag);
 #pragma unroll
   for (int TJ = 0; TJ < 4; ++TJ)
@@ -598,7 +721,6 @@ __device__ __forceinline__ void panel_task(const TileDev& b, const TileTask& tk,
     for (int rr = 0; rr < 4; ++rr) {
       const int row = ACC_ROW(w, l, rr), col = ACC_COL(TJ, l);
       accA[TJ][rr] = TJ >= w ? gld<SC1>(diag + row * T + col) : 0.0;
-      accX[TJ][rr] = row == col ? 1.0 : 0.0;
     }
   double cv[kCsMax];
 #pragma unroll
@@ -606,8 +728,7 @@ __device__ __forceinline__ void panel_task(const TileDev& b, const TileTask& tk,
     cv[j] = p.cs[j] >= 0 ? gld<SC1>(contrib + static_cast<int64_t>(p.cs[j]) * T + l) : 0.0;
   if (p.fast) {
     load_tiles_lds<SC1>(p.pd >= 0 ? slot_ptr(b, p.pd) : nullptr, Ps, own ? slot_ptr(b, tk.dst) : nullptr, As,
-                        p.qa >= 0 ? slot_ptr(b, p.qa) : nullptr, Qs,
-                        p.rb >= 0 && p.rb != p.qa && p.rb != p.pd ? slot_ptr(b, p.rb) : nullptr, Rs, tid);
+                        p.qa >= 0 ? slot_ptr(b, p.qa) : nullptr, Qs, nullptr, nullptr, tid);
   }
   {
     double sacc = 0.0;
@@ -625,7 +746,7 @@ __device__ __forceinline__ void panel_task(const TileDev& b, const TileTask& tk,
       load_tile_lds_t<SC1>(slot_ptr(b, tk.dst), As, tid);
       if (tk.po_end > tk.po_beg) {
         v4d acc[2][2];
-        sum_pairs<SC1>(b, pairs, tk.po_beg, tk.po_end, Qs, Rs, tid, w, l, acc);
+        sum_pairs<SC1>(b, pairs, tk.po_beg, tk.po_end, Qs, Ps, tid, w, l, acc);   // Ps is free until the pd loop
 #pragma unroll
         for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
@@ -664,49 +785,78 @@ __device__ __forceinline__ void panel_task(const TileDev& b, const TileTask& tk,
         for (int rr = 0; rr < 4; ++rr) accA[TJ][rr] += S.Xch[4 * 256 + TJ * 256 + rr * 64 + l];
     }
   }
-  // the own pair's second operand is L(k,c): usually the pending diagonal
-  // operand already in Ps (read only before Ps receives L_kk^-1)
-  const double* Rop = p.rb == p.qa ? Qs : p.rb == p.pd ? Ps : Rs;
-  v4d ao[4];
-#pragma unroll
-  for (int TJ = 0; TJ < 4; ++TJ) ao[TJ] = v4d{0.0, 0.0, 0.0, 0.0};
-  auto own_chunk = [&](int c) {
-#pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4) {
-      const int k = 16 * c + 4 * s4 + lk;
-      const double a = Qs[(16 * w + li) * LD + k];
-#pragma unroll
-      for (int TJ = 0; TJ < 4; ++TJ)
-        ao[TJ] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Rop[(16 * TJ + li) * LD + k], ao[TJ], 0, 0, 0);
-    }
-  };
-  auto idle = [&](int KB) {
-    if (KB == 0 && dp) {
-      // this wave's own diagonal blocks (w, TJ >= w), before it factors
+  // this wave's own diagonal blocks (w, TJ >= w), before it factors
+  auto diagpend = [&]() {
+    if (dp) {
 #pragma unroll
       for (int TJ = 1; TJ < 4; ++TJ)
         if (TJ >= w) accA[TJ] = pend_block(accA[TJ], Ps, w, TJ, l);
     }
-    if (op) {
-      int c0 = 0;
-      for (int kb = 0; kb < KB; ++kb) c0 += kOwnChunks[w][kb];
-      const int c1 = c0 + kOwnChunks[w][KB];
-      for (int c = c0; c < c1; ++c) own_chunk(c);
-    }
   };
   TCLK(2, q, rtc());
+  if (own) {
+    // the own pair's second operand L(k,c): the first one or the pending
+    // diagonal operand (Ps, read only before it is overwritten)
+    const double* Rop = p.rb == p.qa ? Qs : Ps;
+    auto chunk = [&](int c) {   // As(w, c) -= Q(w, :) R(c, :)^T, all 64 k in order
+      if (!op) return;
+      v4d ao[4];   // four independent chains (k-steps s mod 4), summed in order
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) ao[s4] = v4d{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int k0 = 0; k0 < T; k0 += 16)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+          ao[s4] = __builtin_amdgcn_mfma_f64_16x16x4f64(Qs[(16 * w + li) * LD + k0 + 4 * s4 + lk],
+                                                        Rop[(16 * c + li) * LD + k0 + 4 * s4 + lk], ao[s4], 0, 0, 0);
+      const v4d tot = (ao[0] + ao[1]) + (ao[2] + ao[3]);
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) As[ACC_ROW(w, l, rr) * LD + ACC_COL(c, l)] -= tot[rr];
+    };
+    v4d XT[4];
+    factor_own(accA, XT, w, l, S, diagpend, chunk, q);
+    __syncthreads();   // y_3 (wave 1, after the last barrier)
+    TCLK(3, q, rtc());
+    TCLK(8, q, rtc());
+    TCLK(9, q, rtc());
+    // L(i,k) row block w into As (its own rows, row-major), contribution
+    // L(i,k) y_k of its rows from registers
+    double cp = 0.0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        As[(16 * w + li) * LD + 16 * c + lk + 4 * r] = XT[c][r];
+        cp += XT[c][r] * S.yv[16 * c + lk + 4 * r];
+      }
+    cp = sum_groups(cp);
+    TCLK(10, q, rtc());
+    // coalesced 16-byte stores of the 16 rows (write-through in the dataflow kernel)
+    double* dst = slot_ptr(b, tk.dst);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, T * T * 8, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int e = l + 64 * i, row = 16 * w + (e >> 5), c2 = 2 * (e & 31);
+      const d2v v = d2v{As[row * LD + c2], As[row * LD + c2 + 1]};
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) int, v), rs,
+                                             (row * T + c2) * 8, 0, SC1 ? 16 : 0);
+    }
+    TCLK(11, q, rtc());
+    if (lk == 0) gst<SC1>(contrib + static_cast<int64_t>(tk.dst) * T + 16 * w + li, cp);
+    return;
+  }
+  // the diagonal task: L_kk^-1 for the backward substitution, y_k
+  v4d accX[4];
+#pragma unroll
+  for (int TJ = 0; TJ < 4; ++TJ)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) accX[TJ][rr] = ACC_ROW(w, l, rr) == ACC_COL(TJ, l) ? 1.0 : 0.0;
+  auto idle = [&](int KB) {
+    if (KB == 0) diagpend();
+  };
   const bool ok = factor_tile_blk(accA, accX, w, l, S.Xch, &S.rpart[w][0], idle, q);
   TCLK(3, q, rtc());
-  if (!ok && !own && tid == 0) *fail = 1;
-  if (op) {
-    // wave 3 factors in the last step: its chunks ran before it
-#pragma unroll
-    for (int TJ = 0; TJ < 4; ++TJ)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) As[ACC_ROW(w, l, rr) * LD + ACC_COL(TJ, l)] -= ao[TJ][rr];
-  }
-  // L_kk^-1 -> Ps (full square; upper part is exactly zero) and this wave's
-  // rows of y_k = L_kk^-1 vv, reduced across the row groups in registers
+  if (!ok && tid == 0) *fail = 1;
   double yp[4];
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) yp[rr] = 0.0;
@@ -714,64 +864,19 @@ __device__ __forceinline__ void panel_task(const TileDev& b, const TileTask& tk,
   for (int TJ = 0; TJ < 4; ++TJ) {
     const double vj = S.vv[16 * TJ + li];
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      Ps[ACC_ROW(w, l, rr) * LD + ACC_COL(TJ, l)] = accX[TJ][rr];
+    for (int rr = 0; rr < 4; ++rr)
       if (TJ <= w) yp[rr] += accX[TJ][rr] * vj;
-    }
   }
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) yp[rr] = sum16(yp[rr]);
+  double* dst = Linv + static_cast<int64_t>(tk.k) * T * T;
+#pragma unroll
+  for (int TJ = 0; TJ < 4; ++TJ)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) dst[ACC_ROW(w, l, rr) * T + ACC_COL(TJ, l)] = accX[TJ][rr];
   if (li == 0) {
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) S.yv[ACC_ROW(w, l, rr)] = yp[rr];
-  }
-  if (!own) {
-    double* dst = Linv + static_cast<int64_t>(tk.k) * T * T;
-#pragma unroll
-    for (int TJ = 0; TJ < 4; ++TJ)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) dst[ACC_ROW(w, l, rr) * T + ACC_COL(TJ, l)] = accX[TJ][rr];
-    if (li == 0) {
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) y[static_cast<int64_t>(tk.k) * T + ACC_ROW(w, l, rr)] = yp[rr];
-    }
-    return;
-  }
-  __syncthreads();
-  TCLK(8, q, rtc());
-  TCLK(9, q, rtc());
-  // L(i, k) = A L_kk^-T: wave w forms block row w; block column TJ needs
-  // k < 16 (TJ + 1) only (L_kk^-1 is lower triangular, the rest adds zeros)
-  v4d acc[4];
-#pragma unroll
-  for (int TJ = 0; TJ < 4; ++TJ) acc[TJ] = v4d{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int k0 = 0; k0 < T; k0 += 4) {
-    const double a = As[(16 * w + li) * LD + k0 + lk];
-#pragma unroll
-    for (int TJ = 0; TJ < 4; ++TJ)
-      if (k0 < 16 * (TJ + 1))
-        acc[TJ] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Ps[(16 * TJ + li) * LD + k0 + lk], acc[TJ], 0, 0, 0);
-  }
-  TCLK(10, q, rtc());
-  double* dst = slot_ptr(b, tk.dst);
-  double cp[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int TJ = 0; TJ < 4; ++TJ) {
-    const double yj = S.yv[16 * TJ + li];
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      gst<SC1>(dst + ACC_ROW(w, l, rr) * T + ACC_COL(TJ, l), acc[TJ][rr]);
-      cp[rr] += acc[TJ][rr] * yj;
-    }
-  }
-  TCLK(11, q, rtc());
-  // contribution of this tile to row i's right-hand side: L(i, k) y_k
-#pragma unroll
-  for (int rr = 0; rr < 4; ++rr) cp[rr] = sum16(cp[rr]);
-  if (li == 0) {
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) gst<SC1>(contrib + static_cast<int64_t>(tk.dst) * T + ACC_ROW(w, l, rr), cp[rr]);
+    for (int rr = 0; rr < 4; ++rr) y[static_cast<int64_t>(tk.k) * T + ACC_ROW(w, l, rr)] = yp[rr];
   }
 }
 
@@ -783,7 +888,7 @@ __global__ __launch_bounds__(256) void k_tasks(TileDev b, const TileTask* __rest
   const TileTask tk = tasks[blockIdx.x];
   const int tid = threadIdx.x;
   if (tk.kind == 1) {
-    run_update<false>(b, tk, pairs, S.Qs, S.Rs, tid, tid >> 6, tid & 63);
+    run_update<false>(b, tk, pairs, S.Qs, S.Ps, tid, tid >> 6, tid & 63);
     return;
   }
   const PanelPre p = panel_prefetch(b, tk, pairs, r, tid >> 6, tid & 63);
@@ -850,7 +955,7 @@ __global__ __launch_bounds__(256) void k_factor_persist(TileDev b, const TileTas
     }
     __syncthreads();
     TCLK(1, q, rtc());
-    if (tk.kind == 1) run_update<true>(b, tk, pairs, S.Qs, S.Rs, tid, w, l);
+    if (tk.kind == 1) run_update<true>(b, tk, pairs, S.Qs, S.Ps, tid, w, l);
     else panel_task<true>(b, tk, pairs, p, Linv, contrib, y, fail, S, q);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();

@@ -134,11 +134,15 @@ def test_execution_paths_agree(gpu_available, name):
 
 
 def test_llworld_formulation(gpu_available):
+    """Free-running LLWorld. The object poses are pinned only weakly (see
+    test_llworld_per_iteration_conditioned), so the last accept/reject
+    decisions of a free run depend on the summation order: one iteration
+    either way is allowed; the end point must still agree."""
     g, v, _, s = make("T2", formulation=1)
     sg = s.optimize()
     o = Oracle(g, v)
     so = o.optimize()
-    assert sg.iterations == so.iterations
+    assert abs(sg.iterations - so.iterations) <= 1
     assert sg.final_error == pytest.approx(so.final_error, rel=1e-4)
     m = gauge_mask(v)
     assert rel(s.values_data()[m], o.values_data()[m]) < 1e-4
