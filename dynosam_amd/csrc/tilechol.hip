@@ -136,11 +136,29 @@ __device__ __forceinline__ double* slot_ptr(const TileDev& b, int32_t slot) {
 __device__ __forceinline__ double bcast_row_lane(double v, int p) {
   // lane p of every 16-lane row -> the whole row (DPP row_newbcast)
   switch (p) {
-#define NB(q) case q: return __builtin_amdgcn_update_dpp(v, v, 0x150 + q, 0xf, 0xf, false);
+// (every source lane exists, so no "old" value is needed: one v_mov_b64_dpp
+// instead of a copy plus an in-place DPP move)
+#define NB(q) case q: return __builtin_amdgcn_update_dpp(__builtin_nan(""), v, 0x150 + q, 0xf, 0xf, true);
     NB(0) NB(1) NB(2) NB(3) NB(4) NB(5) NB(6) NB(7) NB(8) NB(9) NB(10) NB(11) NB(12) NB(13) NB(14) NB(15)
 #undef NB
   }
   return v;
+}
+
+// row group G (lanes 16G..16G+15) of v broadcast to all four row groups with
+// the gfx950 lane swaps: permlane32_swap(v, v) gives [r0 r1 r0 r1] and
+// [r2 r3 r2 r3], permlane16_swap of one of them with itself gives its two
+// rows each broadcast. Four VALU swaps, no LDS round trip (ds_bpermute).
+__device__ __forceinline__ unsigned row_bcast32(unsigned v, int G) {
+  const auto a = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  const unsigned s = G < 2 ? a[0] : a[1];
+  const auto b = __builtin_amdgcn_permlane16_swap(s, s, false, false);
+  return (G & 1) ? b[1] : b[0];
+}
+__device__ __forceinline__ double row_bcast(double v, int G) {
+  const unsigned lo = row_bcast32(static_cast<unsigned>(__double2loint(v)), G);
+  const unsigned hi = row_bcast32(static_cast<unsigned>(__double2hiint(v)), G);
+  return __hiloint2double(static_cast<int>(hi), static_cast<int>(lo));
 }
 
 __device__ __forceinline__ double pull_lane(double v, int src) {
@@ -173,7 +191,7 @@ __device__ __forceinline__ void factor16_wave(v4d& B, v4d& W, int l, bool& ok, d
   for (int p = 0; p < 16; ++p) {
     const int rp = p >> 2, gp = p & 3;
     const double d = read_lane(B[rp], 16 * gp + p);
-    const double rowp = pull_lane(B[rp], j + 16 * gp);  // B[p][j]
+    const double rowp = row_bcast(B[rp], gp);           // B[p][j]
     const double f = rowp * rcp_nr(d);                   // U[p][j] / U[p][p]
     asm volatile("" : "+v"(jd));
     const double fm = jd > 0 ? f : 0.0;
@@ -551,10 +569,10 @@ __device__ __forceinline__ v4d pend_block(v4d acc, const double* Ps, int bi, int
 // moves only: quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror
 // (a symmetric tree: every lane gets the same, bit-identical sum)
 __device__ __forceinline__ double sum16(double v) {
-  v += __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xf, 0xf, false);
-  v += __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xf, 0xf, false);
-  v += __builtin_amdgcn_update_dpp(v, v, 0x141, 0xf, 0xf, false);
-  v += __builtin_amdgcn_update_dpp(v, v, 0x140, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(__builtin_nan(""), v, 0xB1, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(__builtin_nan(""), v, 0x4E, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(__builtin_nan(""), v, 0x141, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(__builtin_nan(""), v, 0x140, 0xf, 0xf, true);
   return v;
 }
 
