@@ -455,8 +455,11 @@ __device__ __forceinline__ void load_tiles_lds(const double* s0, double* d0, con
 // pair's operands are fetched in one round trip; further pairs (rare) one
 // by one
 template <bool SC1>
+// pa0 / pb0: the first pair's slots when the caller fetched them before the
+// dependency wait (-1: read them here)
 __device__ __forceinline__ void run_update(const TileDev& b, const TileTask& tk, const int32_t* __restrict__ pairs,
-                                           double* Qs, double* Rs, int tid, int w, int l) {
+                                           double* Qs, double* Rs, int tid, int w, int l, int32_t pa0 = -1,
+                                           int32_t pb0 = -1) {
   double* dst = slot_ptr(b, tk.dst);
   double old[2][2][4];
 #pragma unroll
@@ -468,7 +471,8 @@ __device__ __forceinline__ void run_update(const TileDev& b, const TileTask& tk,
   v4d acc[2][2];
   zero_acc(acc);
   for (int e = tk.po_beg; e < tk.po_end; ++e) {
-    const int32_t pa = pairs[2 * e], pb = pairs[2 * e + 1];
+    const bool pre = e == tk.po_beg && pa0 >= 0;
+    const int32_t pa = pre ? pa0 : pairs[2 * e], pb = pre ? pb0 : pairs[2 * e + 1];
     if (e > tk.po_beg) __syncthreads();
     load_tiles_lds<SC1>(slot_ptr(b, pa), Qs, pb != pa ? slot_ptr(b, pb) : nullptr, Rs, nullptr, nullptr, nullptr,
                         nullptr, tid);
@@ -957,7 +961,13 @@ __global__ __launch_bounds__(256) void k_factor_persist(TileDev b, const TileTas
     TCLK(0, q, rtc());
     TCLK(5, q, blockIdx.x);
     PanelPre p;
-    if (tk.kind == 0) p = panel_prefetch(b, tk, pairs, r, w, l);
+    int32_t upa = -1, upb = -1;   // an update's first operand pair
+    if (tk.kind == 0) {
+      p = panel_prefetch(b, tk, pairs, r, w, l);
+    } else if (tk.po_end > tk.po_beg) {
+      upa = pairs[2 * tk.po_beg];
+      upb = pairs[2 * tk.po_beg + 1];
+    }
     if (w == 0) {
       bool ok = true;
       for (int j = dep_start[q] + l; j < dep_start[q + 1]; j += 64) {
@@ -973,7 +983,7 @@ __global__ __launch_bounds__(256) void k_factor_persist(TileDev b, const TileTas
     }
     __syncthreads();
     TCLK(1, q, rtc());
-    if (tk.kind == 1) run_update<true>(b, tk, pairs, S.Qs, S.Ps, tid, w, l);
+    if (tk.kind == 1) run_update<true>(b, tk, pairs, S.Qs, S.Ps, tid, w, l, upa, upb);
     else panel_task<true>(b, tk, pairs, p, Linv, contrib, y, fail, S, q);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
