@@ -1085,12 +1085,41 @@ __device__ void chain_solve_y_thread(const ChainDev& cd, double* __restrict__ ar
   }
 }
 
-// thread per (chain, neighbour pose) pair: with 18 right-hand-side columns
-// a step has enough arithmetic to cover the prefetched loads, and a 16-lane
-// group per pair would leave 15 lanes idle per step
-__global__ __launch_bounds__(kBlock) void k_chain_solve_y(ChainDev cd, double* __restrict__ arena) {
-  const int q = blockIdx.x * kBlock + static_cast<int>(threadIdx.x);
-  if (q < cd.n_nb) chain_solve_y_thread(cd, arena, q);
+// Y = D^-1 W = L^-T L^-1 W for the lone points (static landmarks, chains of
+// one point): a lane per (edge, column of W) in edge order, so a wave reads
+// and writes ~10 consecutive 3x6 blocks with unit stride between lanes and
+// no index chain (edge -> point is one load; W, L and Y offsets follow from
+// the edge index). The same per-column arithmetic as chain_solve_y_thread's
+// n = 1 case (lsolve then ltsolve).
+__device__ __forceinline__ void lone_solve_y(const ChainDev& cd, double* __restrict__ arena, int64_t g) {
+  const int64_t le = g / 6;
+  const int col = static_cast<int>(g - 6 * le);
+  const int64_t e = cd.e_lone0 + le;
+  const int pt = cd.edge_pt[e];
+  double L[9], x[3];
+  ldk(arena + cd.off_L + 9ll * pt, L);
+  const double* W = arena + cd.off_W + 18 * e;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) x[r] = W[6 * r + col];
+  lsolve<1>(L, x);
+  ltsolve<1>(L, x);
+  double* Y = arena + cd.y_lone_base + 18 * le;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) Y[6 * r + col] = x[r];
+}
+
+// Blocks [0, nbl): a thread per (chain, neighbour pose) pair of the long
+// chains (with 18 right-hand-side columns a step has enough arithmetic to
+// cover the prefetched loads); then a lane per (edge, column) of the lone
+// points.
+__global__ __launch_bounds__(kBlock) void k_chain_solve_y(ChainDev cd, double* __restrict__ arena, int nbl) {
+  if (static_cast<int>(blockIdx.x) < nbl) {
+    const int q = blockIdx.x * kBlock + static_cast<int>(threadIdx.x);
+    if (q < cd.n_nb_long) chain_solve_y_thread(cd, arena, q);
+    return;
+  }
+  const int64_t g = static_cast<int64_t>(blockIdx.x - nbl) * kBlock + threadIdx.x;
+  if (g < 6ll * cd.n_lone_edges) lone_solve_y(cd, arena, g);
 }
 
 // t_e = W_e dX_pose(e) for every point-pose edge (edge-parallel)
@@ -1396,7 +1425,9 @@ void launch_chain_factor(const ChainDev& c, double* arena, double lambda, int* f
 }
 void launch_chain_solve_y(const ChainDev& c, double* arena, hipStream_t s) {
   if (c.n_nb == 0) return;
-  k_chain_solve_y<<<nblocks(c.n_nb), kBlock, 0, s>>>(c, arena);
+  const int nbl = nblocks(c.n_nb_long);
+  const int nb = nbl + nblocks(6ll * c.n_lone_edges);
+  if (nb > 0) k_chain_solve_y<<<nb, kBlock, 0, s>>>(c, arena, nbl);
 }
 void launch_backsub(const ChainDev& c, int n_edge, const double* arena, const double* dpose, double* wdx, double* dpt,
                     hipStream_t s) {

@@ -63,6 +63,10 @@ struct ChainDev {
   const uint32_t* nbedge_w = nullptr;
   const int32_t* pt_edge_start = nullptr;
   const int32_t* edge_pose = nullptr;
+  const int32_t* edge_pt = nullptr;
+  int e_lone0 = 0;        // first edge of the lone points
+  int n_lone_edges = 0;   // their edges (the Y blocks follow edge order from y_lone_base)
+  uint64_t y_lone_base = 0;
   uint64_t off_D = 0, off_E = 0, off_gp = 0, off_W = 0, off_v = 0, off_L = 0, off_M = 0;
 };
 

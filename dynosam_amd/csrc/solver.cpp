@@ -121,7 +121,7 @@ struct dynohip_solver {
   TypeDev td[kNTypes];
   GatherBufs gD, gE, gGp, gW, gRed, gGred;
   DevBuf<int32_t> redA, redB;
-  DevBuf<int32_t> comp_start, comp_nb_start, nb_comp, nbedge_start, nbedge_pt, pt_edge_start, edge_pose;
+  DevBuf<int32_t> comp_start, comp_nb_start, nb_comp, nbedge_start, nbedge_pt, pt_edge_start, edge_pose, edge_pt;
   DevBuf<int64_t> comp_y_base;
   DevBuf<uint32_t> nbedge_w;
   DevBuf<double> slots, gred, xy, dpt, wdx, linv, contrib;
@@ -247,6 +247,7 @@ int upload_plan(dynohip_solver* s) {
   HIPCHK(s, s->nbedge_w.upload(P.nbedge_w, st));
   HIPCHK(s, s->pt_edge_start.upload(P.pt_edge_start, st));
   HIPCHK(s, s->edge_pose.upload(P.edge_pose, st));
+  HIPCHK(s, s->edge_pt.upload(P.edge_pt, st));
   HIPCHK(s, s->slots.alloc(static_cast<size_t>(P.n_slots) * kTile * kTile));
   HIPCHK(s, s->tile_pos.upload(P.tile_pos, st));
   HIPCHK(s, s->row_start.upload(P.row_start, st));
@@ -288,6 +289,15 @@ int upload_plan(dynohip_solver* s) {
   c.nbedge_w = s->nbedge_w.p;
   c.pt_edge_start = s->pt_edge_start.p;
   c.edge_pose = s->edge_pose.p;
+  c.edge_pt = s->edge_pt.p;
+  // lone points (every chain after the long ones): their edges, and their Y
+  // blocks, are contiguous in edge order (plan.cpp's lone-point layout)
+  {
+    const int32_t p0 = c.n_long < P.n_comp ? P.comp_start[c.n_long] : P.n_pt;
+    c.e_lone0 = p0 < P.n_pt ? P.pt_edge_start[p0] : P.n_edge;
+    c.n_lone_edges = P.n_edge - c.e_lone0;
+    c.y_lone_base = c.n_long < P.n_comp ? static_cast<uint64_t>(P.comp_y_base[c.n_long]) : 0;
+  }
   c.off_D = P.off_D;
   c.off_E = P.off_E;
   c.off_gp = P.off_gp;
