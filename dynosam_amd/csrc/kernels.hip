@@ -990,9 +990,12 @@ __global__ __launch_bounds__(kBlock) void k_chain_factor(ChainDev cd, double* __
   }
 }
 
-// Y = C^-1 W for one (chain, neighbour pose) pair: thread per pair, the
-// next point's L, M and W prefetched in the forward sweep.
-__device__ void chain_solve_y_thread(const ChainDev& cd, double* __restrict__ arena, int q) {
+// Y = C^-1 W for one (chain, neighbour pose) pair and one column `col` of
+// W (3x6): a lane per (pair, column), the next point's L, M and W column
+// prefetched in the forward sweep. The six columns are independent; one
+// lane per column keeps the per-step chain of exactly rounded divisions
+// (3 per column) short instead of issuing 18 per step on one lane.
+__device__ void chain_solve_y_col(const ChainDev& cd, double* __restrict__ arena, int q, int col) {
   const int c = cd.nb_comp[q];
   const int nb0 = cd.comp_nb_start[c];
   const int m = cd.comp_nb_start[c + 1] - nb0;
@@ -1015,8 +1018,8 @@ __device__ void chain_solve_y_thread(const ChainDev& cd, double* __restrict__ ar
     }
   }
   int ci = 0;
-  // rhs of point i: W of edge (i, b) if the point sees pose b, else 0
-  auto load_rhs = [&](int i, double (&rhs)[18]) {
+  // rhs of point i: column col of W of edge (i, b) if the point sees pose b, else 0
+  auto load_rhs = [&](int i, double (&rhs)[3]) {
     int pt = -1;
     uint32_t w = 0;
     if (cached) {
@@ -1028,21 +1031,22 @@ __device__ void chain_solve_y_thread(const ChainDev& cd, double* __restrict__ ar
       w = cd.nbedge_w[ep];
     }
     if (pt == i) {
-      ldk(arena + w, rhs);
+#pragma unroll
+      for (int r = 0; r < 3; ++r) rhs[r] = arena[w + 6 * r + col];
       ++ep;
       ++ci;
     } else {
 #pragma unroll
-      for (int k = 0; k < 18; ++k) rhs[k] = 0.0;
+      for (int k = 0; k < 3; ++k) rhs[k] = 0.0;
     }
   };
-  double Z[18], rn[18], Ln[9], Mn[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  double Z[3], rn[3], Ln[9], Mn[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   load_rhs(0, rn);
   ldk(arena + cd.off_L + 9ll * i0, Ln);
   for (int i = 0; i < n; ++i) {
-    double rhs[18], L[9], M[9];
+    double rhs[3], L[9], M[9];
 #pragma unroll
-    for (int k = 0; k < 18; ++k) rhs[k] = rn[k];
+    for (int k = 0; k < 3; ++k) rhs[k] = rn[k];
 #pragma unroll
     for (int k = 0; k < 9; ++k) { L[k] = Ln[k]; M[k] = Mn[k]; }
     if (i + 1 < n) {
@@ -1050,38 +1054,40 @@ __device__ void chain_solve_y_thread(const ChainDev& cd, double* __restrict__ ar
       ldk(arena + cd.off_L + 9ll * (i0 + i + 1), Ln);
       ldk(arena + cd.off_M + 9ll * (i0 + i + 1), Mn);
     }
-    if (i > 0) sub_mx<6>(M, Z, rhs);
-    lsolve<6>(L, rhs);
-    double* yo = Y + 18ll * (static_cast<int64_t>(i) * m + b);
+    if (i > 0) sub_mx<1>(M, Z, rhs);
+    lsolve<1>(L, rhs);
+    double* yo = Y + 18ll * (static_cast<int64_t>(i) * m + b) + col;
 #pragma unroll
-    for (int k = 0; k < 18; ++k) { yo[k] = rhs[k]; Z[k] = rhs[k]; }
+    for (int k = 0; k < 3; ++k) { yo[6 * k] = rhs[k]; Z[k] = rhs[k]; }
   }
   // backward (Z holds Y_{n-1} after the forward sweep); point i-1's Y, L
   // and M_i are fetched before point i's result is stored, so the loads
   // overlap the arithmetic instead of following the store
-  double Yn[18], Lb[9], Mb[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, Yb[18];
+  double Yn[3], Lb[9], Mb[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, Yb[3];
   ldk(arena + cd.off_L + 9ll * (i0 + n - 1), Lb);
   for (int i = n - 1; i >= 0; --i) {
-    double* yo = Y + 18ll * (static_cast<int64_t>(i) * m + b);
-    double x[18], L[9], M[9];
+    double* yo = Y + 18ll * (static_cast<int64_t>(i) * m + b) + col;
+    double x[3], L[9], M[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) { L[k] = Lb[k]; M[k] = Mb[k]; }
     if (i == n - 1) {
 #pragma unroll
-      for (int k = 0; k < 18; ++k) x[k] = Z[k];
+      for (int k = 0; k < 3; ++k) x[k] = Z[k];
     } else {
 #pragma unroll
-      for (int k = 0; k < 18; ++k) x[k] = Yb[k];
+      for (int k = 0; k < 3; ++k) x[k] = Yb[k];
     }
     if (i > 0) {
-      ldk(Y + 18ll * (static_cast<int64_t>(i - 1) * m + b), Yb);
+      const double* yp = Y + 18ll * (static_cast<int64_t>(i - 1) * m + b) + col;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) Yb[k] = yp[6 * k];
       ldk(arena + cd.off_L + 9ll * (i0 + i - 1), Lb);
       ldk(arena + cd.off_M + 9ll * (i0 + i), Mb);
     }
-    if (i < n - 1) sub_mtx<6>(M, Yn, x);
-    ltsolve<6>(L, x);
+    if (i < n - 1) sub_mtx<1>(M, Yn, x);
+    ltsolve<1>(L, x);
 #pragma unroll
-    for (int k = 0; k < 18; ++k) { yo[k] = x[k]; Yn[k] = x[k]; }
+    for (int k = 0; k < 3; ++k) { yo[6 * k] = x[k]; Yn[k] = x[k]; }
   }
 }
 
@@ -1089,7 +1095,7 @@ __device__ void chain_solve_y_thread(const ChainDev& cd, double* __restrict__ ar
 // one point): a lane per (edge, column of W) in edge order, so a wave reads
 // and writes ~10 consecutive 3x6 blocks with unit stride between lanes and
 // no index chain (edge -> point is one load; W, L and Y offsets follow from
-// the edge index). The same per-column arithmetic as chain_solve_y_thread's
+// the edge index). The same per-column arithmetic as chain_solve_y_col's
 // n = 1 case (lsolve then ltsolve).
 __device__ __forceinline__ void lone_solve_y(const ChainDev& cd, double* __restrict__ arena, int64_t g) {
   const int64_t le = g / 6;
@@ -1108,14 +1114,12 @@ __device__ __forceinline__ void lone_solve_y(const ChainDev& cd, double* __restr
   for (int r = 0; r < 3; ++r) Y[6 * r + col] = x[r];
 }
 
-// Blocks [0, nbl): a thread per (chain, neighbour pose) pair of the long
-// chains (with 18 right-hand-side columns a step has enough arithmetic to
-// cover the prefetched loads); then a lane per (edge, column) of the lone
-// points.
+// Blocks [0, nbl): a lane per (pair, column) of the long chains' (chain,
+// neighbour pose) pairs; then a lane per (edge, column) of the lone points.
 __global__ __launch_bounds__(kBlock) void k_chain_solve_y(ChainDev cd, double* __restrict__ arena, int nbl) {
   if (static_cast<int>(blockIdx.x) < nbl) {
-    const int q = blockIdx.x * kBlock + static_cast<int>(threadIdx.x);
-    if (q < cd.n_nb_long) chain_solve_y_thread(cd, arena, q);
+    const int g = blockIdx.x * kBlock + static_cast<int>(threadIdx.x);
+    if (g < 6 * cd.n_nb_long) chain_solve_y_col(cd, arena, g / 6, g % 6);
     return;
   }
   const int64_t g = static_cast<int64_t>(blockIdx.x - nbl) * kBlock + threadIdx.x;
@@ -1425,7 +1429,7 @@ void launch_chain_factor(const ChainDev& c, double* arena, double lambda, int* f
 }
 void launch_chain_solve_y(const ChainDev& c, double* arena, hipStream_t s) {
   if (c.n_nb == 0) return;
-  const int nbl = nblocks(c.n_nb_long);
+  const int nbl = nblocks(6ll * c.n_nb_long);
   const int nb = nbl + nblocks(6ll * c.n_lone_edges);
   if (nb > 0) k_chain_solve_y<<<nb, kBlock, 0, s>>>(c, arena, nbl);
 }
