@@ -10,9 +10,11 @@
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <algorithm>
 #include <cstring>
 #include <string>
@@ -803,8 +805,15 @@ int dynohip_set_values(dynohip_solver* s, const uint64_t* keys, const uint8_t* k
                                                     s->local_graph, s->err)
                            : build_plan(g, keys, kind, n, s->plan, s->err);
     if (rc) return rc;
+    static const bool timing = std::getenv("DYNOHIP_PLAN_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
     rc = upload_plan(s);
     if (rc) return rc;
+    if (timing) {
+      (void)hipStreamSynchronize(s->stream);
+      std::fprintf(stderr, "[plan] upload                       %8.2f ms\n",
+                   std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
     if (s->nranks > 1) {
       rc = upload_partition(s);
       if (rc) return rc;

@@ -29,6 +29,7 @@
 #include <string>
 #include <cstdint>
 #include <functional>
+#include <thread>
 #include <vector>
 
 #include "plan.hpp"
@@ -438,12 +439,21 @@ bool build_tile_schedule(Plan& P) {
   schedule(NT, adj, maxnb, g_leaf_override > 0 ? g_leaf_override : 0, best, nr);
   if (!best.ok) return false;
   if (g_leaf_override < 0) {
+    // the candidate leaf sizes are independent schedules: built on threads,
+    // then the cheapest kept in list order (the same choice as a serial scan)
+    std::vector<int> leaves;
     for (int leaf : {4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128, 192, 256}) {
       if (leaf * nr >= NT) break;
-      Sched cand;
-      schedule(NT, adj, maxnb, leaf, cand, nr);
-      if (cand.ok && cand.cost < best.cost) best = std::move(cand);
+      leaves.push_back(leaf);
     }
+    std::vector<Sched> cand(leaves.size());
+    std::vector<std::thread> th;
+    for (size_t c = 1; c < leaves.size(); ++c)
+      th.emplace_back([&, c] { schedule(NT, adj, maxnb, leaves[c], cand[c], nr); });
+    if (!leaves.empty()) schedule(NT, adj, maxnb, leaves[0], cand[0], nr);
+    for (auto& t : th) t.join();
+    for (auto& c : cand)
+      if (c.ok && c.cost < best.cost) best = std::move(c);
   }
   P.nd_leaf = best.leaf;
   P.tile_pos = best.pos;
