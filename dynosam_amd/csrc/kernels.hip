@@ -21,6 +21,7 @@ namespace dynohip {
 namespace {
 
 constexpr int kBlock = 256;
+typedef double v4d __attribute__((ext_vector_type(4)));
 
 inline int nblocks(int64_t n, int b = kBlock) { return static_cast<int>((n + b - 1) / b); }
 
@@ -1126,6 +1127,188 @@ __global__ __launch_bounds__(kBlock) void k_chain_solve_y(ChainDev cd, double* _
   if (g < 6ll * cd.n_lone_edges) lone_solve_y(cd, arena, g);
 }
 
+// ---- lone-point groups: the static landmarks' Schur contributions ----
+// A workgroup per group (plan.hpp LoneGroup): up to kLoneSub points sharing
+// m neighbour poses. With D = L L^T the damped point block (factored by
+// k_chain_factor), Z_a = L^-1 W_a and z = L^-1 g_p, the group's
+// contributions are
+//   pair (a, b), a >= b:  sum_p [a == b] J_a^T J_a - Z_a^T Z_b   (= W_a^T D^-1 W_b)
+//   gradient a:           sum_p J_a^T b_a - Z_a^T z             (= W_a^T D^-1 g_p)
+// The group's index block is one coalesced load; every load of the points'
+// W, J | b, L and g_p is then issued before the first LDS store (one memory
+// round trip), Z and z are formed in LDS, and each thread owns one output
+// row: row r of pair (a, b) (6 sums) or of gradient a. Sums run over the
+// points in member order (deterministic). Each point's data is read once
+// per solve, instead of once per reduced-block entry it feeds.
+constexpr int kLoneStage = (kLoneSub * 18 * kLoneMaxNb + kBlock - 1) / kBlock;   // W (and J) loads per thread
+static_assert(kLoneSub * 3 * kLoneMaxNb <= 2 * kBlock && 9 * kLoneSub <= kBlock, "lone staging of b, L");
+__host__ __device__ constexpr int lone_point_doubles(int m) { return 39 * m + 12; }  // Z, J, b, z, L
+constexpr int kLoneNT = (6 * kLoneMaxNb + 15) / 16;                 // 16-column tiles of Z, at most
+constexpr int kLoneWT = (kLoneNT * (kLoneNT + 1) / 2 + 3) / 4;      // lower tiles per wave, at most
+static_assert(6 * kLoneMaxNb <= 64, "one lane per J_a^T J_a / gradient row");
+
+#ifdef DYNOHIP_LONE_CLOCK
+// per workgroup of the last k_lone_schur launch: s_memrealtime (100 MHz) at
+// start, index block staged, point data staged, Z formed, sums done, end
+// (tools/lone_clock.py)
+__device__ unsigned long long g_lclk[8][8192];
+#define LCLK(i)                                                                                   \
+  do {                                                                                            \
+    if (threadIdx.x == 0 && blockIdx.x < 8192) g_lclk[i][blockIdx.x] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define LCLK(i) \
+  do {          \
+  } while (0)
+#endif
+
+__global__ __launch_bounds__(kBlock) void k_lone_schur(LoneSchurDev d, double* __restrict__ arena) {
+  extern __shared__ double lds[];
+  __shared__ int32_t hdr[kLoneBlk];
+  const int tid = threadIdx.x;
+  LCLK(0);
+  if (blockIdx.x == 0 && tid < 36) arena[d.off_I6 + tid] = (tid % 7 == 0) ? 1.0 : 0.0;
+  for (int q = tid; q < kLoneBlk; q += kBlock) hdr[q] = d.blk[static_cast<int64_t>(blockIdx.x) * kLoneBlk + q];
+  __syncthreads();
+  LCLK(1);
+  const int m = hdr[0], npt = hdr[1], m18 = 18 * m, np = m * (m + 1) / 2, ntask = 6 * np + 6 * m;
+  const int32_t* spt = hdr + 4;
+  const int32_t* se0 = hdr + 4 + kLoneSub;
+  const int32_t* srec = hdr + 4 + 2 * kLoneSub;
+  double* sZ = lds;                       // [point][a][k][c]: W, then Z in place
+  double* sJ = sZ + kLoneSub * m18;       // [point][a][k][c]
+  double* sB = sJ + kLoneSub * m18;       // [point][a][k]
+  double* sz = sB + kLoneSub * 3 * m;     // [point][k]: g_p, then z in place
+  double* sL = sz + 3 * kLoneSub;         // [point][9]
+  const int nW = npt * m18, nB = npt * 3 * m;
+  {
+    double rw[kLoneStage], rj[kLoneStage], rb[2], rl = 0.0, rg = 0.0;
+#pragma unroll
+    for (int u = 0; u < kLoneStage; ++u) {
+      const int q = tid + kBlock * u;
+      rw[u] = rj[u] = 0.0;
+      if (q < nW) {
+        const int p = q / m18, pa = q / 18;
+        rw[u] = arena[d.off_W + 18ll * se0[p] + (q - p * m18)];
+        rj[u] = arena[static_cast<uint32_t>(srec[pa]) + (q - 18 * pa)];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int q = tid + kBlock * u, pa = q / 3;
+      rb[u] = q < nB ? arena[static_cast<uint32_t>(srec[pa]) + 27 + (q - 3 * pa)] : 0.0;
+    }
+    if (tid < 9 * npt) rl = arena[d.off_L + 9ll * spt[tid / 9] + tid % 9];
+    if (tid < 3 * npt) rg = arena[d.off_gp + 3ll * spt[tid / 3] + tid % 3];
+#pragma unroll
+    for (int u = 0; u < kLoneStage; ++u) {
+      const int q = tid + kBlock * u;
+      if (q < nW) {
+        sZ[q] = rw[u];
+        sJ[q] = rj[u];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      if (tid + kBlock * u < nB) sB[tid + kBlock * u] = rb[u];
+    if (tid < 9 * npt) sL[tid] = rl;
+    if (tid < 3 * npt) sz[tid] = rg;
+  }
+  __syncthreads();
+  LCLK(2);
+  // Z = L^-1 W in place, a thread per (point, a, column); z = L^-1 g_p
+  for (int q = tid; q < npt * m * 6 + npt; q += kBlock) {
+    const bool wcol = q < npt * m * 6;
+    const int pa = q / 6, col = q - 6 * pa, p = wcol ? pa / m : q - npt * m * 6;
+    double* x0 = wcol ? sZ + 18 * pa + col : sz + 3 * p;
+    const int st = wcol ? 6 : 1;
+    double L[9], x[3];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) L[k] = sL[9 * p + k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) x[k] = x0[st * k];
+    lsolve<1>(L, x);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) x0[st * k] = x[k];
+  }
+  __syncthreads();
+  LCLK(3);
+  // S = -Z^T Z over K = 3 npt rows (row 3p + k, column 6a + c of Z) on
+  // v_mfma_f64_16x16x4f64: the lower 16x16 tiles, round-robin over the
+  // waves. Beside them on VALU: wave 3 lane (a, r) sums row r of
+  // J_a^T J_a, wave 2 lane (a, r) row r of gradient a (these two waves hold
+  // fewer tiles). The J_a^T J_a rows meet the tiles through LDS.
+  __shared__ double sJJ[36 * kLoneMaxNb];
+  const int wave = tid >> 6, lane = tid & 63, li = lane & 15, lk = lane >> 4;
+  const int n6 = 6 * m, nt = (n6 + 15) / 16, nl = nt * (nt + 1) / 2, K = 3 * npt, ks = (K + 3) >> 2;
+  v4d acc[kLoneWT];
+#pragma unroll
+  for (int j = 0; j < kLoneWT; ++j) {
+    acc[j] = v4d{0.0, 0.0, 0.0, 0.0};
+    const int t = wave + 4 * j;
+    if (t >= nl) break;
+    int I = 0;
+    while ((I + 1) * (I + 2) / 2 <= t) ++I;
+    const int J = t - I * (I + 1) / 2;
+    const int ca = 16 * I + li, cb = 16 * J + li;
+    const bool va = ca < n6, vb = cb < n6;
+    const int oa = 18 * (ca / 6) + ca % 6, ob = 18 * (cb / 6) + cb % 6;
+    for (int s4 = 0; s4 < ks; ++s4) {
+      const int kp = 4 * s4 + lk, p = kp / 3, ro = p * m18 + 6 * (kp - 3 * p);
+      const bool vk = kp < K;
+      const double za = (va && vk) ? sZ[ro + oa] : 0.0;
+      const double zb = (vb && vk) ? sZ[ro + ob] : 0.0;
+      acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(-za, zb, acc[j], 0, 0, 0);
+    }
+  }
+  const uint32_t out = static_cast<uint32_t>(hdr[2]);
+  if (wave >= 2 && lane < n6) {
+    const int a = lane / 6, r = lane - 6 * a;
+    if (wave == 3) {
+      double jj[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+      for (int p = 0; p < npt; ++p) {
+        const double* Jp = sJ + p * m18 + 18 * a;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const double jr = Jp[6 * k + r];
+#pragma unroll
+          for (int c = 0; c < 6; ++c) jj[c] += jr * Jp[6 * k + c];
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 6; ++c) sJJ[36 * a + 6 * r + c] = jj[c];
+    } else {
+      double g = 0.0;
+      for (int p = 0; p < npt; ++p) {
+        const double* Jp = sJ + p * m18 + 18 * a + r;
+        const double* Zp = sZ + p * m18 + 18 * a + r;
+        const double* Bp = sB + p * 3 * m + 3 * a;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) g += Jp[6 * k] * Bp[k] - Zp[6 * k] * sz[3 * p + k];
+      }
+      arena[out + 36 * np + lane] = g;
+    }
+  }
+  __syncthreads();
+  // lane (li, lk) of a tile holds rows lk + 4i, column li
+#pragma unroll
+  for (int j = 0; j < kLoneWT; ++j) {
+    const int t = wave + 4 * j;
+    if (t >= nl) break;
+    int I = 0;
+    while ((I + 1) * (I + 2) / 2 <= t) ++I;
+    const int J = t - I * (I + 1) / 2;
+    const int col = 16 * J + li, b = col / 6, c = col - 6 * b;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = 16 * I + lk + 4 * i, a = row / 6, r = row - 6 * a;
+      if (row < n6 && col < n6 && b <= a)
+        arena[out + 36 * (a * (a + 1) / 2 + b) + 6 * r + c] = acc[j][i] + (a == b ? sJJ[36 * a + 6 * r + c] : 0.0);
+    }
+  }
+  LCLK(4);
+}
+
 // t_e = W_e dX_pose(e) for every point-pose edge (edge-parallel)
 __global__ __launch_bounds__(kBlock) void k_wdx(ChainDev cd, int n_edge, const double* __restrict__ arena,
                                                 const double* __restrict__ dpose, double* __restrict__ t) {
@@ -1433,6 +1616,22 @@ void launch_chain_solve_y(const ChainDev& c, double* arena, hipStream_t s) {
   const int nb = nbl + nblocks(6ll * c.n_lone_edges);
   if (nb > 0) k_chain_solve_y<<<nb, kBlock, 0, s>>>(c, arena, nbl);
 }
+int debug_lone_clock(void* out) {
+#ifdef DYNOHIP_LONE_CLOCK
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lclk), sizeof(unsigned long long) * 8 * 8192) == hipSuccess ? 0 : -1;
+#else
+  (void)out;
+  return -1;
+#endif
+}
+
+extern "C" int dynohip_debug_lone_clock(unsigned long long* out) { return debug_lone_clock(out); }
+
+void launch_lone_schur(const LoneSchurDev& d, double* arena, hipStream_t s) {
+  if (d.n_group > 0)
+    k_lone_schur<<<d.n_group, kBlock, sizeof(double) * kLoneSub * lone_point_doubles(d.max_m), s>>>(d, arena);
+}
+
 void launch_backsub(const ChainDev& c, int n_edge, const double* arena, const double* dpose, double* wdx, double* dpt,
                     hipStream_t s) {
   if (c.n_comp == 0) return;

@@ -70,6 +70,14 @@ struct ChainDev {
   uint64_t off_D = 0, off_E = 0, off_gp = 0, off_W = 0, off_v = 0, off_L = 0, off_M = 0;
 };
 
+// lone-point groups (plan.hpp LoneGroup), a workgroup per group
+struct LoneSchurDev {
+  int n_group = 0;
+  int max_m = 0;                          // largest m (sizes the staging LDS)
+  const int32_t* blk = nullptr;           // kLoneBlk ints per group
+  uint64_t off_W = 0, off_L = 0, off_gp = 0, off_I6 = 0;
+};
+
 // reduced system in 64x64 tiles; tile (row tile i, column tile j) with
 // pos[i] >= pos[j] lives at slots + slot * 4096 (row-major)
 struct TileDev {
@@ -129,6 +137,10 @@ void launch_sep_rhs(int n_sep_tiles, const int32_t* tile, const int32_t* start, 
 void launch_chain_factor(const ChainDev& c, double* arena, double lambda, int* fail, const ZeroDev& z,
                          hipStream_t s);
 void launch_chain_solve_y(const ChainDev& c, double* arena, hipStream_t s);
+// the lone-point groups' partial reduced blocks and gradients (after
+// launch_chain_factor: reads L and v of the lone points)
+void launch_lone_schur(const LoneSchurDev& d, double* arena, hipStream_t s);
+int debug_lone_clock(void* out);   // -DDYNOHIP_LONE_CLOCK builds: the stamps of the last launch
 // dpt = C^-1 (gp - W dpose); wdx: scratch of 3 doubles per point-pose edge
 void launch_backsub(const ChainDev& c, int n_edge, const double* arena, const double* dpose, double* wdx, double* dpt,
                     hipStream_t s);

@@ -569,6 +569,7 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
   // owning a point range walks only its points' references, and every
   // target still lists its entries in factor order.
   bool chain_ok = true;
+  std::vector<uint8_t> lone_grouped(P.n_pt, 0);   // per point: in a lone-point group
   {
     std::vector<int64_t> rstart(static_cast<size_t>(P.n_pt) + 1, 0);
     for (int t = 0; t < kNTypes; ++t) {
@@ -646,6 +647,111 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
                         },
                         out);
     }
+
+    // ---- lone-point groups (plan.hpp LoneGroup) ----
+    // Eligible: a lone point with 1..kLoneMaxNb neighbour poses and exactly
+    // one PoseToPoint factor per neighbour (every static landmark of the
+    // formulations). Grouped by the neighbour list (bucketed by its first
+    // pose, then compared), in point order; a group is split into
+    // near-equal subgroups of at most kLoneSub points.
+    P.lgroup.clear();
+    P.lone_pose.clear();
+    P.lone_blk.clear();
+    P.lone_max_m = 0;
+    int32_t c_long = 0;
+    while (c_long < P.n_comp && P.comp_start[c_long + 1] - P.comp_start[c_long] >= 2) ++c_long;
+    const int32_t p_lone = c_long < P.n_comp ? P.comp_start[c_long] : P.n_pt;
+    const int32_t e_l0 = p_lone < P.n_pt ? P.pt_edge_start[p_lone] : P.n_edge;
+    const int32_t n_lone = P.n_pt - p_lone;
+    std::vector<uint8_t> ok(static_cast<size_t>(n_lone), 0);
+    std::vector<uint32_t> prec(static_cast<size_t>(P.n_edge - e_l0));
+    const TypePlan& t0 = P.types[0];
+    parallel_for(n_lone, [&](int64_t q0, int64_t q1) {
+      for (int64_t q = q0; q < q1; ++q) {
+        const int32_t pt = p_lone + static_cast<int32_t>(q);
+        const int32_t e0 = P.pt_edge_start[pt], m = P.pt_edge_start[pt + 1] - e0;
+        if (m < 1 || m > kLoneMaxNb || rstart[pt + 1] - rstart[pt] != m) continue;
+        uint32_t seen = 0;
+        bool good = true;
+        for (int64_t k = rstart[pt]; k < rstart[pt + 1]; ++k) {
+          const uint64_t r = refs[k];
+          const int i = static_cast<int>(r >> 8);
+          if (((r >> 4) & 15) != 0) { good = false; break; }
+          const int a = find_edge(pt, t0.idx[2 * i]) - e0;
+          if ((seen >> a) & 1u) { good = false; break; }
+          seen |= 1u << a;
+          prec[e0 - e_l0 + a] = block_off(t0, 0, i, 0);
+        }
+        ok[q] = good;
+      }
+    });
+    std::vector<int32_t> fstart(static_cast<size_t>(P.n_pose) + 1, 0), byfirst;
+    for (int32_t q = 0; q < n_lone; ++q)
+      if (ok[q]) fstart[P.edge_pose[P.pt_edge_start[p_lone + q]] + 1]++;
+    for (int32_t x = 0; x < P.n_pose; ++x) fstart[x + 1] += fstart[x];
+    byfirst.resize(fstart[P.n_pose]);
+    {
+      std::vector<int32_t> cur(fstart.begin(), fstart.end() - 1);
+      for (int32_t q = 0; q < n_lone; ++q)
+        if (ok[q]) byfirst[cur[P.edge_pose[P.pt_edge_start[p_lone + q]]]++] = p_lone + q;
+    }
+    auto same_list = [&](int32_t u, int32_t v) {
+      const int32_t eu = P.pt_edge_start[u], ev = P.pt_edge_start[v], m = P.pt_edge_start[u + 1] - eu;
+      if (P.pt_edge_start[v + 1] - ev != m) return false;
+      for (int32_t a = 0; a < m; ++a)
+        if (P.edge_pose[eu + a] != P.edge_pose[ev + a]) return false;
+      return true;
+    };
+    align2();
+    P.off_I6 = arena;
+    arena += 36;
+    std::vector<std::vector<int32_t>> cls;
+    int64_t n_grouped = 0;
+    for (int32_t x = 0; x < P.n_pose; ++x) {
+      cls.clear();
+      for (int32_t k = fstart[x]; k < fstart[x + 1]; ++k) {
+        const int32_t pt = byfirst[k];
+        size_t ci = 0;
+        while (ci < cls.size() && !same_list(cls[ci][0], pt)) ++ci;
+        if (ci == cls.size()) cls.emplace_back();
+        cls[ci].push_back(pt);
+      }
+      for (const std::vector<int32_t>& mem : cls) {
+        const int32_t e0 = P.pt_edge_start[mem[0]], m = P.pt_edge_start[mem[0] + 1] - e0;
+        const int32_t n = static_cast<int32_t>(mem.size()), nsub = (n + kLoneSub - 1) / kLoneSub;
+        for (int32_t u = 0; u < nsub; ++u) {
+          const int32_t k0 = static_cast<int32_t>(int64_t{n} * u / nsub), k1 = static_cast<int32_t>(int64_t{n} * (u + 1) / nsub);
+          LoneGroup G;
+          G.m = m;
+          G.npt = k1 - k0;
+          G.pose_beg = static_cast<int32_t>(P.lone_pose.size());
+          G.out = static_cast<uint32_t>(arena);
+          arena += 36ull * (m * (m + 1) / 2) + 6ull * m;
+          P.lone_max_m = std::max(P.lone_max_m, m);
+          for (int32_t a = 0; a < m; ++a) P.lone_pose.push_back(P.edge_pose[e0 + a]);
+          const size_t bo = P.lone_blk.size();
+          P.lone_blk.resize(bo + kLoneBlk);
+          int32_t* blk = P.lone_blk.data() + bo;
+          std::fill(blk, blk + kLoneBlk, 0);
+          blk[0] = m;
+          blk[1] = G.npt;
+          blk[2] = static_cast<int32_t>(G.out);
+          for (int32_t k = k0; k < k1; ++k) {
+            const int32_t pt = mem[k], u = k - k0;
+            blk[4 + u] = pt;
+            blk[4 + kLoneSub + u] = P.pt_edge_start[pt];
+            lone_grouped[pt] = 1;
+            const int32_t ep = P.pt_edge_start[pt] - e_l0;
+            for (int32_t a = 0; a < m; ++a) blk[4 + 2 * kLoneSub + m * u + a] = static_cast<int32_t>(prec[ep + a]);
+          }
+          P.lgroup.push_back(G);
+        }
+        n_grouped += n;
+      }
+    }
+    P.lone_all_grouped = n_grouped == n_lone;
+    P.arena_size = arena;
+    if (arena >= (1ull << 32)) { err = "graph too large for 32-bit arena offsets"; return DYNOHIP_ESTRUCT; }
   }
 
 
@@ -662,7 +768,8 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
       for (int t = 0; t < kNTypes; ++t) {
         const TypePlan& tp = P.types[t];
         const int nk = kNKeys[t], d = kDim[t];
-        for (int i = 0; i < tp.n; ++i)
+        for (int i = 0; i < tp.n; ++i) {
+          if (t == 0 && lone_grouped[tp.idx[i * nk + 1]]) continue;
           for (int sa = 0; sa < nk; ++sa) {
             if (kSlotKind[t][sa] != 0) continue;
             const int32_t A = tp.idx[i * nk + sa];
@@ -673,7 +780,21 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
               pair_fn(A, B, GEntry{block_off(tp, t, i, sa), block_off(tp, t, i, sb), d, 1});
             }
           }
+        }
       }
+    };
+    // the lone-point groups' partial blocks (after every factor and component)
+    auto emit_group_pairs = [&](int32_t blo, int32_t bhi, auto&& pair_fn) {
+      for (const LoneGroup& G : P.lgroup) {
+        const int32_t* ps = P.lone_pose.data() + G.pose_beg;
+        if (ps[G.m - 1] < blo || ps[0] > bhi) continue;
+        for (int a = 0; a < G.m; ++a)
+          for (int b = 0; b <= a; ++b)
+            pair_fn(ps[a], ps[b], GEntry{static_cast<uint32_t>(P.off_I6), G.out + 36u * (a * (a + 1) / 2 + b), 6, 1});
+      }
+    };
+    auto comp_grouped = [&](int c) {
+      return P.comp_start[c + 1] - P.comp_start[c] == 1 && lone_grouped[P.comp_start[c]];
     };
     auto emit_comp_pairs = [&](int c, auto&& pair_fn) {
       const int32_t nb0 = P.comp_nb_start[c], m = P.comp_nb_start[c + 1] - nb0;
@@ -695,16 +816,24 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
       for (int t = 0; t < kNTypes; ++t) {
         const TypePlan& tp = P.types[t];
         const int nk = kNKeys[t], d = kDim[t];
-        for (int i = 0; i < tp.n; ++i)
+        for (int i = 0; i < tp.n; ++i) {
+          if (t == 0 && lone_grouped[tp.idx[i * nk + 1]]) continue;
           for (int sa = 0; sa < nk; ++sa)
             if (kSlotKind[t][sa] == 0) fn(tp.idx[i * nk + sa], GEntry{block_off(tp, t, i, sa), b_off(tp, t, i), d, 1});
+        }
       }
       for (int c = 0; c < P.n_comp; ++c) {
         const int32_t nb0 = P.comp_nb_start[c], m = P.comp_nb_start[c + 1] - nb0;
-        if (m == 0 || P.nb_pose[nb0 + m - 1] < p0 || P.nb_pose[nb0] >= p1) continue;
+        if (m == 0 || P.nb_pose[nb0 + m - 1] < p0 || P.nb_pose[nb0] >= p1 || comp_grouped(c)) continue;
         for (int a = 0; a < m; ++a)
           for (int32_t q = P.nbedge_start[nb0 + a]; q < P.nbedge_start[nb0 + a + 1]; ++q)
             fn(P.nb_pose[nb0 + a], GEntry{P.nbedge_w[q], static_cast<uint32_t>(P.off_v + 3ull * (P.comp_start[c] + P.nbedge_pt[q])), 3, -1});
+      }
+      for (const LoneGroup& G : P.lgroup) {
+        const int32_t* ps = P.lone_pose.data() + G.pose_beg;
+        if (ps[G.m - 1] < p0 || ps[0] >= p1) continue;
+        const uint32_t g0 = G.out + 36u * (G.m * (G.m + 1) / 2);
+        for (int a = 0; a < G.m; ++a) fn(ps[a], GEntry{static_cast<uint32_t>(P.off_I6), g0 + 6u * a, 6, 1});
       }
     };
     // pair index: dense rows of width (max A - B) + 1 when that is small,
@@ -794,9 +923,10 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
                         emit_factor_pairs(pf);
                         for (int c = 0; c < P.n_comp; ++c) {
                           const int32_t nb0 = P.comp_nb_start[c], nb1 = P.comp_nb_start[c + 1];
-                          if (nb1 == nb0 || P.nb_pose[nb1 - 1] < blo || P.nb_pose[nb0] > bhi) continue;
+                          if (nb1 == nb0 || P.nb_pose[nb1 - 1] < blo || P.nb_pose[nb0] > bhi || comp_grouped(c)) continue;
                           emit_comp_pairs(c, pf);
                         }
+                        emit_group_pairs(blo, bhi, pf);
                       },
                       P.gRed);
     const std::vector<int64_t> gcut = even_cuts(P.n_pose);

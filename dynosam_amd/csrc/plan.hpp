@@ -53,6 +53,28 @@ struct GEntry {
   int32_t sign;
 };
 
+// Lone-point group (k_lone_schur): up to kLoneSub lone points (static
+// landmarks) sharing one sorted list of m neighbour poses, every point with
+// exactly one PoseToPoint factor per neighbour and no other factor (a group
+// of more points is split into several). Its workgroup sums the group's
+// contributions to the reduced system into arena + out: the m(m+1)/2
+// pose-pair blocks (a >= b, index a(a+1)/2 + b, 6x6 row-major, row = pose
+// a) of H_cc - W_a^T D^-1 W_b, then the m 6-vector gradients
+// J_a^T b - W_a^T D^-1 g_p. The reduced gathers read them as (identity,
+// partial) entries. On the device a group is one block of kLoneBlk ints:
+// [m, npt, out, 0, point[kLoneSub], first edge[kLoneSub],
+//  PoseToPoint record offset (J_pose at +0, b at +27)[kLoneSub][m]].
+constexpr int kLoneMaxNb = 10;
+constexpr int kLoneSub = 16;
+constexpr int kLoneBlk = 200;
+static_assert(4 + 2 * kLoneSub + kLoneSub * kLoneMaxNb <= kLoneBlk, "lone block");
+struct LoneGroup {
+  int32_t m;        // neighbour poses
+  int32_t npt;      // member points
+  int32_t pose_beg; // neighbour poses: lone_pose[pose_beg .. + m)
+  uint32_t out;     // arena offset of the partial blocks
+};
+
 // one workgroup task of the tile Cholesky (see tiles.cpp / tilechol.hip).
 // Operand pairs (A, B) index Plan::pairs; a pair stands for A B^T.
 struct TileTask {
@@ -148,6 +170,14 @@ struct Plan {
   // gathers
   GatherList gD, gE, gGp, gW, gRed, gGred;
   std::vector<int32_t> red_A, red_B;    // reduced target pose indices (A >= B)
+  // lone-point groups (k_lone_schur); their points' factor pairs and
+  // component pairs are not in gRed / gGred
+  std::vector<LoneGroup> lgroup;
+  std::vector<int32_t> lone_pose;
+  std::vector<int32_t, default_init_allocator<int32_t>> lone_blk;   // kLoneBlk per group (device form)
+  int lone_max_m = 0;
+  bool lone_all_grouped = false;        // every lone point is in a group (no lone Y is read)
+  uint64_t off_I6 = 0;                  // 6x6 identity (the A operand of the partial entries)
   // arena
   uint64_t off_D = 0, off_E = 0, off_gp = 0, off_W = 0, off_Y = 0, off_v = 0, off_L = 0, off_M = 0;
   uint64_t arena_size = 0;

@@ -126,6 +126,8 @@ struct dynohip_solver {
   DevBuf<int32_t> comp_start, comp_nb_start, nb_comp, nbedge_start, nbedge_pt, pt_edge_start, edge_pose, edge_pt;
   DevBuf<int64_t> comp_y_base;
   DevBuf<uint32_t> nbedge_w;
+  DevBuf<int32_t> lone_blk;
+  LoneSchurDev ld;
   DevBuf<double> slots, gred, xy, dpt, wdx, linv, contrib;
   DevBuf<int32_t> tile_pos, row_start, row_col, row_slot, bent, pairs;
   DevBuf<TileTask> ftask;
@@ -297,7 +299,8 @@ int upload_plan(dynohip_solver* s) {
   {
     const int32_t p0 = c.n_long < P.n_comp ? P.comp_start[c.n_long] : P.n_pt;
     c.e_lone0 = p0 < P.n_pt ? P.pt_edge_start[p0] : P.n_edge;
-    c.n_lone_edges = P.n_edge - c.e_lone0;
+    // grouped lone points' Y is formed inside k_lone_schur and never stored
+    c.n_lone_edges = P.lone_all_grouped ? 0 : P.n_edge - c.e_lone0;
     c.y_lone_base = c.n_long < P.n_comp ? static_cast<uint64_t>(P.comp_y_base[c.n_long]) : 0;
   }
   c.off_D = P.off_D;
@@ -307,6 +310,15 @@ int upload_plan(dynohip_solver* s) {
   c.off_v = P.off_v;
   c.off_L = P.off_L;
   c.off_M = P.off_M;
+  HIPCHK(s, s->lone_blk.upload(P.lone_blk, st));
+  LoneSchurDev& ld = s->ld;
+  ld.n_group = static_cast<int>(P.lgroup.size());
+  ld.blk = s->lone_blk.p;
+  ld.max_m = P.lone_max_m;
+  ld.off_W = P.off_W;
+  ld.off_L = P.off_L;
+  ld.off_gp = P.off_gp;
+  ld.off_I6 = P.off_I6;
   TileDev& b = s->bd;
   b.NT = P.NT;
   b.n_red = P.n_red;
@@ -445,6 +457,7 @@ int enqueue_try(dynohip_solver* s, double lambda) {
   z.n[2] = static_cast<int64_t>(s->fsync.n) / 2;
   launch_chain_factor(s->cd, A, lambda, s->failp, z, st);
   launch_chain_solve_y(s->cd, A, st);
+  launch_lone_schur(s->ld, A, st);
   if (timed) (void)hipEventRecord(s->ev[3], st);
   launch_gather_reduced(s->gRed.dev(P.gRed.ntargets()), s->redA.p, s->redB.p, s->gGred.dev(P.gGred.ntargets()),
                         s->gred.p, A, s->bd, lambda, st, s->nranks > 1 ? s->damp.p : nullptr);
