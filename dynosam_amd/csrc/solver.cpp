@@ -153,7 +153,13 @@ struct dynohip_solver {
   // the speculative linearisation of an accepted step); next_oldlin is its
   // linear error at delta = 0
   bool lin_valid = false;
-  double next_oldlin = 0.0;
+  // (the speculative linearisation's error at delta = 0, result[3], arrives
+  // with the next try's results)
+  // try results, copied into pinned host memory behind an event that is
+  // recorded before the speculative linearisation is enqueued: the host
+  // decides while the GPU linearises
+  double* hres = nullptr;
+  hipEvent_t ev_res = nullptr;
   int iterations = 0, inner = 0, converged = 0;
   std::vector<dynohip_trace_entry> trace;
   // values snapshot (bench hook)
@@ -587,9 +593,9 @@ int lm_iterate(dynohip_solver* s) {
   const bool speculate = !s->timing;
   double oldLin = 0.0;
   bool have_old = false;
+  int oldlin_slot = 2;   // result[] slot of the linear error at delta = 0
   if (s->lin_valid) {
-    oldLin = s->next_oldlin;
-    have_old = true;
+    oldlin_slot = 3;
   } else {
     if (s->timing) (void)hipEventRecord(s->ev[0], st);
     enqueue_linearize(s, s->pose.p, s->pt.p, s->result.p + 2);
@@ -613,12 +619,16 @@ int lm_iterate(dynohip_solver* s) {
     }
     int trc = enqueue_try(s, s->lambda);
     if (trc) return trc;
+    HIPCHK(s, hipMemcpyAsync(s->hres, s->result.p, 5 * sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPCHK(s, hipEventRecord(s->ev_res, st));
     if (speculate) {
+      // result[3] is read with the next try's results (stream order keeps
+      // this launch's value until then)
       enqueue_linearize(s, s->pose_c.p, s->pt_c.p, s->result.p + 3);
     }
+    HIPCHK(s, hipEventSynchronize(s->ev_res));
     double res[5];
-    HIPCHK(s, hipMemcpyAsync(res, s->result.p, 5 * sizeof(double), hipMemcpyDeviceToHost, st));
-    HIPCHK(s, hipStreamSynchronize(st));
+    std::memcpy(res, s->hres, sizeof(res));
     int fail = 0;
     std::memcpy(&fail, &res[4], sizeof(int));
     if (s->nranks > 1) {
@@ -631,7 +641,7 @@ int lm_iterate(dynohip_solver* s) {
       fail = (red[4] > 0 ? 1 : 0) | (red[5] > 0 ? 2 : 0) | (red[6] > 0 ? 4 : 0);
     }
     if (!have_old) {
-      oldLin = res[2];
+      oldLin = res[oldlin_slot];
       te.old_linear_error = oldLin;
       have_old = true;
       if (s->timing) {
@@ -676,10 +686,7 @@ int lm_iterate(dynohip_solver* s) {
     if (step_ok) {
       std::swap(s->pose.p, s->pose_c.p);
       std::swap(s->pt.p, s->pt_c.p);
-      if (speculate) {
-        s->lin_valid = true;
-        s->next_oldlin = res[3];
-      }
+      if (speculate) s->lin_valid = true;
       s->error = newError;
       s->lambda /= s->prm.lambda_factor;
       if (s->lambda < s->prm.lambda_lower_bound) s->lambda = s->prm.lambda_lower_bound;
@@ -755,6 +762,11 @@ int dynohip_create(int device_id, dynohip_solver** out) {
   (void)hipEventCreateWithFlags(&s->ev_main, hipEventDisableTiming);
   (void)hipEventCreateWithFlags(&s->ev_side, hipEventDisableTiming);
   for (auto& e : s->ev) (void)hipEventCreate(&e);
+  if (hipEventCreateWithFlags(&s->ev_res, hipEventDisableTiming) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&s->hres), 8 * sizeof(double), hipHostMallocDefault) != hipSuccess) {
+    dynohip_destroy(s);
+    return DYNOHIP_EHIP;
+  }
   // the dataflow factorisation keeps one 158 KB-LDS workgroup per CU
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_id) == hipSuccess && cus > 0)
@@ -771,6 +783,8 @@ void dynohip_destroy(dynohip_solver* s) {
   for (auto& e : s->ev)
     if (e) (void)hipEventDestroy(e);
   if (s->side) (void)hipStreamSynchronize(s->side);
+  if (s->ev_res) (void)hipEventDestroy(s->ev_res);
+  if (s->hres) (void)hipHostFree(s->hres);
   if (s->ev_main) (void)hipEventDestroy(s->ev_main);
   if (s->ev_side) (void)hipEventDestroy(s->ev_side);
   if (s->side) (void)hipStreamDestroy(s->side);
