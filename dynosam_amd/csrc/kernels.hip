@@ -640,12 +640,71 @@ __device__ __forceinline__ void gather_thread(const GatherDev& g, int blk, const
 // the point-side blocks of one linearisation in one launch, a thread per
 // target: D (3x3 per point), E (3x3 per chain link), g_p (3 per point) and
 // W (3x6 per point-pose edge), in block ranges of that order
+// The lone points of one group block (plan.hpp LoneGroup): a lane per
+// (point, neighbour a) reads its PoseToPoint record once (J_pose | J_point |
+// b, 30 contiguous doubles), writes W_a = J_p^T J_x, and the m lanes of a
+// point (consecutive, floor(64 / m) points per wave) sum J_p^T J_p and
+// J_p^T b into D and g_p in neighbour order (deterministic).
+static_assert(4 * (64 / kLoneMaxNb) >= kLoneSub, "a group block's points fit the workgroup's waves");
+__device__ __forceinline__ void lone_point_block(const PointGatherDev& pg, int g, const double* __restrict__ arena) {
+  const int32_t* blk = pg.lone_blk + static_cast<int64_t>(g) * kLoneBlk;
+  const int m = blk[0], npt = blk[1];
+  const int lane = threadIdx.x & 63, per = 64 / m, uu = lane / m, a = lane - uu * m;
+  const int u = (threadIdx.x >> 6) * per + uu;
+  const bool valid = uu < per && u < npt;
+  double Dp[9], gp[3];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) Dp[k] = 0.0;
+  gp[0] = gp[1] = gp[2] = 0.0;
+  if (valid) {
+    const double* R = arena + static_cast<uint32_t>(blk[4 + 2 * kLoneSub + m * u + a]);
+    double Jx[18], Jp[9], bb[3];
+#pragma unroll
+    for (int k = 0; k < 18; ++k) Jx[k] = R[k];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) Jp[k] = R[18 + k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) bb[k] = R[27 + k];
+    double* W = pg.dst[3] + 18ll * (blk[4 + kLoneSub + u] + a);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+#pragma unroll
+      for (int c = 0; c < 6; ++c) W[6 * k + c] = Jp[k] * Jx[c] + Jp[3 + k] * Jx[6 + c] + Jp[6 + k] * Jx[12 + c];
+#pragma unroll
+      for (int l = 0; l < 3; ++l) Dp[3 * k + l] = Jp[k] * Jp[l] + Jp[3 + k] * Jp[3 + l] + Jp[6 + k] * Jp[6 + l];
+      gp[k] = Jp[k] * bb[0] + Jp[3 + k] * bb[1] + Jp[6 + k] * bb[2];
+    }
+  }
+  // lane a == 0 of each point sums its m lanes (all lanes take part in the shuffles)
+  double Ds[9], gs[3];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) Ds[k] = 0.0;
+  gs[0] = gs[1] = gs[2] = 0.0;
+  for (int j = 0; j < m; ++j) {
+    const int src = min(lane + j, 63);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) Ds[k] += __shfl(Dp[k], src);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) gs[k] += __shfl(gp[k], src);
+  }
+  if (valid && a == 0) {
+    const int pt = blk[4 + u];
+    double* D = pg.dst[0] + 9ll * pt;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) D[k] = Ds[k];
+    double* G = pg.dst[2] + 3ll * pt;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) G[k] = gs[k];
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_gather_point(PointGatherDev p, const double* __restrict__ arena) {
   const int b = blockIdx.x;
   if (b < p.bstart[1]) gather_thread<3, 3>(p.g[0], b, arena, p.dst[0]);
   else if (b < p.bstart[2]) gather_thread<3, 3>(p.g[1], b - p.bstart[1], arena, p.dst[1]);
   else if (b < p.bstart[3]) gather_thread<3, 1>(p.g[2], b - p.bstart[2], arena, p.dst[2]);
-  else gather_thread<3, 6>(p.g[3], b - p.bstart[3], arena, p.dst[3]);
+  else if (b < p.bstart[4]) gather_thread<3, 6>(p.g[3], b - p.bstart[3], arena, p.dst[3]);
+  else lone_point_block(p, b - p.bstart[4], arena);
 }
 
 // a wave per 6x6 target
@@ -1552,7 +1611,8 @@ void launch_linerr(const TypeDev* td, const double* arena, const double* dpose, 
   if (gp.last < 0) launch_empty_sum(partials, out, nullptr, nullptr, s);
 }
 
-void launch_gather_point(const GatherDev (&g)[4], double* const (&dst)[4], const double* arena, hipStream_t s) {
+void launch_gather_point(const GatherDev (&g)[4], double* const (&dst)[4], const double* arena, hipStream_t s,
+                         int n_lone, const int32_t* lone_blk) {
   PointGatherDev p;
   p.bstart[0] = 0;
   for (int k = 0; k < 4; ++k) {
@@ -1560,8 +1620,11 @@ void launch_gather_point(const GatherDev (&g)[4], double* const (&dst)[4], const
     p.dst[k] = dst[k];
     p.bstart[k + 1] = p.bstart[k] + nblocks(g[k].n);
   }
-  if (p.bstart[4] == 0) return;
-  k_gather_point<<<p.bstart[4], kBlock, 0, s>>>(p, arena);
+  p.n_lone = n_lone;
+  p.lone_blk = lone_blk;
+  const int nb = p.bstart[4] + n_lone;
+  if (nb == 0) return;
+  k_gather_point<<<nb, kBlock, 0, s>>>(p, arena);
 }
 
 void launch_gather_reduced(const GatherDev& band, const int32_t* tA, const int32_t* tB, const GatherDev& grad,

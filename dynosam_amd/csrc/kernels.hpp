@@ -31,6 +31,10 @@ struct PointGatherDev {
   GatherDev g[4];
   double* dst[4] = {};
   int bstart[5] = {};
+  // lone-point groups (plan.hpp LoneGroup): a workgroup per group block
+  // forms D, g_p and W of its points from their PoseToPoint records
+  int n_lone = 0;
+  const int32_t* lone_blk = nullptr;
 };
 
 struct ReducedGatherDev {
@@ -124,7 +128,8 @@ void launch_linerr(const TypeDev* td, const double* arena, const double* dpose, 
                    unsigned* counter, double* out, hipStream_t s);
 
 // point-side gathers (thread per target), dst = arena + off
-void launch_gather_point(const GatherDev (&g)[4], double* const (&dst)[4], const double* arena, hipStream_t s);
+void launch_gather_point(const GatherDev (&g)[4], double* const (&dst)[4], const double* arena, hipStream_t s,
+                         int n_lone = 0, const int32_t* lone_blk = nullptr);
 // reduced blocks into their tiles (+ lambda), reduced gradient, identity padding
 void launch_gather_reduced(const GatherDev& band, const int32_t* tA, const int32_t* tB, const GatherDev& grad,
                            double* gred, const double* arena, const TileDev& b, double lambda, hipStream_t s,

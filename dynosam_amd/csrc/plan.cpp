@@ -632,22 +632,6 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
           }
         }
     };
-    for (int which = 0; which < 4; ++which) {
-      GatherList& out = which == 0 ? P.gD : which == 1 ? P.gE : which == 2 ? P.gGp : P.gW;
-      const int64_t nt = which == 3 ? P.n_edge : P.n_pt;
-      const std::vector<int64_t> cut = even_cuts(nt);
-      csr_target_ranges(nt, cut,
-                        [&](int r, auto&& fn) {
-                          if (cut[r + 1] <= cut[r]) return;
-                          if (which != 3) {
-                            emit_point(which, static_cast<int32_t>(cut[r]), static_cast<int32_t>(cut[r + 1]), fn);
-                          } else {
-                            emit_point(which, P.edge_pt[cut[r]], P.edge_pt[cut[r + 1] - 1] + 1, fn);
-                          }
-                        },
-                        out);
-    }
-
     // ---- lone-point groups (plan.hpp LoneGroup) ----
     // Eligible: a lone point with 1..kLoneMaxNb neighbour poses and exactly
     // one PoseToPoint factor per neighbour (every static landmark of the
@@ -752,6 +736,28 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
     P.lone_all_grouped = n_grouped == n_lone;
     P.arena_size = arena;
     if (arena >= (1ull << 32)) { err = "graph too large for 32-bit arena offsets"; return DYNOHIP_ESTRUCT; }
+    // with every lone point grouped, their D, g_p and W come from the
+    // group blocks (k_gather_point's lone blocks): the CSR gathers stop at
+    // the first lone point / edge (E stays whole: lone points have none)
+    plan_mark("lone-point groups", tmark);
+    const int32_t pt_end = P.lone_all_grouped ? p_lone : P.n_pt;
+    const int32_t edge_end = P.lone_all_grouped ? e_l0 : P.n_edge;
+    for (int which = 0; which < 4; ++which) {
+      GatherList& out = which == 0 ? P.gD : which == 1 ? P.gE : which == 2 ? P.gGp : P.gW;
+      const int64_t nt = which == 3 ? edge_end : which == 1 ? P.n_pt : pt_end;
+      const std::vector<int64_t> cut = even_cuts(nt);
+      csr_target_ranges(nt, cut,
+                        [&](int r, auto&& fn) {
+                          if (cut[r + 1] <= cut[r]) return;
+                          if (which != 3) {
+                            emit_point(which, static_cast<int32_t>(cut[r]), static_cast<int32_t>(cut[r + 1]), fn);
+                          } else {
+                            emit_point(which, P.edge_pt[cut[r]], P.edge_pt[cut[r + 1] - 1] + 1, fn);
+                          }
+                        },
+                        out);
+    }
+
   }
 
 

@@ -442,7 +442,8 @@ void enqueue_linearize(dynohip_solver* s, const double* pose, const double* pt, 
   const GatherDev g[4] = {s->gD.dev(P.gD.ntargets()), s->gE.dev(P.gE.ntargets()), s->gGp.dev(P.gGp.ntargets()),
                           s->gW.dev(P.gW.ntargets())};
   double* const dst[4] = {A + P.off_D, A + P.off_E, A + P.off_gp, A + P.off_W};
-  launch_gather_point(g, dst, A, s->stream);
+  launch_gather_point(g, dst, A, s->stream, P.lone_all_grouped ? static_cast<int>(P.lgroup.size()) : 0,
+                      s->lone_blk.p);
 }
 
 // damped solve + linearised error + retract + error for one lambda.
