@@ -1463,12 +1463,61 @@ __device__ void backsub_group(const ChainDev& cd, const double* __restrict__ are
   }
 }
 
+// dp = D^-1 (g_p - sum_a W_a dX_a) for the lone points of one group block
+// (plan.hpp LoneGroup): a lane per (point, neighbour a) forms W_a dX_a from
+// its edge, the m lanes of a point are summed by shuffles in neighbour order
+// (the same lane layout as lone_point_block), then the point's lane solves.
+__device__ void backsub_lone_block(const ChainDev& cd, const int32_t* __restrict__ lone_blk, int g,
+                                   const double* __restrict__ arena, const double* __restrict__ dpose,
+                                   double* __restrict__ dpt) {
+  const int32_t* blk = lone_blk + static_cast<int64_t>(g) * kLoneBlk;
+  const int m = blk[0], npt = blk[1];
+  const int lane = threadIdx.x & 63, per = 64 / m, uu = lane / m, a = lane - uu * m;
+  const int u = (threadIdx.x >> 6) * per + uu;
+  const bool valid = uu < per && u < npt;
+  double t[3] = {0.0, 0.0, 0.0};
+  if (valid) {
+    const int e = blk[4 + kLoneSub + u] + a;
+    double W[18], dx[6];
+    ldk(arena + cd.off_W + 18ll * e, W);
+    ldk(dpose + 6ll * cd.edge_pose[e], dx);
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int k = 0; k < 6; ++k) t[r] += W[6 * r + k] * dx[k];
+  }
+  double s[3] = {0.0, 0.0, 0.0};
+  for (int j = 0; j < m; ++j) {
+    const int src = min(lane + j, 63);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) s[r] += __shfl(t[r], src);
+  }
+  if (valid && a == 0) {
+    const int pt = blk[4 + u];
+    const double* gp = arena + cd.off_gp + 3ll * pt;
+    double x[3] = {gp[0] - s[0], gp[1] - s[1], gp[2] - s[2]}, L[9];
+    ldk(arena + cd.off_L + 9ll * pt, L);
+    lsolve<1>(L, x);
+    ltsolve<1>(L, x);
+    dpt[3ll * pt] = x[0]; dpt[3ll * pt + 1] = x[1]; dpt[3ll * pt + 2] = x[2];
+  }
+}
+
+// Blocks: [0, nbg) 16-lane groups over the long chains, [nbg, nbg + nbs) a
+// thread per lone point (when they are not grouped), then the lone-point
+// group blocks (when they are)
 __global__ __launch_bounds__(kBlock) void k_backsub(ChainDev cd, const double* __restrict__ arena,
-                                                    const double* __restrict__ t, double* __restrict__ dpt, int nbg) {
+                                                    const double* __restrict__ t, double* __restrict__ dpt, int nbg,
+                                                    int nbs, const double* __restrict__ dpose,
+                                                    const int32_t* __restrict__ lone_blk) {
   const int blk = blockIdx.x;
   if (blk < nbg) {
     const int c = (blk * kBlock + static_cast<int>(threadIdx.x)) / kGrp;
     if (c < cd.n_long) backsub_group(cd, arena, t, dpt, c, threadIdx.x % kGrp);
+    return;
+  }
+  if (blk >= nbg + nbs) {
+    backsub_lone_block(cd, lone_blk, blk - nbg - nbs, arena, dpose, dpt);
     return;
   }
   const int c = cd.n_long + (blk - nbg) * kBlock + static_cast<int>(threadIdx.x);
@@ -1696,11 +1745,14 @@ void launch_lone_schur(const LoneSchurDev& d, double* arena, hipStream_t s) {
 }
 
 void launch_backsub(const ChainDev& c, int n_edge, const double* arena, const double* dpose, double* wdx, double* dpt,
-                    hipStream_t s) {
+                    hipStream_t s, int n_lone, const int32_t* lone_blk) {
   if (c.n_comp == 0) return;
-  if (n_edge > 0) k_wdx<<<nblocks(n_edge), kBlock, 0, s>>>(c, n_edge, arena, dpose, wdx);
+  // grouped lone points form their W dX themselves: k_wdx stops at their first edge
+  const int n_wdx = n_lone > 0 ? c.e_lone0 : n_edge;
+  if (n_wdx > 0) k_wdx<<<nblocks(n_wdx), kBlock, 0, s>>>(c, n_wdx, arena, dpose, wdx);
   const int nbg = nblocks(static_cast<int64_t>(c.n_long) * kGrp);
-  k_backsub<<<nbg + nblocks(c.n_comp - c.n_long), kBlock, 0, s>>>(c, arena, wdx, dpt, nbg);
+  const int nbs = n_lone > 0 ? 0 : nblocks(c.n_comp - c.n_long);
+  k_backsub<<<nbg + nbs + n_lone, kBlock, 0, s>>>(c, arena, wdx, dpt, nbg, nbs, dpose, lone_blk);
 }
 
 void launch_retract(int n_pose, int n_pt, const double* pose, const double* pt, const double* dpose,

@@ -148,7 +148,7 @@ void launch_lone_schur(const LoneSchurDev& d, double* arena, hipStream_t s);
 int debug_lone_clock(void* out);   // -DDYNOHIP_LONE_CLOCK builds: the stamps of the last launch
 // dpt = C^-1 (gp - W dpose); wdx: scratch of 3 doubles per point-pose edge
 void launch_backsub(const ChainDev& c, int n_edge, const double* arena, const double* dpose, double* wdx, double* dpt,
-                    hipStream_t s);
+                    hipStream_t s, int n_lone = 0, const int32_t* lone_blk = nullptr);
 
 // factor the tiles and solve (L L^T) x = r (forward substitution fused
 // into the factorisation: contrib holds L(i,k) y_k per stored tile). Linv

@@ -500,7 +500,8 @@ int enqueue_try(dynohip_solver* s, double lambda) {
   if (timed && s->nranks > 1) (void)hipEventRecord(s->ev[5], st);
   if (timed) (void)hipEventRecord(s->ev[6], st);
   // pose deltas are x[0 .. 6 n_pose) in pose-index order
-  launch_backsub(s->cd, P.n_edge, A, x, s->wdx.p, s->dpt.p, st);
+  launch_backsub(s->cd, P.n_edge, A, x, s->wdx.p, s->dpt.p, st,
+                 P.lone_all_grouped ? static_cast<int>(P.lgroup.size()) : 0, s->lone_blk.p);
   enqueue_linerr(s, x, s->dpt.p, s->partials.p, s->result.p);
   if (timed) (void)hipEventRecord(s->ev[7], st);
   launch_retract(P.n_pose, P.n_pt, s->pose.p, s->pt.p, x, s->dpt.p, s->pose_c.p, s->pt_c.p, st);

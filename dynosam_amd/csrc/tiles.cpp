@@ -25,6 +25,7 @@
 // level. The leaf size is picked by a small cost model of the launch
 // sequence.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <cstdint>
@@ -475,6 +476,7 @@ bool build_tile_schedule(Plan& P) {
     return n;
   };
   P.back_part_tiles = 2;
+  if (const char* e = std::getenv("DYNOHIP_BACK_PART_TILES")) P.back_part_tiles = std::max(1, std::atoi(e));   // sweep knob
   while (count_parts(P.back_part_tiles) > kBackPersistMax && P.back_part_tiles < 64) P.back_part_tiles *= 2;
   if (count_parts(P.back_part_tiles) > kBackPersistMax) P.back_part_tiles = 2;  // level launches
   const int32_t tpp = P.back_part_tiles;
