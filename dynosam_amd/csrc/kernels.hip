@@ -394,9 +394,11 @@ __device__ __forceinline__ double linerr_one(const TypeDev& tp, int i, const dou
 // ---- type groups ------------------------------------------------------------
 // One launch covers every factor type of a group (a bit mask over types):
 // block b belongs to the type whose [bstart[T], bstart[T+1]) holds it, so a
-// block is uniform in type and the per-type block numbering, and with it the
-// partial-sum layout, is the same as one launch per type. Types outside the
-// mask span no blocks.
+// block is uniform in type. Types outside the mask span no blocks. The
+// kernels map workgroup x to block nblocks - 1 - x: the few, long-running
+// blocks of the pose-pose and ternary types (last in type order) are
+// dispatched first and the many short PoseToPoint blocks fill in behind them.
+// A workgroup's partial keeps slot pbase + x (the sum's order is fixed).
 struct GroupDev {
   TypeDev t[kNTypes];
   int bstart[kNTypes + 1];
@@ -481,7 +483,7 @@ template <unsigned M>
 __global__ __launch_bounds__(kBlock) void k_linearize(GroupDev g, const double* __restrict__ pose,
                                                       const double* __restrict__ pt, double* __restrict__ arena,
                                                       SumDev sd) {
-  const double e = group_apply<M>(g, blockIdx.x, [&](auto tc, int i) {
+  const double e = group_apply<M>(g, gridDim.x - 1 - blockIdx.x, [&](auto tc, int i) {
     return linearize_one<decltype(tc)::value>(g.t[decltype(tc)::value], i, pose, pt, arena);
   });
   group_finish(e, g, sd);
@@ -490,7 +492,7 @@ __global__ __launch_bounds__(kBlock) void k_linearize(GroupDev g, const double* 
 template <unsigned M>
 __global__ __launch_bounds__(kBlock) void k_error(GroupDev g, const double* __restrict__ pose,
                                                   const double* __restrict__ pt, SumDev sd) {
-  const double e = group_apply<M>(g, blockIdx.x, [&](auto tc, int i) {
+  const double e = group_apply<M>(g, gridDim.x - 1 - blockIdx.x, [&](auto tc, int i) {
     return error_one<decltype(tc)::value>(g.t[decltype(tc)::value], i, pose, pt);
   });
   group_finish(e, g, sd);
@@ -500,7 +502,7 @@ template <unsigned M>
 __global__ __launch_bounds__(kBlock) void k_linerr(GroupDev g, const double* __restrict__ arena,
                                                    const double* __restrict__ dpose, const double* __restrict__ dpt,
                                                    SumDev sd) {
-  const double e = group_apply<M>(g, blockIdx.x, [&](auto tc, int i) {
+  const double e = group_apply<M>(g, gridDim.x - 1 - blockIdx.x, [&](auto tc, int i) {
     return linerr_one<decltype(tc)::value>(g.t[decltype(tc)::value], i, arena, dpose, dpt);
   });
   group_finish(e, g, sd);
@@ -1550,15 +1552,14 @@ __global__ __launch_bounds__(kBlock) void k_retract(int n_pose, int n_pt, const 
 // Launch groups: PoseToPoint alone (it dominates the factor count and keeps
 // its own occupancy), the low-count Ternary/Between/Prior together, and the
 // two LLWorld types alone (their register counts would cap the others).
-constexpr unsigned kGroups[] = {1u << 0, (1u << 1) | (1u << 2) | (1u << 3), 1u << 4, 1u << 5};
+constexpr unsigned kGroups[] = {0xFu, 1u << 4, 1u << 5};
 constexpr int kNGroups = sizeof(kGroups) / sizeof(kGroups[0]);
 
 #define DH_GROUP_DISPATCH(g, KERNEL, grid, ...)                                   \
   switch (g) {                                                                     \
     case 0: KERNEL<kGroups[0]><<<grid, kBlock, 0, s>>>(__VA_ARGS__); break;        \
     case 1: KERNEL<kGroups[1]><<<grid, kBlock, 0, s>>>(__VA_ARGS__); break;        \
-    case 2: KERNEL<kGroups[2]><<<grid, kBlock, 0, s>>>(__VA_ARGS__); break;        \
-    default: KERNEL<kGroups[3]><<<grid, kBlock, 0, s>>>(__VA_ARGS__); break;       \
+    default: KERNEL<kGroups[2]><<<grid, kBlock, 0, s>>>(__VA_ARGS__); break;       \
   }
 
 namespace {
@@ -1597,7 +1598,7 @@ GroupPlan plan_groups(const TypeDev* td) {
 }
 
 // the types of a group must be contiguous in type order for pbase to hold
-static_assert(kGroups[1] == 0xEu, "group 1 must cover types 1..3 contiguously");
+static_assert(kGroups[0] == 0xFu, "group 0 must cover types 0..3 contiguously");
 
 SumDev sum_for(const GroupPlan& gp, int g, double* partials, unsigned* counter, double* out) {
   SumDev sd;
