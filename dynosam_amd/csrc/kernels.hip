@@ -1176,12 +1176,92 @@ __device__ __forceinline__ void lone_solve_y(const ChainDev& cd, double* __restr
   for (int r = 0; r < 3; ++r) Y[6 * r + col] = x[r];
 }
 
+// The same column solve with the chain's L and M staged in LDS by the
+// workgroup (one round trip for all its chains instead of one dependent load
+// per step), the pair's W column loaded up front (at most kYEdges edges), and
+// the forward results kept in registers for the backward sweep (chains of at
+// most kYMaxN points). The operations and their order are chain_solve_y_col's.
+constexpr int kYStage = 128;   // staged points per workgroup, at most
+constexpr int kYMaxN = 10;
+constexpr int kYEdges = 4;
+__device__ __forceinline__ void chain_solve_y_lds(const ChainDev& cd, double* __restrict__ arena,
+                                                  const double* __restrict__ sLM, int p0, int q, int col,
+                                                  const int (&ept)[kYEdges], const double (&ew)[kYEdges][3]) {
+  const int c = cd.nb_comp[q];
+  const int nb0 = cd.comp_nb_start[c];
+  const int m = cd.comp_nb_start[c + 1] - nb0;
+  const int b = q - nb0;
+  const int i0 = cd.comp_start[c], n = cd.comp_start[c + 1] - i0;
+  double* Y = arena + cd.comp_y_base[c] + 18ll * b + col;
+  const double* LM = sLM + 18 * (i0 - p0);
+  double Zh[kYMaxN][3];
+#pragma unroll
+  for (int i = 0; i < kYMaxN; ++i) {
+    if (i < n) {
+      double rhs[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+      for (int k = 0; k < kYEdges; ++k)
+        if (ept[k] == i) { rhs[0] = ew[k][0]; rhs[1] = ew[k][1]; rhs[2] = ew[k][2]; }
+      if (i > 0) sub_mx<1>(LM + 18 * i + 9, Zh[i > 0 ? i - 1 : 0], rhs);
+      lsolve<1>(LM + 18 * i, rhs);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) Zh[i][k] = rhs[k];
+    }
+  }
+  double Yn[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+  for (int i = kYMaxN - 1; i >= 0; --i) {
+    if (i < n) {
+      double x[3] = {Zh[i][0], Zh[i][1], Zh[i][2]};
+      if (i < n - 1) sub_mtx<1>(LM + 18 * (i + 1) + 9, Yn, x);
+      ltsolve<1>(LM + 18 * i, x);
+      double* yo = Y + 18ll * static_cast<int64_t>(i) * m;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) { yo[6 * k] = x[k]; Yn[k] = x[k]; }
+    }
+  }
+}
+
 // Blocks [0, nbl): a lane per (pair, column) of the long chains' (chain,
 // neighbour pose) pairs; then a lane per (edge, column) of the lone points.
 __global__ __launch_bounds__(kBlock) void k_chain_solve_y(ChainDev cd, double* __restrict__ arena, int nbl) {
   if (static_cast<int>(blockIdx.x) < nbl) {
+    __shared__ double sLM[kYStage * 18];
     const int g = blockIdx.x * kBlock + static_cast<int>(threadIdx.x);
-    if (g < 6 * cd.n_nb_long) chain_solve_y_col(cd, arena, g / 6, g % 6);
+    const int npair = cd.n_nb_long;
+    const int qa = blockIdx.x * kBlock / 6, qb = min((blockIdx.x * kBlock + kBlock - 1) / 6, npair - 1);
+    const int p0 = cd.comp_start[cd.nb_comp[qa]], p1 = cd.comp_start[cd.nb_comp[qb] + 1];
+    const bool staged = p1 - p0 <= kYStage;
+    if (staged)
+      for (int k = threadIdx.x; k < 18 * (p1 - p0); k += kBlock) {
+        const int i = k / 18, e = k - 18 * i;
+        sLM[k] = e < 9 ? arena[cd.off_L + 9ll * (p0 + i) + e] : arena[cd.off_M + 9ll * (p0 + i) + e - 9];
+      }
+    // the lane's pair: its edges' W column, up front
+    const int q = g / 6, col = g - 6 * q;
+    int ept[kYEdges];
+    double ew[kYEdges][3];
+    bool fast = false;
+    if (g < 6 * npair) {
+      const int ep = cd.nbedge_start[q], ne = cd.nbedge_start[q + 1] - ep;
+      const int c = cd.nb_comp[q];
+      fast = staged && ne <= kYEdges && cd.comp_start[c + 1] - cd.comp_start[c] <= kYMaxN;
+#pragma unroll
+      for (int k = 0; k < kYEdges; ++k) {
+        ept[k] = -1;
+        ew[k][0] = ew[k][1] = ew[k][2] = 0.0;
+        if (fast && k < ne) {
+          ept[k] = cd.nbedge_pt[ep + k];
+          const double* W = arena + cd.nbedge_w[ep + k] + col;
+          ew[k][0] = W[0]; ew[k][1] = W[6]; ew[k][2] = W[12];
+        }
+      }
+    }
+    __syncthreads();
+    if (g < 6 * npair) {
+      if (fast) chain_solve_y_lds(cd, arena, sLM, p0, q, col, ept, ew);
+      else chain_solve_y_col(cd, arena, q, col);
+    }
     return;
   }
   const int64_t g = static_cast<int64_t>(blockIdx.x - nbl) * kBlock + threadIdx.x;
