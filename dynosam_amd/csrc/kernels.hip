@@ -711,7 +711,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_point(PointGatherDev p, const
 
 // a wave per 6x6 target
 __device__ __forceinline__ void gather_band(const GatherDev& g, const int32_t* __restrict__ tA,
-                                            const int32_t* __restrict__ tB, int blk,
+                                            const int32_t* __restrict__ tB, const uint32_t* __restrict__ tslot, int blk,
                                             const double* __restrict__ arena, const TileDev& b, double lambda,
                                             const uint8_t* __restrict__ damp) {
   const int t = (blk * kBlock + static_cast<int>(threadIdx.x)) >> 6;
@@ -732,7 +732,10 @@ __device__ __forceinline__ void gather_band(const GatherDev& g, const int32_t* _
   if (A == B && r < c) return;
   const int row = 6 * A + r, col = 6 * B + c;
   const double val = a1[0] + (A == B && r == c && (!damp || damp[row]) ? lambda : 0.0);
-  const int64_t at = tile_index(b, row, col);
+  // the tile from the target's precomputed slots (no lookup chain)
+  const uint32_t e = tslot[4 * t + 2 * ((row >> 6) != ((6 * A) >> 6)) + ((col >> 6) != ((6 * B) >> 6))];
+  const int64_t at = static_cast<int64_t>(e & 0x7fffffffu) * kTile * kTile +
+                     ((e >> 31) ? (col % kTile) * kTile + row % kTile : (row % kTile) * kTile + col % kTile);
   b.slots[at] = val;
   // diagonal tiles are stored full (symmetric), so the factorisation reads
   // them with plain coalesced loads
@@ -771,7 +774,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_reduced(ReducedGatherDev r, c
                                                            TileDev b, double lambda) {
   const int hb = blockIdx.x;
   if (hb < r.nb_band) {
-    gather_band(r.band, r.tA, r.tB, xcd_block(hb, r.nb_band), arena, b, lambda, r.damp);
+    gather_band(r.band, r.tA, r.tB, r.tslot, xcd_block(hb, r.nb_band), arena, b, lambda, r.damp);
   } else if (hb < r.nb_band + r.nb_grad) {
     gather_grad(r.grad, xcd_block(hb - r.nb_band, r.nb_grad), arena, r.gred);
   } else {
@@ -1757,7 +1760,8 @@ void launch_gather_point(const GatherDev (&g)[4], double* const (&dst)[4], const
   k_gather_point<<<nb, kBlock, 0, s>>>(p, arena);
 }
 
-void launch_gather_reduced(const GatherDev& band, const int32_t* tA, const int32_t* tB, const GatherDev& grad,
+void launch_gather_reduced(const GatherDev& band, const int32_t* tA, const int32_t* tB, const uint32_t* tslot,
+                           const GatherDev& grad,
                            double* gred, const double* arena, const TileDev& b, double lambda, hipStream_t s,
                            const uint8_t* damp) {
   ReducedGatherDev r;
@@ -1765,6 +1769,7 @@ void launch_gather_reduced(const GatherDev& band, const int32_t* tA, const int32
   r.band = band;
   r.tA = tA;
   r.tB = tB;
+  r.tslot = tslot;
   r.grad = grad;
   r.gred = gred;
   r.nb_band = (nblocks(static_cast<int64_t>(band.n) * 64) + 7) / 8 * 8;

@@ -41,6 +41,7 @@ struct ReducedGatherDev {
   GatherDev band;              // 6x6 reduced blocks (targets tA[t], tB[t])
   const int32_t* tA = nullptr;
   const int32_t* tB = nullptr;
+  const uint32_t* tslot = nullptr;   // Plan::red_slot
   GatherDev grad;              // 6-vector reduced gradient per pose
   double* gred = nullptr;
   int nb_band = 0, nb_grad = 0;
@@ -131,7 +132,8 @@ void launch_linerr(const TypeDev* td, const double* arena, const double* dpose, 
 void launch_gather_point(const GatherDev (&g)[4], double* const (&dst)[4], const double* arena, hipStream_t s,
                          int n_lone = 0, const int32_t* lone_blk = nullptr);
 // reduced blocks into their tiles (+ lambda), reduced gradient, identity padding
-void launch_gather_reduced(const GatherDev& band, const int32_t* tA, const int32_t* tB, const GatherDev& grad,
+void launch_gather_reduced(const GatherDev& band, const int32_t* tA, const int32_t* tB, const uint32_t* tslot,
+                           const GatherDev& grad,
                            double* gred, const double* arena, const TileDev& b, double lambda, hipStream_t s,
                            const uint8_t* damp = nullptr);
 // partitioned: r[rows of separator tile] -= sum of this rank's contributions

@@ -181,6 +181,7 @@ int build_partitioned_plan(const dynohip_graph_view& g, const uint64_t* keys, co
   L.sep_tile_ranges = std::move(G.sep_tile_ranges);
   L.band_D = std::move(G.band_D);
   L.max_D = G.max_D;
+  compute_red_slots(L);
   // damping: interior rows by their owner, separator rows by rank 0 (the
   // ranks' diagonals are summed in the exchange)
   part.damp_row.assign(static_cast<size_t>(L.n_red), 0);

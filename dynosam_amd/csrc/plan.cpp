@@ -238,6 +238,30 @@ static void plan_mark(const char* what, double& t) {
   t = n;
 }
 
+void compute_red_slots(Plan& P) {
+  const int64_t nt = static_cast<int64_t>(P.red_A.size());
+  P.red_slot.resize(4 * static_cast<size_t>(nt));
+  auto lookup = [&](int i, int j) -> uint32_t {   // stored tile of natural tiles (i, j), as tile_index
+    uint32_t tr = 0;
+    if (P.tile_pos[i] < P.tile_pos[j]) { std::swap(i, j); tr = 1u << 31; }
+    const auto b = P.row_col.begin() + P.row_start[i], e = P.row_col.begin() + P.row_start[i + 1];
+    const auto it = std::lower_bound(b, e, j);
+    if (it == e || *it != j) return ~0u;
+    return static_cast<uint32_t>(P.row_slot[it - P.row_col.begin()]) | tr;
+  };
+  parallel_for(nt, [&](int64_t t0, int64_t t1) {
+    for (int64_t t = t0; t < t1; ++t) {
+      const int r0 = 6 * P.red_A[t] / kTile, r1 = (6 * P.red_A[t] + 5) / kTile;
+      const int c0 = 6 * P.red_B[t] / kTile, c1 = (6 * P.red_B[t] + 5) / kTile;
+      uint32_t* o = P.red_slot.data() + 4 * t;
+      o[0] = lookup(r0, c0);
+      o[1] = c1 != c0 ? lookup(r0, c1) : ~0u;
+      o[2] = r1 != r0 ? lookup(r1, c0) : ~0u;
+      o[3] = (r1 != r0 && c1 != c0) ? lookup(r1, c1) : ~0u;
+    }
+  });
+}
+
 int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t* kind, size_t n, Plan& P,
                std::string& err, int nranks, int rank, bool with_schedule) {
   double tmark = plan_now();
@@ -963,6 +987,8 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
     return DYNOHIP_ESTRUCT;
   }
   plan_mark("tile schedule", tmark);
+  if (with_schedule) compute_red_slots(P);
+  plan_mark("reduced target slots", tmark);
   return DYNOHIP_OK;
 }
 

@@ -170,6 +170,10 @@ struct Plan {
   // gathers
   GatherList gD, gE, gGp, gW, gRed, gGred;
   std::vector<int32_t> red_A, red_B;    // reduced target pose indices (A >= B)
+  // per target, the slots of the (up to) 2 x 2 tiles its 6x6 block touches:
+  // [row tile of 6A / of 6A+5][col tile of 6B / of 6B+5], bit 31 = the tile is
+  // stored transposed (its column tile is eliminated later); ~0u: not stored
+  std::vector<uint32_t> red_slot;
   // lone-point groups (k_lone_schur); their points' factor pairs and
   // component pairs are not in gRed / gGred
   std::vector<LoneGroup> lgroup;
@@ -228,6 +232,9 @@ struct Plan {
 // P.nranks > 1 the top of the dissection is split into rank subtrees; false
 // when the graph is too short for that many.
 bool build_tile_schedule(Plan& P);
+
+// Plan::red_slot from the tile structure (after the tile schedule).
+void compute_red_slots(Plan& P);
 
 // returns DYNOHIP_OK or an error code with `err` filled. nranks > 1 builds
 // the partitioned tile schedule of `rank` (the graph is the global one);

@@ -123,6 +123,7 @@ struct dynohip_solver {
   TypeDev td[kNTypes];
   GatherBufs gD, gE, gGp, gW, gRed, gGred;
   DevBuf<int32_t> redA, redB;
+  DevBuf<uint32_t> redslot;
   DevBuf<int32_t> comp_start, comp_nb_start, nb_comp, nbedge_start, nbedge_pt, pt_edge_start, edge_pose, edge_pt;
   DevBuf<int64_t> comp_y_base;
   DevBuf<uint32_t> nbedge_w;
@@ -248,6 +249,7 @@ int upload_plan(dynohip_solver* s) {
     return DYNOHIP_EHIP;
   HIPCHK(s, s->redA.upload(P.red_A, st));
   HIPCHK(s, s->redB.upload(P.red_B, st));
+  HIPCHK(s, s->redslot.upload(P.red_slot, st));
   HIPCHK(s, s->comp_start.upload(P.comp_start, st));
   HIPCHK(s, s->comp_nb_start.upload(P.comp_nb_start, st));
   HIPCHK(s, s->nb_comp.upload(P.nb_comp, st));
@@ -466,7 +468,8 @@ int enqueue_try(dynohip_solver* s, double lambda) {
   launch_chain_solve_y(s->cd, A, st);
   launch_lone_schur(s->ld, A, st);
   if (timed) (void)hipEventRecord(s->ev[3], st);
-  launch_gather_reduced(s->gRed.dev(P.gRed.ntargets()), s->redA.p, s->redB.p, s->gGred.dev(P.gGred.ntargets()),
+  launch_gather_reduced(s->gRed.dev(P.gRed.ntargets()), s->redA.p, s->redB.p, s->redslot.p,
+                        s->gGred.dev(P.gGred.ntargets()),
                         s->gred.p, A, s->bd, lambda, st, s->nranks > 1 ? s->damp.p : nullptr);
   if (timed) (void)hipEventRecord(s->ev[4], st);
   double* y = s->xy.p;
