@@ -489,22 +489,29 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
       std::vector<int32_t> cur(cnt.begin(), cnt.end() - 1);
       each([&](int32_t pt, int32_t pose) { poses[cur[pt]++] = pose; });
     }
+    // per point (in parallel): sort + unique its poses in place, then the
+    // prefix of the unique counts places every point's edges
     P.pt_edge_start.assign(P.n_pt + 1, 0);
-    P.edge_pt.clear();
-    P.edge_pose.clear();
-    P.edge_pt.reserve(poses.size());
-    P.edge_pose.reserve(poses.size());
-    for (int pt = 0; pt < P.n_pt; ++pt) {
-      auto b = poses.begin() + cnt[pt], e = poses.begin() + cnt[pt + 1];
-      std::sort(b, e);
-      e = std::unique(b, e);
-      for (auto it = b; it != e; ++it) {
-        P.edge_pt.push_back(pt);
-        P.edge_pose.push_back(*it);
+    parallel_for(P.n_pt, [&](int64_t p0, int64_t p1) {
+      for (int64_t pt = p0; pt < p1; ++pt) {
+        auto b = poses.begin() + cnt[pt], e = poses.begin() + cnt[pt + 1];
+        std::sort(b, e);
+        P.pt_edge_start[pt + 1] = static_cast<int32_t>(std::unique(b, e) - b);
       }
-      P.pt_edge_start[pt + 1] = static_cast<int32_t>(P.edge_pose.size());
-    }
-    P.n_edge = static_cast<int>(P.edge_pose.size());
+    });
+    for (int pt = 0; pt < P.n_pt; ++pt) P.pt_edge_start[pt + 1] += P.pt_edge_start[pt];
+    P.n_edge = P.pt_edge_start[P.n_pt];
+    P.edge_pt.resize(P.n_edge);
+    P.edge_pose.resize(P.n_edge);
+    parallel_for(P.n_pt, [&](int64_t p0, int64_t p1) {
+      for (int64_t pt = p0; pt < p1; ++pt) {
+        const int32_t o = P.pt_edge_start[pt], k = P.pt_edge_start[pt + 1] - o;
+        for (int32_t j = 0; j < k; ++j) {
+          P.edge_pt[o + j] = static_cast<int32_t>(pt);
+          P.edge_pose[o + j] = poses[cnt[pt] + j];
+        }
+      }
+    });
   }
   auto find_edge = [&](int32_t pt, int32_t pose) -> int32_t {
     auto b = P.edge_pose.begin() + P.pt_edge_start[pt];
@@ -538,23 +545,10 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
   P.nbedge_w.reserve(P.n_edge);
   P.nbedge_start.reserve(static_cast<size_t>(P.n_edge) + 1);
   std::vector<int32_t> nb;
-  for (int c = 0; c < P.n_comp; ++c) {
-    if (P.comp_start[c + 1] - P.comp_start[c] == 1) {
-      // a lone point: its neighbour poses are its (sorted, unique) edges
-      const int32_t i = P.comp_start[c];
-      const int32_t e0 = P.pt_edge_start[i], e1 = P.pt_edge_start[i + 1];
-      P.comp_y_base[c] = static_cast<int64_t>(arena);
-      arena += 18ull * (e1 - e0);
-      for (int32_t e = e0; e < e1; ++e) {
-        P.nb_pose.push_back(P.edge_pose[e]);
-        P.nb_comp.push_back(c);
-        P.nbedge_pt.push_back(0);
-        P.nbedge_w.push_back(static_cast<uint32_t>(P.off_W + 18ull * e));
-        P.nbedge_start.push_back(static_cast<int32_t>(P.nbedge_pt.size()));
-      }
-      P.comp_nb_start.push_back(static_cast<int32_t>(P.nb_pose.size()));
-      continue;
-    }
+  // chains of >= 2 points come first (longest first), the lone points last
+  int32_t c_lone = 0;
+  while (c_lone < P.n_comp && P.comp_start[c_lone + 1] - P.comp_start[c_lone] >= 2) ++c_lone;
+  for (int c = 0; c < c_lone; ++c) {
     nb.clear();
     for (int32_t i = P.comp_start[c]; i < P.comp_start[c + 1]; ++i)
       for (int32_t e = P.pt_edge_start[i]; e < P.pt_edge_start[i + 1]; ++e) nb.push_back(P.edge_pose[e]);
@@ -577,6 +571,38 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
       P.nbedge_start.push_back(static_cast<int32_t>(P.nbedge_pt.size()));
     }
     P.comp_nb_start.push_back(static_cast<int32_t>(P.nb_pose.size()));
+  }
+  {
+    // a lone point's neighbour poses are its (sorted, unique) edges, one edge
+    // each; the lone points' edges are contiguous, so every position follows
+    // from the edge index (filled in parallel)
+    const int32_t e_l0 = c_lone < P.n_comp ? P.pt_edge_start[P.comp_start[c_lone]] : P.n_edge;
+    const int64_t nl = P.n_edge - e_l0;
+    const int64_t nb_base = static_cast<int64_t>(P.nb_pose.size()), ne_base = static_cast<int64_t>(P.nbedge_pt.size());
+    P.nb_pose.resize(nb_base + nl);
+    P.nb_comp.resize(nb_base + nl);
+    P.nbedge_pt.resize(ne_base + nl);
+    P.nbedge_w.resize(ne_base + nl);
+    P.nbedge_start.resize(nb_base + nl + 1);
+    P.comp_nb_start.resize(static_cast<size_t>(P.n_comp) + 1);
+    const uint64_t y0 = arena;
+    arena += 18ull * nl;
+    parallel_for(P.n_comp - c_lone, [&](int64_t q0, int64_t q1) {
+      for (int64_t q = q0; q < q1; ++q) {
+        const int32_t c = c_lone + static_cast<int32_t>(q), i = P.comp_start[c];
+        const int32_t e0 = P.pt_edge_start[i], e1 = P.pt_edge_start[i + 1];
+        P.comp_y_base[c] = static_cast<int64_t>(y0 + 18ull * (e0 - e_l0));
+        for (int32_t e = e0; e < e1; ++e) {
+          const int64_t j = e - e_l0;
+          P.nb_pose[nb_base + j] = P.edge_pose[e];
+          P.nb_comp[nb_base + j] = c;
+          P.nbedge_pt[ne_base + j] = 0;
+          P.nbedge_w[ne_base + j] = static_cast<uint32_t>(P.off_W + 18ull * e);
+          P.nbedge_start[nb_base + j + 1] = static_cast<int32_t>(ne_base + j + 1);
+        }
+        P.comp_nb_start[c + 1] = static_cast<int32_t>(nb_base + (e1 - e_l0));
+      }
+    });
   }
   P.off_v = arena; arena += 3ull * P.n_pt;
   align2();
@@ -713,18 +739,27 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
     align2();
     P.off_I6 = arena;
     arena += 36;
-    std::vector<std::vector<int32_t>> cls;
+    // per first-pose bucket: class representatives, each point's class, and
+    // the members of one class at a time (flat scratch, no per-bucket allocation)
+    std::vector<int32_t> rep, cls_of, mem;
+    P.lone_blk.reserve(static_cast<size_t>(kLoneBlk) * (byfirst.size() / kLoneSub + 2 * static_cast<size_t>(P.n_pose) + 1));
     int64_t n_grouped = 0;
     for (int32_t x = 0; x < P.n_pose; ++x) {
-      cls.clear();
-      for (int32_t k = fstart[x]; k < fstart[x + 1]; ++k) {
+      const int32_t k0b = fstart[x], k1b = fstart[x + 1];
+      if (k0b == k1b) continue;
+      rep.clear();
+      cls_of.resize(k1b - k0b);
+      for (int32_t k = k0b; k < k1b; ++k) {
         const int32_t pt = byfirst[k];
         size_t ci = 0;
-        while (ci < cls.size() && !same_list(cls[ci][0], pt)) ++ci;
-        if (ci == cls.size()) cls.emplace_back();
-        cls[ci].push_back(pt);
+        while (ci < rep.size() && !same_list(rep[ci], pt)) ++ci;
+        if (ci == rep.size()) rep.push_back(pt);
+        cls_of[k - k0b] = static_cast<int32_t>(ci);
       }
-      for (const std::vector<int32_t>& mem : cls) {
+      for (size_t ci = 0; ci < rep.size(); ++ci) {
+        mem.clear();
+        for (int32_t k = k0b; k < k1b; ++k)
+          if (cls_of[k - k0b] == static_cast<int32_t>(ci)) mem.push_back(byfirst[k]);
         const int32_t e0 = P.pt_edge_start[mem[0]], m = P.pt_edge_start[mem[0] + 1] - e0;
         const int32_t n = static_cast<int32_t>(mem.size()), nsub = (n + kLoneSub - 1) / kLoneSub;
         for (int32_t u = 0; u < nsub; ++u) {
