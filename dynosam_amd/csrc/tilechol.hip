@@ -1094,7 +1094,10 @@ __global__ __launch_bounds__(kBackThreads) void k_back_persist(TileDev b, const 
                                                                double* partials, int* arrive, unsigned* done,
                                                                unsigned epoch, int* fail) {
   constexpr int NP = kBackThreads / T;
-  constexpr int CH = 2;  // entries per chunk; the first chunk is fetched before the wait
+#ifndef DYNOHIP_BACK_CH
+#define DYNOHIP_BACK_CH 4
+#endif
+  constexpr int CH = DYNOHIP_BACK_CH;  // entries per chunk; the first chunk is fetched before the wait
   __shared__ double part[NP][T];
   __shared__ double rv[T];
   __shared__ double xs[CH][T];
