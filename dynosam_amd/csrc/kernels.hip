@@ -1446,8 +1446,15 @@ __global__ __launch_bounds__(kBlock) void k_lone_schur(LoneSchurDev d, double* _
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = 16 * I + lk + 4 * i, a = row / 6, r = row - 6 * a;
-      if (row < n6 && col < n6 && b <= a)
-        arena[out + 36 * (a * (a + 1) / 2 + b) + 6 * r + c] = acc[j][i] + (a == b ? sJJ[36 * a + 6 * r + c] : 0.0);
+      if (row < n6 && col < n6 && b <= a) {
+        const double v = acc[j][i] + (a == b ? sJJ[36 * a + 6 * r + c] : 0.0);
+        arena[out + 36 * (a * (a + 1) / 2 + b) + 6 * r + c] = v;
+        // a diagonal block that straddles a 16-column boundary has entries
+        // (r < c) in an upper tile, which no lane computes: they get the
+        // symmetric value, so all 36 entries the gather reads are written
+        if (a == b && r > c && (6 * a + c) / 16 < (6 * a + r) / 16)
+          arena[out + 36 * (a * (a + 1) / 2 + a) + 6 * c + r] = v;
+      }
     }
   }
   LCLK(4);

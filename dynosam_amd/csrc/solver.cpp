@@ -346,6 +346,28 @@ int upload_plan(dynohip_solver* s) {
   s->sd.fdep = s->fdep.p;
   s->sd.fqueue = s->fsync.p;
   s->sd.wcnt = s->fsync.p + 4;
+  // debug: DYNOHIP_POISON_MASK fills the selected device buffers with NaN
+  // bytes after a re-plan (bit 0 arena, 1 partials, 2 slots, 3 gred, 4 xy,
+  // 5 dpt, 6 wdx, 7 linv, 8 contrib, 9 bpartials, 10 pose_c/pt_c), so a read
+  // of a never-written element shows up
+  if (const char* pm = std::getenv("DYNOHIP_POISON_MASK")) {
+    const unsigned mask = static_cast<unsigned>(std::strtoul(pm, nullptr, 0));
+    auto poison = [&](unsigned bit, void* p, size_t bytes) {
+      if ((mask >> bit) & 1u && p && bytes) (void)hipMemsetAsync(p, 0xff, bytes, st);
+    };
+    poison(0, s->arena.p, s->arena.n * 8);
+    poison(1, s->partials.p, s->partials.n * 8);
+    poison(2, s->slots.p, s->slots.n * 8);
+    poison(3, s->gred.p, s->gred.n * 8);
+    poison(4, s->xy.p, s->xy.n * 8);
+    poison(5, s->dpt.p, s->dpt.n * 8);
+    poison(6, s->wdx.p, s->wdx.n * 8);
+    poison(7, s->linv.p, s->linv.n * 8);
+    poison(8, s->contrib.p, s->contrib.n * 8);
+    poison(9, s->bpartials.p, s->bpartials.n * 8);
+    poison(10, s->pose_c.p, s->pose_c.n * 8);
+    poison(10, s->pt_c.p, s->pt_c.n * 8);
+  }
   HIPCHK(s, hipStreamSynchronize(st));
   return 0;
 }
