@@ -375,19 +375,22 @@ def test_no_read_before_write(gpu_available, monkeypatch, name, kw):
     """Every device buffer a solve reads is written first in that solve (or
     by the plan upload): with the arena, partial sums, tiles, right-hand
     sides, solution, scratch and candidate values filled with NaN bytes after
-    the plan upload (DYNOHIP_POISON_MASK, solver.cpp), the conditioned
-    per-iteration parity still holds. A fresh allocation's zeroed pages hide
-    such a read: a test run after others (reused memory) does not."""
+    the plan upload (DYNOHIP_POISON_MASK, solver.cpp), LM iterations give
+    bit-identical values and the same iteration counts as without. A fresh
+    allocation's zeroed pages hide such a read; a run after other tests
+    (reused memory) does not."""
+    def run():
+        g, v, _, s = make(name, **kw)
+        s.reset()
+        out = []
+        for _ in range(4):
+            r = s.iterate()
+            out.append((r.iterations, r.inner_iterations, s.values_data().copy()))
+        return out
+    clean = run()
     monkeypatch.setenv("DYNOHIP_POISON_MASK", str((1 << 11) - 1))
-    g, v, _, s = make(name, **kw)
-    o = Oracle(g, v)
-    mask = gauge_mask(v) if kw.get("formulation") == 1 else slice(None)
-    assert np.isfinite(s.error())
-    s.reset()
-    o.reset()
-    for it in range(4):
-        o.set_values_data(s.values_data())
-        sg, so = s.iterate(), o.iterate()
-        assert (sg.iterations, sg.inner_iterations) == (so.iterations, so.inner_iterations), it
-        assert np.all(np.isfinite(s.values_data()))
-        assert rel(s.values_data()[mask], o.values_data()[mask]) < PER_ITER_TOL, it
+    poisoned = run()
+    for it, ((i0, n0, v0), (i1, n1, v1)) in enumerate(zip(clean, poisoned)):
+        assert (i0, n0) == (i1, n1), it
+        assert np.all(np.isfinite(v1)), it
+        assert np.array_equal(v0, v1), it
