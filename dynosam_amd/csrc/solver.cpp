@@ -156,14 +156,11 @@ struct dynohip_solver {
   bool lin_valid = false;
   // (the speculative linearisation's error at delta = 0, result[3], arrives
   // with the next try's results)
-  // try results, written by the kernels' final reductions straight into
-  // pinned host memory ([0] linear error, [1] nonlinear error, [2] and [3]/[5]
-  // errors at delta = 0, [4] fail bits); the host waits on an event recorded
-  // before the speculative linearisation is enqueued, so it decides while the
-  // GPU linearises
+  // try results, copied into pinned host memory behind an event that is
+  // recorded before the speculative linearisation is enqueued: the host
+  // decides while the GPU linearises
   double* hres = nullptr;
   hipEvent_t ev_res = nullptr;
-  int spec_slot = 3;   // hres slot of the last speculative linearisation's error at delta = 0
   int iterations = 0, inner = 0, converged = 0;
   std::vector<dynohip_trace_entry> trace;
   // values snapshot (bench hook)
@@ -444,9 +441,8 @@ int sep_copy(dynohip_solver* s, bool pack) {
 }
 
 // error at (pose, pt) into result[slot]
-void enqueue_error(dynohip_solver* s, const double* pose, const double* pt, double* partials, double* out,
-                   int* fail_out) {
-  launch_error(s->td, pose, pt, partials, s->sumctr.p, out, s->failp, fail_out,
+void enqueue_error(dynohip_solver* s, const double* pose, const double* pt, double* partials, double* out) {
+  launch_error(s->td, pose, pt, partials, s->sumctr.p, out, s->failp, reinterpret_cast<int*>(s->result.p + 4),
                s->stream);
 }
 
@@ -455,7 +451,7 @@ void enqueue_linerr(dynohip_solver* s, const double* dpose, const double* dpt, d
 }
 
 int compute_error(dynohip_solver* s, const double* pose, const double* pt, double* err_out) {
-  enqueue_error(s, pose, pt, s->partials.p, s->result.p, reinterpret_cast<int*>(s->result.p + 4));
+  enqueue_error(s, pose, pt, s->partials.p, s->result.p);
   HIPCHK(s, hipMemcpyAsync(err_out, s->result.p, sizeof(double), hipMemcpyDeviceToHost, s->stream));
   HIPCHK(s, hipStreamSynchronize(s->stream));
   return comm_sum(s, err_out, 1, 0);
@@ -531,12 +527,10 @@ int enqueue_try(dynohip_solver* s, double lambda) {
   // pose deltas are x[0 .. 6 n_pose) in pose-index order
   launch_backsub(s->cd, P.n_edge, A, x, s->wdx.p, s->dpt.p, st,
                  P.lone_all_grouped ? static_cast<int>(P.lgroup.size()) : 0, s->lone_blk.p);
-  // the try's results go straight to pinned host memory (hres)
-  enqueue_linerr(s, x, s->dpt.p, s->partials.p, s->hres);
+  enqueue_linerr(s, x, s->dpt.p, s->partials.p, s->result.p);
   if (timed) (void)hipEventRecord(s->ev[7], st);
   launch_retract(P.n_pose, P.n_pt, s->pose.p, s->pt.p, x, s->dpt.p, s->pose_c.p, s->pt_c.p, st);
-  enqueue_error(s, s->pose_c.p, s->pt_c.p, s->partials.p + s->partial_slots, s->hres + 1,
-                reinterpret_cast<int*>(s->hres + 4));
+  enqueue_error(s, s->pose_c.p, s->pt_c.p, s->partials.p + s->partial_slots, s->result.p + 1);
   if (timed) (void)hipEventRecord(s->ev[8], st);
   return 0;
 }
@@ -631,7 +625,7 @@ int lm_iterate(dynohip_solver* s) {
     oldlin_slot = 3;
   } else {
     if (s->timing) (void)hipEventRecord(s->ev[0], st);
-    enqueue_linearize(s, s->pose.p, s->pt.p, s->hres + 2);
+    enqueue_linearize(s, s->pose.p, s->pt.p, s->result.p + 2);
     if (s->timing) (void)hipEventRecord(s->ev[1], st);
   }
   s->lin_valid = false;
@@ -652,18 +646,16 @@ int lm_iterate(dynohip_solver* s) {
     }
     int trc = enqueue_try(s, s->lambda);
     if (trc) return trc;
+    HIPCHK(s, hipMemcpyAsync(s->hres, s->result.p, 5 * sizeof(double), hipMemcpyDeviceToHost, st));
     HIPCHK(s, hipEventRecord(s->ev_res, st));
-    // the speculative linearisation's error at delta = 0 goes to the slot
-    // (3 or 5) the previous one did not use: the host reads that one below
-    const int spec_prev = s->spec_slot;
     if (speculate) {
-      s->spec_slot = spec_prev == 3 ? 5 : 3;
-      enqueue_linearize(s, s->pose_c.p, s->pt_c.p, s->hres + s->spec_slot);
+      // result[3] is read with the next try's results (stream order keeps
+      // this launch's value until then)
+      enqueue_linearize(s, s->pose_c.p, s->pt_c.p, s->result.p + 3);
     }
     HIPCHK(s, hipEventSynchronize(s->ev_res));
     double res[5];
     std::memcpy(res, s->hres, sizeof(res));
-    res[3] = s->hres[spec_prev];
     int fail = 0;
     std::memcpy(&fail, &res[4], sizeof(int));
     if (s->nranks > 1) {
@@ -798,7 +790,7 @@ int dynohip_create(int device_id, dynohip_solver** out) {
   (void)hipEventCreateWithFlags(&s->ev_side, hipEventDisableTiming);
   for (auto& e : s->ev) (void)hipEventCreate(&e);
   if (hipEventCreateWithFlags(&s->ev_res, hipEventDisableTiming) != hipSuccess ||
-      hipHostMalloc(reinterpret_cast<void**>(&s->hres), 8 * sizeof(double), hipHostMallocCoherent) != hipSuccess) {
+      hipHostMalloc(reinterpret_cast<void**>(&s->hres), 8 * sizeof(double), hipHostMallocDefault) != hipSuccess) {
     dynohip_destroy(s);
     return DYNOHIP_EHIP;
   }
