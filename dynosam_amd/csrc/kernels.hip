@@ -717,6 +717,9 @@ __device__ __forceinline__ void gather_band(const GatherDev& g, const int32_t* _
   const int t = (blk * kBlock + static_cast<int>(threadIdx.x)) >> 6;
   const int q = threadIdx.x & 63;
   if (t >= g.n) return;
+  // the target's poses and tile slots, fetched ahead of its entries
+  const int A = tA[t], B = tB[t];
+  const uint32_t ts[4] = {tslot[4 * t], tslot[4 * t + 1], tslot[4 * t + 2], tslot[4 * t + 3]};
   double acc[36], a18[18], a9[9], a5[5], a3[3], a2[2], a1[1];
   group_accumulate<6, 6, 64, 1>(g.start, g.ent, t, q, arena, acc);
   rs_step<36, 32>(acc, a18, q & 32);
@@ -727,13 +730,13 @@ __device__ __forceinline__ void gather_band(const GatherDev& g, const int32_t* _
   rs_step<2, 1>(a2, a1, q & 1);
   const int idx = rs_index<36>(q);
   if (idx < 0) return;
-  const int A = tA[t], B = tB[t];
   const int r = idx / 6, c = idx % 6;
   if (A == B && r < c) return;
   const int row = 6 * A + r, col = 6 * B + c;
   const double val = a1[0] + (A == B && r == c && (!damp || damp[row]) ? lambda : 0.0);
   // the tile from the target's precomputed slots (no lookup chain)
-  const uint32_t e = tslot[4 * t + 2 * ((row >> 6) != ((6 * A) >> 6)) + ((col >> 6) != ((6 * B) >> 6))];
+  const int sel = 2 * ((row >> 6) != ((6 * A) >> 6)) + ((col >> 6) != ((6 * B) >> 6));
+  const uint32_t e = sel == 0 ? ts[0] : sel == 1 ? ts[1] : sel == 2 ? ts[2] : ts[3];
   const int64_t at = static_cast<int64_t>(e & 0x7fffffffu) * kTile * kTile +
                      ((e >> 31) ? (col % kTile) * kTile + row % kTile : (row % kTile) * kTile + col % kTile);
   b.slots[at] = val;

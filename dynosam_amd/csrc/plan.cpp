@@ -829,12 +829,25 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
   {
     // the pair enumeration: the factors' pose pairs, then every component's
     // neighbour-pose pairs, components in order
+    // the PoseToPoint factors outside the lone groups, in factor order (the
+    // enumerations below run once per worker and pass: they skip the grouped
+    // ones without visiting them)
+    std::vector<int32_t> keep0;
+    keep0.reserve(P.types[0].n);
+    for (int i = 0; i < P.types[0].n; ++i)
+      if (!lone_grouped[P.types[0].idx[2 * i + 1]]) keep0.push_back(i);
+    auto for_factors = [&](int t, auto&& fn) {
+      if (t == 0) {
+        for (int32_t i : keep0) fn(i);
+      } else {
+        for (int i = 0; i < P.types[t].n; ++i) fn(i);
+      }
+    };
     auto emit_factor_pairs = [&](auto&& pair_fn) {  // pair_fn(A, B, entry)
       for (int t = 0; t < kNTypes; ++t) {
         const TypePlan& tp = P.types[t];
         const int nk = kNKeys[t], d = kDim[t];
-        for (int i = 0; i < tp.n; ++i) {
-          if (t == 0 && lone_grouped[tp.idx[i * nk + 1]]) continue;
+        for_factors(t, [&](int i) {
           for (int sa = 0; sa < nk; ++sa) {
             if (kSlotKind[t][sa] != 0) continue;
             const int32_t A = tp.idx[i * nk + sa];
@@ -845,7 +858,7 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
               pair_fn(A, B, GEntry{block_off(tp, t, i, sa), block_off(tp, t, i, sb), d, 1});
             }
           }
-        }
+        });
       }
     };
     // the lone-point groups' partial blocks (after every factor and component)
@@ -881,11 +894,10 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
       for (int t = 0; t < kNTypes; ++t) {
         const TypePlan& tp = P.types[t];
         const int nk = kNKeys[t], d = kDim[t];
-        for (int i = 0; i < tp.n; ++i) {
-          if (t == 0 && lone_grouped[tp.idx[i * nk + 1]]) continue;
+        for_factors(t, [&](int i) {
           for (int sa = 0; sa < nk; ++sa)
             if (kSlotKind[t][sa] == 0) fn(tp.idx[i * nk + sa], GEntry{block_off(tp, t, i, sa), b_off(tp, t, i), d, 1});
-        }
+        });
       }
       for (int c = 0; c < P.n_comp; ++c) {
         const int32_t nb0 = P.comp_nb_start[c], m = P.comp_nb_start[c + 1] - nb0;
