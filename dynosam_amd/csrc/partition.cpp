@@ -254,6 +254,30 @@ extern "C" int dynohip_plan_export(const dynohip_graph_view* g, const uint64_t* 
     raw(G->ent.data(), G->ent.size() * sizeof(GEntry));
   }
   else if (nm == "red_b") vec(P.red_B);
+  // lone-point groups (plan.hpp LoneGroup): the device blocks, each group's
+  // (m, npt, pose_beg, out), its neighbour poses, the edge structure and the
+  // PoseToPoint records they point into
+  else if (nm == "lone_blk") raw(P.lone_blk.data(), P.lone_blk.size() * sizeof(int32_t));
+  else if (nm == "lgroup") raw(P.lgroup.data(), P.lgroup.size() * sizeof(LoneGroup));
+  else if (nm == "lone_pose") vec(P.lone_pose);
+  else if (nm == "lone_info") {
+    int32_t c_long = 0;
+    while (c_long < P.n_comp && P.comp_start[c_long + 1] - P.comp_start[c_long] >= 2) ++c_long;
+    tmp = {P.lone_all_grouped ? 1 : 0, static_cast<int32_t>(P.lgroup.size()), P.lone_max_m,
+           c_long < P.n_comp ? P.comp_start[c_long] : P.n_pt, P.n_pt};
+    vec(tmp);
+  } else if (nm == "pt_edges") vec(P.pt_edge_start);   // (names ending in _start are gather lists)
+  else if (nm == "edge_pose") vec(P.edge_pose);
+  else if (nm == "comp_starts") vec(P.comp_start);
+  else if (nm.size() == 9 && nm.compare(0, 8, "type_idx") == 0 && nm[8] >= '0' && nm[8] < '0' + kNTypes)
+    vec(P.types[nm[8] - '0'].idx);
+  else if (nm == "type_rec") {   // per type: arena offset of the first record, doubles per record
+    for (int t = 0; t < kNTypes; ++t) {
+      tmp.push_back(static_cast<int32_t>(P.types[t].base));
+      tmp.push_back(static_cast<int32_t>(P.types[t].stride));
+    }
+    vec(tmp);
+  }
   else if (nm == "value_owner") vec(part.value_owner);
   else if (nm == "damp_row") {
     tmp.assign(part.damp_row.begin(), part.damp_row.end());

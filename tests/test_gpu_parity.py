@@ -14,6 +14,7 @@ from dynosam_amd import synth
 from dynosam_amd.graph import NonlinearFactorGraph, Values
 from dynosam_amd.optimizer import DynohipError, Solver
 from oracle_binding import Oracle
+from graphs_extra import mixed_lone_graph
 
 pytestmark = pytest.mark.gpu
 
@@ -370,7 +371,7 @@ def test_errors(gpu_available):
         s4.optimize()
 
 
-@pytest.mark.parametrize("name,kw", [("T2", {}), ("T2", {"formulation": 1}), ("C1", {})])
+@pytest.mark.parametrize("name,kw", [("T2", {}), ("T2", {"formulation": 1}), ("C1", {}), ("mixed", {})])
 def test_no_read_before_write(gpu_available, monkeypatch, name, kw):
     """Every device buffer a solve reads is written first in that solve (or
     by the plan upload): with the arena, partial sums, tiles, right-hand
@@ -380,7 +381,13 @@ def test_no_read_before_write(gpu_available, monkeypatch, name, kw):
     allocation's zeroed pages hide such a read; a run after other tests
     (reused memory) does not."""
     def run():
-        g, v, _, s = make(name, **kw)
+        if name == "mixed":   # lone points partly outside the groups (graphs_extra)
+            g, v, _, _ = mixed_lone_graph()
+            s = Solver(0)
+            s.set_graph(g)
+            s.set_values(v)
+        else:
+            g, v, _, s = make(name, **kw)
         s.reset()
         out = []
         for _ in range(4):
@@ -394,3 +401,26 @@ def test_no_read_before_write(gpu_available, monkeypatch, name, kw):
         assert (i0, n0) == (i1, n1), it
         assert np.all(np.isfinite(v1)), it
         assert np.array_equal(v0, v1), it
+
+
+def test_mixed_lone_points_conditioned(gpu_available):
+    """Some lone points outside the groups (graphs_extra.mixed_lone_graph):
+    groups for the rest, the CSR point gathers, lone Y and per-point
+    back-substitution for every lone point; conditioned per-iteration parity
+    at the north-star bar, as test_per_iteration_parity_conditioned."""
+    g, v, _, _ = mixed_lone_graph()
+    s = Solver(0)
+    s.set_graph(g)
+    s.set_values(v)
+    o = Oracle(g, v)
+    assert s.error() == pytest.approx(o.error(), rel=1e-12)
+    s.reset()
+    o.reset()
+    for it in range(6):
+        o.set_values_data(s.values_data())
+        start = s.values_data()
+        sg, so = s.iterate(), o.iterate()
+        assert (sg.iterations, sg.inner_iterations) == (so.iterations, so.inner_iterations), it
+        if np.linalg.norm(o.values_data() - start) == 0:
+            continue
+        assert rel(s.values_data(), o.values_data()) < PER_ITER_TOL, it
