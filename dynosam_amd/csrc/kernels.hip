@@ -1400,13 +1400,29 @@ __global__ __launch_bounds__(kBlock) void k_lone_schur(LoneSchurDev d, double* _
     const int ca = 16 * I + li, cb = 16 * J + li;
     const bool va = ca < n6, vb = cb < n6;
     const int oa = 18 * (ca / 6) + ca % 6, ob = 18 * (cb / 6) + cb % 6;
-    for (int s4 = 0; s4 < ks; ++s4) {
+    // two independent accumulator chains (even / odd K-steps, operands of
+    // both loaded first), added at the end: the MFMA latency is hidden
+    auto operands = [&](int s4, double& za, double& zb) {
       const int kp = 4 * s4 + lk, p = kp / 3, ro = p * m18 + 6 * (kp - 3 * p);
       const bool vk = kp < K;
-      const double za = (va && vk) ? sZ[ro + oa] : 0.0;
-      const double zb = (vb && vk) ? sZ[ro + ob] : 0.0;
-      acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(-za, zb, acc[j], 0, 0, 0);
+      za = (va && vk) ? sZ[ro + oa] : 0.0;
+      zb = (vb && vk) ? sZ[ro + ob] : 0.0;
+    };
+    v4d acc1 = v4d{0.0, 0.0, 0.0, 0.0};
+    int s4 = 0;
+    for (; s4 + 1 < ks; s4 += 2) {
+      double za0, zb0, za1, zb1;
+      operands(s4, za0, zb0);
+      operands(s4 + 1, za1, zb1);
+      acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(-za0, zb0, acc[j], 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(-za1, zb1, acc1, 0, 0, 0);
     }
+    if (s4 < ks) {
+      double za0, zb0;
+      operands(s4, za0, zb0);
+      acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(-za0, zb0, acc[j], 0, 0, 0);
+    }
+    acc[j] += acc1;
   }
   const uint32_t out = static_cast<uint32_t>(hdr[2]);
   if (wave >= 2 && lane < n6) {
