@@ -38,6 +38,10 @@ __device__ __forceinline__ double block_sum(double v) {
   return r;
 }
 
+// Factor evaluation (residuals, Jacobians, whitening, Huber weights, the
+// nonlinear error) without FMA contraction: rounded exactly as oracle/oracle.c
+// rounds the same expressions (see se3.hpp).
+#pragma clang fp contract(off)
 __device__ __forceinline__ void skew_into(const double* q, double* J, int ld, int c0, double sign) {
   // sign * skew(q) written at columns c0..c0+2
   J[0 * ld + c0 + 0] = 0.0;        J[0 * ld + c0 + 1] = -sign * q[2]; J[0 * ld + c0 + 2] = sign * q[1];
@@ -357,6 +361,8 @@ __device__ __forceinline__ double error_one(const TypeDev& tp, int i, const doub
   }
   return 0.5 * d2;
 }
+
+#pragma clang fp contract(fast)
 
 // JacobianFactor::error(delta) = 0.5 ||A delta - b||^2
 template <int T>
@@ -1658,9 +1664,11 @@ __global__ __launch_bounds__(kBlock) void k_retract(int n_pose, int n_pt, const 
 }  // namespace
 
 // ---------------------------------------------------------------- launchers
-// Launch groups: PoseToPoint alone (it dominates the factor count and keeps
-// its own occupancy), the low-count Ternary/Between/Prior together, and the
-// two LLWorld types alone (their register counts would cap the others).
+// Launch groups: PoseToPoint together with the low-count Ternary/Between/Prior
+// types in one launch (group 0), and the two LLWorld types alone (their
+// register counts would cap the others). Within a launch, workgroups are
+// mapped to blocks in reverse, so the long pose-pose / ternary blocks (last
+// in type order) start first and the short PoseToPoint blocks fill in.
 constexpr unsigned kGroups[] = {0xFu, 1u << 4, 1u << 5};
 constexpr int kNGroups = sizeof(kGroups) / sizeof(kGroups[0]);
 

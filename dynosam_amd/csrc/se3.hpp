@@ -10,6 +10,15 @@
 #include <cfloat>
 #include <cmath>
 
+// No fused multiply-add contraction in the pose arithmetic: every product
+// and sum is rounded as the CPU restatement rounds it (oracle/oracle.c, the
+// same formulas in the same order, compiled without FMA), so the residuals
+// and Jacobians of the factor kernels are bit-identical to the oracle's.
+// Near convergence the Huber weights k/||r|| of the sigma-1e-5 ternary
+// factors are computed from residuals dominated by cancellation; rounding
+// them differently moved whole Jacobian rows by ~1e-5.
+#pragma clang fp contract(off)
+
 namespace dynohip {
 
 #define DH_HD __host__ __device__ __forceinline__
@@ -200,3 +209,5 @@ DH_HD void pose_logmap(const P3& T, double* xi) {
 DH_HD P3 pose_retract(const P3& T, const double* xi) { return compose(T, pose_expmap(xi)); }
 
 }  // namespace dynohip
+
+#pragma clang fp contract(fast)

@@ -163,8 +163,9 @@ struct dynohip_solver {
   hipEvent_t ev_res = nullptr;
   int iterations = 0, inner = 0, converged = 0;
   std::vector<dynohip_trace_entry> trace;
-  // values snapshot (bench hook)
+  // values snapshot (bench hook), tagged with the plan it was taken under
   DevBuf<double> pose_snap, pt_snap;
+  uint64_t plan_gen = 0, snap_gen = 0;   // snap_gen 0: no snapshot
   // phase timing (HIP events, optional)
   bool timing = false;
   hipEvent_t ev[9] = {};
@@ -515,6 +516,9 @@ int enqueue_try(dynohip_solver* s, double lambda) {
     s->sd1.epoch = s->sd.epoch;
     launch_tile_forward(s->bd, s->sd1, P.flevel1, P.fpanels1, s->linv.p, s->gred.p, s->contrib.p, y, s->failp, st,
                         s->side, s->ev_main, s->ev_side);
+    // (ms_cholesky of a partitioned handle spans both forward phases and the
+    // exchange between them)
+    if (timed) (void)hipEventRecord(s->ev[5], st);
     launch_tile_backward(s->bd, s->sd, P.bplevel, s->linv.p, y, x, s->failp, st);
   } else {
     launch_tile_forward(s->bd, s->sd, P.flevel, P.fpanels, s->linv.p, s->gred.p, s->contrib.p, y, s->failp, st,
@@ -522,7 +526,6 @@ int enqueue_try(dynohip_solver* s, double lambda) {
     if (timed) (void)hipEventRecord(s->ev[5], st);
     launch_tile_backward(s->bd, s->sd, P.bplevel, s->linv.p, y, x, s->failp, st);
   }
-  if (timed && s->nranks > 1) (void)hipEventRecord(s->ev[5], st);
   if (timed) (void)hipEventRecord(s->ev[6], st);
   // pose deltas are x[0 .. 6 n_pose) in pose-index order
   launch_backsub(s->cd, P.n_edge, A, x, s->wdx.p, s->dpt.p, st,
@@ -875,6 +878,7 @@ int dynohip_set_values(dynohip_solver* s, const uint64_t* keys, const uint8_t* k
     s->value_keys.assign(keys, keys + n);
     s->value_kind.assign(kind, kind + n);
     s->has_plan = true;
+    ++s->plan_gen;   // a snapshot of the previous graph's values no longer applies
     s->base_stats_valid = false;
   }
   s->lin_valid = false;
@@ -1048,6 +1052,44 @@ int dynohip_linearize(dynohip_solver* s, double* out, size_t n_doubles) {
   return DYNOHIP_OK;
 }
 
+int dynohip_solve_delta(dynohip_solver* s, double lambda, double* delta_out, size_t n_doubles, int* solved_out) {
+  int rc = ready(s);
+  if (rc) return rc;
+  if (s->nranks > 1) return set_err(s, DYNOHIP_EINVAL, "solve_delta: single-GPU handles only");
+  if (!(lambda >= 0.0) || !std::isfinite(lambda)) return set_err(s, DYNOHIP_EINVAL, "solve_delta: lambda %g", lambda);
+  size_t need = 0;
+  for (uint8_t k : s->value_kind) need += k == DYNOHIP_POSE3 ? 6 : 3;
+  if (!delta_out || n_doubles < need)
+    return set_err(s, DYNOHIP_EINVAL, "solve_delta: output buffer too small (%zu < %zu)", n_doubles, need);
+  (void)hipSetDevice(s->device);
+  const Plan& P = s->plan;
+  // the same launches as one tryLambda of lm_iterate, at the current values
+  s->lin_valid = false;
+  enqueue_linearize(s, s->pose.p, s->pt.p, s->result.p + 2);
+  rc = enqueue_try(s, lambda);
+  if (rc) return rc;
+  const size_t nrp = static_cast<size_t>(P.NT) * kTile;
+  std::vector<double> hx(6ull * P.n_pose), hq(3ull * P.n_pt);
+  double res[5];
+  if (!hx.empty()) HIPCHK(s, hipMemcpyAsync(hx.data(), s->xy.p + nrp, hx.size() * sizeof(double), hipMemcpyDeviceToHost, s->stream));
+  if (!hq.empty()) HIPCHK(s, hipMemcpyAsync(hq.data(), s->dpt.p, hq.size() * sizeof(double), hipMemcpyDeviceToHost, s->stream));
+  HIPCHK(s, hipMemcpyAsync(res, s->result.p, sizeof(res), hipMemcpyDeviceToHost, s->stream));
+  HIPCHK(s, hipStreamSynchronize(s->stream));
+  int fail = 0;
+  std::memcpy(&fail, &res[4], sizeof(int));
+  if (fail & 6) return set_err(s, DYNOHIP_EHIP, "solve_delta: dependency wait timed out");
+  if (solved_out) *solved_out = fail == 0 && std::isfinite(res[0]);
+  size_t off = 0;
+  for (size_t i = 0; i < s->value_kind.size(); ++i) {
+    const bool pose = s->value_kind[i] == DYNOHIP_POSE3;
+    const int sz = pose ? 6 : 3;
+    const double* src = pose ? &hx[6ull * P.user_idx[i]] : &hq[3ull * P.user_idx[i]];
+    std::memcpy(delta_out + off, src, sz * sizeof(double));
+    off += sz;
+  }
+  return DYNOHIP_OK;
+}
+
 int dynohip_values_snapshot(dynohip_solver* s) {
   int rc = ready(s);
   if (rc) return rc;
@@ -1059,6 +1101,7 @@ int dynohip_values_snapshot(dynohip_solver* s) {
   if (P.n_pose) HIPCHK(s, hipMemcpyAsync(s->pose_snap.p, s->pose.p, 12ull * P.n_pose * sizeof(double), hipMemcpyDeviceToDevice, s->stream));
   if (P.n_pt) HIPCHK(s, hipMemcpyAsync(s->pt_snap.p, s->pt.p, 3ull * P.n_pt * sizeof(double), hipMemcpyDeviceToDevice, s->stream));
   HIPCHK(s, hipStreamSynchronize(s->stream));
+  s->snap_gen = s->plan_gen;
   return DYNOHIP_OK;
 }
 
@@ -1066,7 +1109,9 @@ int dynohip_values_restore(dynohip_solver* s) {
   int rc = ready(s);
   if (rc) return rc;
   const Plan& P = s->plan;
-  if ((P.n_pose && s->pose_snap.n != 12ull * P.n_pose) || (P.n_pt && s->pt_snap.n != 3ull * P.n_pt))
+  // a snapshot taken before the last re-plan belongs to another graph, even
+  // when its buffer sizes happen to match (equal-length sliding windows)
+  if (s->snap_gen == 0 || s->snap_gen != s->plan_gen)
     return set_err(s, DYNOHIP_ESTATE, "no snapshot of the current graph's values");
   (void)hipSetDevice(s->device);
   s->lin_valid = false;

@@ -105,6 +105,19 @@ class Solver:
         self.lib.dynohip_get_trace(self.h, arr, n.value, C.byref(n))
         return _abi.trace_to_dicts(arr[: n.value])
 
+    def solve_delta(self, lam):
+        """Test hook: one damped solve at the current values and lambda
+        (one tryLambda's linear system); returns (solved, delta) with delta
+        in value order, 6 per pose and 3 per point."""
+        kinds = self._values.kinds
+        n = int(np.where(kinds == _abi.POSE3, 6, 3).sum())
+        out = np.zeros(n)
+        ok = C.c_int()
+        _check(self.lib, self.h, self.lib.dynohip_solve_delta(self.h, float(lam),
+                                                              out.ctypes.data_as(C.POINTER(C.c_double)), n,
+                                                              C.byref(ok)))
+        return bool(ok.value), out
+
     def linearize(self):
         n = self.lib.dynohip_linearize_size(self.h)
         out = np.zeros(n)

@@ -37,7 +37,12 @@
 extern "C" {
 #endif
 
-#define DYNOHIP_ABI_VERSION 2
+/* 2: dynohip_stats split of ms_cholesky / ms_solve; dynorefine_batch gained
+      its trailing `ternary_inactive` pointer (dynorefine.h is covered by
+      this version: a consumer built against an older header must not call
+      dynorefine_upload).
+   3: dynohip_solve_delta. */
+#define DYNOHIP_ABI_VERSION 3
 
 typedef enum {
   DYNOHIP_OK = 0,
@@ -192,6 +197,17 @@ int dynohip_get_trace(dynohip_solver* s, dynohip_trace_entry* out,
    `out` receives sum_t n_t * dim_t * (cols_t + 1) doubles. */
 int dynohip_linearize(dynohip_solver* s, double* out, size_t n_doubles);
 size_t dynohip_linearize_size(const dynohip_solver* s);
+
+/* Test hook: one damped linear solve at the current values, exactly as one
+   tryLambda of dynohip_iterate performs it (linearise, Schur of the point
+   chains, tile Cholesky of the reduced system, back-substitution):
+   (J^T J + lambda I) delta = -J^T b. `delta_out` receives the tangent-space
+   step in the set_values order: 6 per pose ([omega; v], the candidate is
+   X * Exp(delta)), 3 per point. *solved_out (may be null) = 0 when the damped
+   system is indefinite (GTSAM's IndeterminantLinearSystemException). The
+   values are not changed; the next iterate re-linearises. Single-GPU
+   handles only (DYNOHIP_EINVAL on a partitioned one). */
+int dynohip_solve_delta(dynohip_solver* s, double lambda, double* delta_out, size_t n_doubles, int* solved_out);
 
 /* Bench hooks: device-side snapshot / restore of the current values (no
    PCIe traffic), and problem / work statistics. */

@@ -27,6 +27,12 @@
  *
  * Plain C, host pointers; a handle owns its device buffers and is used from
  * one thread.
+ *
+ * Versioning: the layout of dynorefine_batch is covered by
+ * DYNOHIP_ABI_VERSION (dynohip.h). Version 2 appended `ternary_inactive`; a
+ * consumer checks dynohip_abi_version() == DYNOHIP_ABI_VERSION before
+ * calling dynorefine_upload, since a batch built against an older header is
+ * shorter and its missing trailing pointer would be read as garbage.
  */
 #ifndef DYNOREFINE_H_
 #define DYNOREFINE_H_

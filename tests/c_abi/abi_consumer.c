@@ -14,7 +14,11 @@
  *                       create/set_graph/set_values/optimize/get_values on
  *                       device 0, checked against the CPU oracle
  *                       (liboracle.so, test infrastructure): same iterations
- *                       and inner iterations, values within 1e-6 relative.
+ *                       and inner iterations, values within 1e-6 relative;
+ *                       then one dynorefine batch with every field of the
+ *                       version-3 dynorefine_batch filled (incl. the
+ *                       trailing ternary_inactive mask): an all-zero mask
+ *                       gives the same results as a null one.
  *
  * Prints "OK ..." and exits 0 on success; any mismatch exits 1.
  */
@@ -24,6 +28,7 @@
 #include <string.h>
 
 #include "dynohip.h"
+#include "dynorefine.h"
 #include "dynosynth.h"
 #include "oracle.h"
 
@@ -92,12 +97,76 @@ static int host_checks(void) {
   /* RGBDBackendModule.cc:201-202: full batch at frame full_batch_frame - 1 */
   EXPECT(dynohip_full_batch_trigger(6, 5) == 1, "full batch at its frame");
   EXPECT(dynohip_full_batch_trigger(6, 6) == 0, "full batch only once");
+  /* dynorefine_batch layout of this header version (13 pointer-sized fields) */
+  EXPECT(sizeof(dynorefine_batch) == 13 * sizeof(void*), "dynorefine_batch size %zu", sizeof(dynorefine_batch));
   /* no device in the build container: create reports an error, no crash */
   if (getenv("ABI_EXPECT_NO_DEVICE")) {
     int rc = dynohip_create(0, &s);
     EXPECT(rc != DYNOHIP_OK && s == NULL, "create without a device: rc %d", rc);
   }
   return fails;
+}
+
+/* one (object, frame pair) refinement problem, 12 tracklets of a rigid body
+   moved by a small motion and seen by a camera that moved too */
+static int refine_checks(void) {
+  enum { NT = 12 };
+  double Xa[12] = {1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0}, Xb[12] = {1, 0, 0, 0, 1, 0, 0, 0, 1, 0.1, 0, 0};
+  double H0[12] = {1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0}, cal[5] = {500, 500, 0, 320, 240};
+  double kpa[2 * NT], kpb[2 * NT], ma[3 * NT], mb[3 * NT], Ha[12], Hb[12];
+  int32_t ts[2] = {0, NT};
+  uint8_t mask[NT], oa[NT], ob[NT];
+  dynorefine_result ra, rb;
+  dynorefine_params rp;
+  dynohip_lm_params lm;
+  dynorefine_batch b;
+  dynorefine_solver* r = NULL;
+  int i, k, bad = 0;
+  for (i = 0; i < NT; ++i) {
+    const double x = -0.5 + 0.09 * i, y = 0.3 * ((i % 3) - 1), z = 4.0 + 0.05 * (i % 5);
+    ma[3 * i] = x; ma[3 * i + 1] = y; ma[3 * i + 2] = z;
+    mb[3 * i] = x + 0.05; mb[3 * i + 1] = y; mb[3 * i + 2] = z + 0.02; /* true motion: a translation */
+    kpa[2 * i] = cal[0] * x / z + cal[3];
+    kpa[2 * i + 1] = cal[1] * y / z + cal[4];
+    kpb[2 * i] = cal[0] * (mb[3 * i] - Xb[9]) / mb[3 * i + 2] + cal[3];
+    kpb[2 * i + 1] = cal[1] * mb[3 * i + 1] / mb[3 * i + 2] + cal[4];
+    mask[i] = 0;
+  }
+  memset(&b, 0, sizeof(b));
+  b.n_problems = 1;
+  b.track_start = ts;
+  b.X_k_1 = Xa;
+  b.X_k = Xb;
+  b.H_init = H0;
+  b.calibration = cal;
+  b.kp_k_1 = kpa;
+  b.kp_k = kpb;
+  b.m_k_1 = ma;
+  b.m_k = mb;
+  b.X_k_1_init = Xa;
+  b.X_k_init = Xb;
+  b.ternary_inactive = NULL;
+  dynorefine_params_default(&rp);
+  dynohip_lm_params_default(&lm);
+  if (dynorefine_create(0, &r) != DYNOHIP_OK) return 1;
+  if (dynorefine_run(r, &b, &rp, &lm, Ha, oa, &ra) != DYNOHIP_OK) {
+    fprintf(stderr, "dynorefine: %s\n", dynorefine_last_error(r));
+    dynorefine_destroy(r);
+    return 1;
+  }
+  b.ternary_inactive = mask;
+  if (dynorefine_run(r, &b, &rp, &lm, Hb, ob, &rb) != DYNOHIP_OK) {
+    fprintf(stderr, "dynorefine (mask): %s\n", dynorefine_last_error(r));
+    dynorefine_destroy(r);
+    return 1;
+  }
+  for (k = 0; k < 12; ++k) bad += !isfinite(Ha[k]) || Ha[k] != Hb[k];
+  for (i = 0; i < NT; ++i) bad += oa[i] != ob[i];
+  bad += ra.iterations != rb.iterations || ra.inner_iterations != rb.inner_iterations || ra.status != rb.status;
+  bad += !(ra.error_after <= ra.error_before);
+  if (bad) fprintf(stderr, "dynorefine: masked/unmasked mismatch (%d)\n", bad);
+  dynorefine_destroy(r);
+  return bad;
 }
 
 static int gpu_checks(void) {
@@ -148,6 +217,7 @@ static int gpu_checks(void) {
   EXPECT(sqrt(num / den) < 1e-6, "values rel %.3e", sqrt(num / den));
   EXPECT(fabs(gs.final_error - os.final_error) <= 1e-6 * fabs(os.final_error), "final error %.9g vs %.9g",
          gs.final_error, os.final_error);
+  EXPECT(refine_checks() == 0, "dynorefine batch");
   printf("OK gpu iterations=%d inner=%d rel=%.3e error=%.9g\n", gs.iterations, gs.inner_iterations, sqrt(num / den),
          gs.final_error);
   free(gv);

@@ -32,7 +32,7 @@ def test_dynosynth_exports_every_declared_symbol():
 
 def test_abi_version_and_defaults():
     lib = _native.load("libdynohip.so")
-    assert lib.dynohip_abi_version() == 2
+    assert lib.dynohip_abi_version() == 3
     p = _abi.LMParams()
     lib.dynohip_lm_params_default(C.byref(p))
     d = _abi.LMParams.gtsam_default()

@@ -337,11 +337,16 @@ def test_partitioned_lm_matches_single_gpu(tmp_path, nranks):
 def test_partitioned_c5_two_ranks(tmp_path):
     """configs[4] (C5: 2000 frames, 20 objects, 500k landmarks) split over 2
     ranks sharing the GPU: per-iteration conditioned parity with the
-    single-handle solve at 1e-6 over the first outer iterations, and a
-    free-running solve with the same iteration counts and accept sequence."""
-    res, r = _run_partition_check(tmp_path, "C5", 2, extra=("--conditioned", "6"), timeout=420)
+    single-handle solve at 1e-6 over the first outer iterations, the first
+    two of them also against the CPU oracle (same inner iterations and
+    accepts, values within 1e-6), and a free-running solve with the same
+    iteration counts and accept sequence."""
+    res, r = _run_partition_check(tmp_path, "C5", 2, extra=("--conditioned", "6", "--oracle", "2"), timeout=420)
     assert r.returncode == 0 and res["ok"], json_tail(res, r)
     assert res["conditioned"]["values_rel_max"] < 1e-6
+    assert res["conditioned"]["oracle_iterations"] == 2
+    assert res["conditioned"]["oracle_same_inner_and_accepts"]
+    assert res["conditioned"]["oracle_values_rel_max"] < 1e-6
     f = res["free"]
     assert f["iterations"][0] == f["iterations"][1] and f["same_accept_sequence"]
 

@@ -54,6 +54,10 @@ def main():
     ap.add_argument("--control-leaf", type=int, default=2,
                     help="nested-dissection leaf size of the control handle's tile ordering")
     ap.add_argument("--no-free", action="store_true", help="skip the free-running comparison")
+    ap.add_argument("--oracle", type=int, default=0,
+                    help="also run the CPU oracle (tests/oracle_binding, test infrastructure) on rank 0 for the "
+                         "first N conditioned iterations and compare the partitioned values with it")
+    ap.add_argument("--oracle-threads", type=int, default=16)
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     import torch
@@ -84,7 +88,15 @@ def main():
     part.set_values(values)
     t1 = time.perf_counter()
     res = {"config": args.config, "ranks": world, "backend": args.backend, "s_setup": t1 - t0}
-    ref = ctrl = None
+    ref = ctrl = orc = None
+    if rank == 0 and args.oracle > 0:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from oracle_binding import Oracle   # the checker
+        try:
+            nthr = len(os.sched_getaffinity(0))
+        except AttributeError:
+            nthr = os.cpu_count() or 1
+        orc = Oracle(graph, values, threads=max(1, min(args.oracle_threads, nthr)))
     if rank == 0:
         ref = Solver(dev)
         ref.set_graph(graph)
@@ -165,6 +177,18 @@ def main():
                     outs[name] = (s, h.values_data())
                 sr, rv = outs["single"]
                 sc, cv = outs["control"]
+                if orc is not None and it < args.oracle:
+                    orc.set_values_data(v_it.data)
+                    orc.reset(lm_params(lam))
+                    so = orc.iterate()
+                    ov = orc.values_data()
+                    row.update({"oracle_inner": so.inner_iterations, "oracle_accepted": so.iterations,
+                                "oracle_error": so.final_error, "oracle_values_rel": rel(pv, ov),
+                                "single_oracle_values_rel": rel(rv, ov),
+                                "oracle_error_rel": abs(sp.final_error - so.final_error) /
+                                max(abs(so.final_error), 1e-300),
+                                "oracle_same_inner_and_accepts": so.inner_iterations == sp.inner_iterations and
+                                so.iterations == sp.iterations})
                 step = np.linalg.norm(rv - v_it.data)
                 row.update({
                     "inner": [sp.inner_iterations, sr.inner_iterations, sc.inner_iterations],
@@ -190,13 +214,20 @@ def main():
             vmax = max((r["values_rel"] for r in rows), default=0.0)
             cmax = max((r["control_values_rel"] for r in rows), default=0.0)
             same = all(r["inner"][0] == r["inner"][1] and r["accepted"][0] == r["accepted"][1] for r in rows)
-            ok_cond = same and vmax < args.tol
+            orows = [r for r in rows if "oracle_values_rel" in r]
+            omax = max((r["oracle_values_rel"] for r in orows), default=0.0)
+            osame = all(r["oracle_same_inner_and_accepts"] for r in orows)
+            ok_cond = same and vmax < args.tol and (not orows or (osame and omax < args.tol))
             res["conditioned"] = {"iterations": len(rows), "values_rel_max": vmax,
                                   "control_values_rel_max": cmax,
                                   "step_rel_max": max((r["step_rel"] for r in rows), default=0.0),
                                   "control_step_rel_max": max((r["control_step_rel"] for r in rows), default=0.0),
                                   "error_rel_max": max((r["error_rel"] for r in rows), default=0.0),
-                                  "same_inner_and_accepts": same, "rows": rows}
+                                  "same_inner_and_accepts": same,
+                                  "oracle_iterations": len(orows), "oracle_values_rel_max": omax,
+                                  "oracle_same_inner_and_accepts": osame,
+                                  "oracle_error_rel_max": max((r["oracle_error_rel"] for r in orows), default=0.0),
+                                  "rows": rows}
     owner, xdoubles = part.value_owner()
     st = part.stats()
     counts = [None] * world
