@@ -84,6 +84,8 @@ def _declare(name, lib):
         lib.dynohip_get_trace.restype = C.c_int
         lib.dynohip_solve_delta.argtypes = [vp, C.c_double, P(C.c_double), C.c_size_t, P(C.c_int)]
         lib.dynohip_solve_delta.restype = C.c_int
+        lib.dynohip_pool_trim.argtypes = []
+        lib.dynohip_pool_trim.restype = C.c_int
         lib.dynohip_linearize.argtypes = [vp, P(C.c_double), C.c_size_t]
         lib.dynohip_linearize.restype = C.c_int
         lib.dynohip_linearize_size.argtypes = [vp]

@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <algorithm>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -28,18 +29,112 @@ using namespace dynohip;
 
 namespace {
 
+// Process-wide cache of device allocations, per device. A destroyed handle
+// (or a buffer that grows) gives its allocations back here instead of calling
+// hipFree (a device-wide synchronising call, ~0.2 ms each, 12 ms for a whole
+// C2 handle), and the next allocation of a similar size takes one back: the
+// reference constructs a fresh LevenbergMarquardtOptimizer per call
+// (RGBDBackendModule.cc:207,364), and a fresh handle per call then costs no
+// device allocation at all after the first. Held bytes are capped
+// (DYNOHIP_POOL_MAX_MB, default 16384); dynohip_pool_trim() frees them.
+class DevPool {
+ public:
+  static DevPool& get() {
+    static DevPool* p = new DevPool();   // never destroyed (process exit releases the device)
+    return *p;
+  }
+  // a cached block of `bytes` <= size <= 2 * bytes on `dev`, or nullptr
+  void* take(int dev, size_t bytes, size_t* got) {
+    std::lock_guard<std::mutex> lk(mu_);
+    size_t best = SIZE_MAX;
+    size_t bi = 0;
+    for (size_t i = 0; i < free_.size(); ++i) {
+      const Blk& b = free_[i];
+      if (b.dev == dev && b.bytes >= bytes && b.bytes <= 2 * bytes + 4096 && b.bytes < best) {
+        best = b.bytes;
+        bi = i;
+      }
+    }
+    if (best == SIZE_MAX) return nullptr;
+    void* p = free_[bi].p;
+    *got = free_[bi].bytes;
+    held_ -= free_[bi].bytes;
+    free_[bi] = free_.back();
+    free_.pop_back();
+    return p;
+  }
+  void give(int dev, void* p, size_t bytes) {
+    if (!p) return;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (held_ + bytes <= max_bytes_) {
+        free_.push_back({p, bytes, dev});
+        held_ += bytes;
+        return;
+      }
+    }
+    (void)hipFree(p);
+  }
+  size_t trim() {
+    std::vector<Blk> all;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      all.swap(free_);
+      held_ = 0;
+    }
+    size_t n = 0;
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    for (const Blk& b : all) {
+      (void)hipSetDevice(b.dev);
+      (void)hipFree(b.p);
+      n += b.bytes;
+    }
+    (void)hipSetDevice(cur);
+    return n;
+  }
+
+ private:
+  DevPool() {
+    const char* e = std::getenv("DYNOHIP_POOL_MAX_MB");
+    max_bytes_ = (e ? std::strtoull(e, nullptr, 10) : 16384ull) << 20;
+  }
+  struct Blk {
+    void* p;
+    size_t bytes;
+    int dev;
+  };
+  std::mutex mu_;
+  std::vector<Blk> free_;
+  size_t held_ = 0, max_bytes_ = 0;
+};
+
 // Device buffer that keeps its allocation: a handle re-planned for another
 // graph (the next sliding window, the next full-batch call) reuses it when it
-// is large enough, so only growth pays hipMalloc/hipFree (a device-wide
-// synchronising call). Contents are not preserved across alloc().
+// is large enough; otherwise, and when the handle is destroyed, the
+// allocation goes back to the process-wide DevPool. Contents are not
+// preserved across alloc().
 template <typename T>
 struct DevBuf {
   T* p = nullptr;
   size_t n = 0;
   size_t cap = 0;
+  int dev = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;              // one owner per allocation
+  DevBuf& operator=(const DevBuf&) = delete;
   ~DevBuf() { release(); }
+  // exchange allocations with another buffer (the LM's accepted step swaps
+  // current and candidate values): every field, since pooled blocks of one
+  // count can differ in capacity
+  void swap(DevBuf& o) {
+    std::swap(p, o.p);
+    std::swap(n, o.n);
+    std::swap(cap, o.cap);
+    std::swap(dev, o.dev);
+  }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p) DevPool::get().give(dev, p, cap * sizeof(T));
     p = nullptr;
     n = cap = 0;
   }
@@ -49,7 +144,15 @@ struct DevBuf {
       return hipSuccess;
     }
     release();
+    (void)hipGetDevice(&dev);
     const size_t c = count + count / 8;   // some headroom for the next graph
+    size_t got = 0;
+    if (void* q = DevPool::get().take(dev, count * sizeof(T), &got)) {
+      p = static_cast<T*>(q);
+      n = count;
+      cap = got / sizeof(T);
+      return hipSuccess;
+    }
     const hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), c * sizeof(T));
     if (e != hipSuccess) {
       p = nullptr;
@@ -65,6 +168,43 @@ struct DevBuf {
     if (e != hipSuccess || v.empty()) return e;
     return hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s);
   }
+};
+
+// Streams, events and the pinned result buffer of a handle, recycled the
+// same way (creating them cost ~5 ms per handle).
+struct HandleRes {
+  int device = 0;
+  hipStream_t stream = nullptr, side = nullptr;
+  hipEvent_t ev_main = nullptr, ev_side = nullptr, ev_res = nullptr;
+  hipEvent_t ev[9] = {};
+  double* hres = nullptr;
+};
+
+class ResPool {
+ public:
+  static ResPool& get() {
+    static ResPool* p = new ResPool();
+    return *p;
+  }
+  bool take(int dev, HandleRes* out) {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (size_t i = 0; i < free_.size(); ++i)
+      if (free_[i].device == dev) {
+        *out = free_[i];
+        free_[i] = free_.back();
+        free_.pop_back();
+        return true;
+      }
+    return false;
+  }
+  void give(const HandleRes& r) {
+    std::lock_guard<std::mutex> lk(mu_);
+    free_.push_back(r);
+  }
+
+ private:
+  std::mutex mu_;
+  std::vector<HandleRes> free_;
 };
 
 struct GraphCopy {
@@ -714,8 +854,8 @@ int lm_iterate(dynohip_solver* s) {
     te.stop = stop;
     push_trace(s, te);
     if (step_ok) {
-      std::swap(s->pose.p, s->pose_c.p);
-      std::swap(s->pt.p, s->pt_c.p);
+      s->pose.swap(s->pose_c);
+      s->pt.swap(s->pt_c);
       if (speculate) s->lin_valid = true;
       s->error = newError;
       s->lambda /= s->prm.lambda_factor;
@@ -782,21 +922,37 @@ int dynohip_create(int device_id, dynohip_solver** out) {
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return DYNOHIP_EHIP;
   if (device_id < 0 || device_id >= ndev) return DYNOHIP_EINVAL;
   if (hipSetDevice(device_id) != hipSuccess) return DYNOHIP_EHIP;
+  HandleRes r;
+  if (!ResPool::get().take(device_id, &r)) {
+    r.device = device_id;
+    bool ok = hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&r.side, hipStreamNonBlocking) == hipSuccess &&
+              hipEventCreateWithFlags(&r.ev_main, hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&r.ev_side, hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&r.ev_res, hipEventDisableTiming) == hipSuccess &&
+              hipHostMalloc(reinterpret_cast<void**>(&r.hres), 8 * sizeof(double), hipHostMallocDefault) == hipSuccess;
+    for (auto& e : r.ev) ok = ok && hipEventCreate(&e) == hipSuccess;
+    if (!ok) {
+      for (auto& e : r.ev)
+        if (e) (void)hipEventDestroy(e);
+      if (r.ev_res) (void)hipEventDestroy(r.ev_res);
+      if (r.ev_main) (void)hipEventDestroy(r.ev_main);
+      if (r.ev_side) (void)hipEventDestroy(r.ev_side);
+      if (r.hres) (void)hipHostFree(r.hres);
+      if (r.side) (void)hipStreamDestroy(r.side);
+      if (r.stream) (void)hipStreamDestroy(r.stream);
+      return DYNOHIP_EHIP;
+    }
+  }
   dynohip_solver* s = new dynohip_solver();
   s->device = device_id;
-  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking) != hipSuccess) {
-    delete s;
-    return DYNOHIP_EHIP;
-  }
-  (void)hipEventCreateWithFlags(&s->ev_main, hipEventDisableTiming);
-  (void)hipEventCreateWithFlags(&s->ev_side, hipEventDisableTiming);
-  for (auto& e : s->ev) (void)hipEventCreate(&e);
-  if (hipEventCreateWithFlags(&s->ev_res, hipEventDisableTiming) != hipSuccess ||
-      hipHostMalloc(reinterpret_cast<void**>(&s->hres), 8 * sizeof(double), hipHostMallocDefault) != hipSuccess) {
-    dynohip_destroy(s);
-    return DYNOHIP_EHIP;
-  }
+  s->stream = r.stream;
+  s->side = r.side;
+  s->ev_main = r.ev_main;
+  s->ev_side = r.ev_side;
+  s->ev_res = r.ev_res;
+  for (int k = 0; k < 9; ++k) s->ev[k] = r.ev[k];
+  s->hres = r.hres;
   // the dataflow factorisation keeps one 158 KB-LDS workgroup per CU
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_id) == hipSuccess && cus > 0)
@@ -806,20 +962,30 @@ int dynohip_create(int device_id, dynohip_solver** out) {
   return DYNOHIP_OK;
 }
 
+// The handle's streams, events and pinned buffer go back to ResPool and its
+// device buffers to DevPool (see DevPool): destroying a handle frees nothing
+// and synchronises only its own streams.
 void dynohip_destroy(dynohip_solver* s) {
   if (!s) return;
   (void)hipSetDevice(s->device);
   if (s->stream) (void)hipStreamSynchronize(s->stream);
-  for (auto& e : s->ev)
-    if (e) (void)hipEventDestroy(e);
   if (s->side) (void)hipStreamSynchronize(s->side);
-  if (s->ev_res) (void)hipEventDestroy(s->ev_res);
-  if (s->hres) (void)hipHostFree(s->hres);
-  if (s->ev_main) (void)hipEventDestroy(s->ev_main);
-  if (s->ev_side) (void)hipEventDestroy(s->ev_side);
-  if (s->side) (void)hipStreamDestroy(s->side);
-  if (s->stream) (void)hipStreamDestroy(s->stream);
+  HandleRes r;
+  r.device = s->device;
+  r.stream = s->stream;
+  r.side = s->side;
+  r.ev_main = s->ev_main;
+  r.ev_side = s->ev_side;
+  r.ev_res = s->ev_res;
+  for (int k = 0; k < 9; ++k) r.ev[k] = s->ev[k];
+  r.hres = s->hres;
+  if (r.stream) ResPool::get().give(r);
   delete s;
+}
+
+int dynohip_pool_trim(void) {
+  const size_t n = DevPool::get().trim();
+  return static_cast<int>(std::min<size_t>(n >> 20, 0x7fffffff));
 }
 
 const char* dynohip_last_error(const dynohip_solver* s) { return s ? s->err.c_str() : "null handle"; }

@@ -454,12 +454,18 @@ __device__ __forceinline__ void load_tiles_lds(const double* s0, double* d0, con
 // dst -= sum over the task's pairs of A B^T: the destination and the first
 // pair's operands are fetched in one round trip; further pairs (rare) one
 // by one
-template <bool SC1>
+struct NoWait {
+  __device__ void operator()() const {}
+};
+
+template <bool SC1, class LateWait = NoWait>
 // pa0 / pb0: the first pair's slots when the caller fetched them before the
-// dependency wait (-1: read them here)
+// dependency wait (-1: read them here). late(): called between the
+// destination loads and the operand loads (the dataflow kernel waits there
+// for the operand tiles, whose producers usually finish last)
 __device__ __forceinline__ void run_update(const TileDev& b, const TileTask& tk, const int32_t* __restrict__ pairs,
                                            double* Qs, double* Rs, int tid, int w, int l, int32_t pa0 = -1,
-                                           int32_t pb0 = -1) {
+                                           int32_t pb0 = -1, LateWait&& late = LateWait()) {
   double* dst = slot_ptr(b, tk.dst);
   double old[2][2][4];
 #pragma unroll
@@ -468,6 +474,7 @@ __device__ __forceinline__ void run_update(const TileDev& b, const TileTask& tk,
     for (int tj = 0; tj < 2; ++tj)
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) old[ti][tj][rr] = gld<SC1>(dst + MFMA_ROW(w, l, ti, rr) * T + MFMA_COL(w, l, tj));
+  late();
   v4d acc[2][2];
   zero_acc(acc);
   for (int e = tk.po_beg; e < tk.po_end; ++e) {
@@ -721,10 +728,11 @@ __device__ __forceinline__ bool factor_own(v4d (&accA)[4], v4d (&XT)[4], int w, 
   }
 }
 
-template <bool SC1>
+template <bool SC1, class LateWait = NoWait>
 __device__ __forceinline__ void panel_task(const TileDev& b, const TileTask& tk, const int32_t* __restrict__ pairs,
                                            const PanelPre& p, double* __restrict__ Linv, double* __restrict__ contrib,
-                                           double* __restrict__ y, int* fail, TaskLds& S, int q = 0) {
+                                           double* __restrict__ y, int* fail, TaskLds& S, int q = 0,
+                                           LateWait&& late = LateWait()) {
   double* const Ps = S.Ps;
   double* const Qs = S.Qs;
   double* const As = S.As;
@@ -732,9 +740,12 @@ __device__ __forceinline__ void panel_task(const TileDev& b, const TileTask& tk,
   const int w = tid >> 6, l = tid & 63;
   const int li = l & 15, lk = l >> 4;
   const bool own = tk.i != tk.k;
-  // (1) one round trip: the diagonal tile (stored symmetric) into registers,
-  // the right-hand side contributions L(k,c) y_c of eliminated columns, and
-  // the operand tiles into LDS
+  // (1) two round trips: first what the dependency-ready tiles hold (the
+  // diagonal tile, stored symmetric, into registers, and the own tile into
+  // LDS), issued before the wait for the pending operands (late(): in the
+  // dataflow kernel the tiles the previous task on the critical path just
+  // produced), then those operand tiles into LDS and the right-hand side
+  // contributions L(k,c) y_c of eliminated columns
   v4d accA[4];
   const double* diag = slot_ptr(b, tk.diag);
 #pragma unroll
@@ -744,12 +755,15 @@ __device__ __forceinline__ void panel_task(const TileDev& b, const TileTask& tk,
       const int row = ACC_ROW(w, l, rr), col = ACC_COL(TJ, l);
       accA[TJ][rr] = TJ >= w ? gld<SC1>(diag + row * T + col) : 0.0;
     }
+  if (p.fast && own)
+    load_tiles_lds<SC1>(nullptr, Ps, slot_ptr(b, tk.dst), As, nullptr, Qs, nullptr, nullptr, tid);
+  late();
   double cv[kCsMax];
 #pragma unroll
   for (int j = 0; j < kCsMax; ++j)
     cv[j] = p.cs[j] >= 0 ? gld<SC1>(contrib + static_cast<int64_t>(p.cs[j]) * T + l) : 0.0;
   if (p.fast) {
-    load_tiles_lds<SC1>(p.pd >= 0 ? slot_ptr(b, p.pd) : nullptr, Ps, own ? slot_ptr(b, tk.dst) : nullptr, As,
+    load_tiles_lds<SC1>(p.pd >= 0 ? slot_ptr(b, p.pd) : nullptr, Ps, nullptr, As,
                         p.qa >= 0 ? slot_ptr(b, p.qa) : nullptr, Qs, nullptr, nullptr, tid);
   }
   {
@@ -968,10 +982,30 @@ __global__ __launch_bounds__(256) void k_factor_persist(TileDev b, const TileTas
       upa = pairs[2 * tk.po_beg];
       upb = pairs[2 * tk.po_beg + 1];
     }
-    if (w == 0) {
+    // Dependencies in two classes: the pending operand tiles (a panel's
+    // pending pairs, an update's first pair), whose producers are usually
+    // the last to finish, and the rest. The task loads what the rest guards
+    // while wave 0 still waits for the operands (late()).
+    int32_t o0 = -1, o1 = -1, o2 = -1;
+    if (tk.kind == 0) {
+      if (p.fast) {
+        o0 = p.pd;
+        o1 = p.qa;
+        o2 = p.rb;
+      }
+    } else {
+      o0 = upa;
+      o1 = upb;
+    }
+    const bool split = o0 >= 0 || o1 >= 0;
+    auto wait_deps = [&](int cls) {   // cls 0: not an operand slot, 1: an operand slot, 2: all
+      if (w != 0) return;
       bool ok = true;
       for (int j = dep_start[q] + l; j < dep_start[q + 1]; j += 64) {
-        const unsigned* c = wcnt + dep[2 * j];
+        const int32_t sl = dep[2 * j];
+        const int c1 = (sl == o0 || sl == o1 || sl == o2) ? 1 : 0;
+        if (cls != 2 && c1 != cls) continue;
+        const unsigned* c = wcnt + sl;
         const unsigned need = static_cast<unsigned>(dep[2 * j + 1]);
         int spins = 0;
         while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
@@ -980,11 +1014,18 @@ __global__ __launch_bounds__(256) void k_factor_persist(TileDev b, const TileTas
         }
       }
       if (!ok) atomicOr(fail, 4);
-    }
+    };
+    wait_deps(split ? 0 : 2);
     __syncthreads();
     TCLK(1, q, rtc());
-    if (tk.kind == 1) run_update<true>(b, tk, pairs, S.Qs, S.Ps, tid, w, l, upa, upb);
-    else panel_task<true>(b, tk, pairs, p, Linv, contrib, y, fail, S, q);
+    auto late = [&]() {
+      if (split) {
+        wait_deps(1);
+        __syncthreads();
+      }
+    };
+    if (tk.kind == 1) run_update<true>(b, tk, pairs, S.Qs, S.Ps, tid, w, l, upa, upb, late);
+    else panel_task<true>(b, tk, pairs, p, Linv, contrib, y, fail, S, q, late);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     TCLK(4, q, rtc());

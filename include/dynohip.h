@@ -154,7 +154,15 @@ int dynohip_abi_version(void);
 void dynohip_lm_params_default(dynohip_lm_params* p);
 
 int dynohip_create(int device_id, dynohip_solver** out);
+/* Destroying a handle returns its device buffers, streams and events to a
+   process-wide cache that the next dynohip_create / plan on the same device
+   reuses (the reference constructs a fresh optimiser per call,
+   RGBDBackendModule.cc:207,364): after the first, a fresh handle per call
+   allocates nothing. Cached device bytes are capped by the environment
+   variable DYNOHIP_POOL_MAX_MB (default 16384). */
 void dynohip_destroy(dynohip_solver* s);
+/* Frees every cached device buffer (not the streams); returns the MiB freed. */
+int dynohip_pool_trim(void);
 const char* dynohip_last_error(const dynohip_solver* s);
 
 /* Upload the graph (structure + measurements). Builds all index structures
