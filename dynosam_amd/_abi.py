@@ -22,8 +22,8 @@ FACTOR_SLOTS = ((0, 1), (1, 1, 0), (0, 0), (0,), (1, 1, 0, 0), (0, 0, 0))
 POSE3 = 0
 POINT3 = 1
 
-# dynohip_allreduce_fn(void* ctx, double* buf, size_t n, int on_device)
-ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.c_size_t, C.c_int)
+# dynohip_allreduce_fn(void* ctx, double* buf, size_t n, int on_device, void* stream)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.c_size_t, C.c_int, C.c_void_p)
 
 
 class FactorBlock(C.Structure):

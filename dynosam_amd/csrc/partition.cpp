@@ -59,8 +59,11 @@ int build_partitioned_plan(const dynohip_graph_view& g, const uint64_t* keys, co
     err = "partitioned solve needs a power-of-two rank count >= 2 and 0 <= rank < nranks";
     return DYNOHIP_EINVAL;
   }
+  // the global graph's structure (point chains, reduced system, the
+  // partitioned tile schedule) without its gather lists: this rank's own
+  // plan below builds those for its share only
   Plan G;
-  int rc = build_plan(g, keys, kind, n, G, err, nranks, rank, true);
+  int rc = build_plan(g, keys, kind, n, G, err, nranks, rank, true, true);
   if (rc) return rc;
   part = Partition();
   part.nranks = nranks;

@@ -263,7 +263,7 @@ void compute_red_slots(Plan& P) {
 }
 
 int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t* kind, size_t n, Plan& P,
-               std::string& err, int nranks, int rank, bool with_schedule) {
+               std::string& err, int nranks, int rank, bool with_schedule, bool structure_only) {
   double tmark = plan_now();
   P = Plan();
   P.nranks = nranks;
@@ -613,14 +613,14 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
   if (arena >= (1ull << 32)) { err = "graph too large for 32-bit arena offsets"; return DYNOHIP_ESTRUCT; }
 
   plan_mark("before point-side gathers", tmark);
+  std::vector<uint8_t> lone_grouped(P.n_pt, 0);   // per point: in a lone-point group
   // ---- point-side gathers (CSR builds run on worker threads) ----
   // Point-slot references (type, factor, slot) in enumeration order
   // (type-major, then factor, then slot), stably sorted by point: a worker
   // owning a point range walks only its points' references, and every
   // target still lists its entries in factor order.
   bool chain_ok = true;
-  std::vector<uint8_t> lone_grouped(P.n_pt, 0);   // per point: in a lone-point group
-  {
+  if (!structure_only) {
     std::vector<int64_t> rstart(static_cast<size_t>(P.n_pt) + 1, 0);
     for (int t = 0; t < kNTypes; ++t) {
       const TypePlan& tp = P.types[t];
@@ -990,6 +990,7 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
     // per worker, the B range of its targets: a component whose neighbour
     // poses (sorted) miss it emits nothing there and is skipped whole
     const std::vector<int64_t> rcut = even_cuts(static_cast<int64_t>(P.red_A.size()));
+    if (!structure_only) {
     csr_target_ranges(P.red_A.size(), rcut,
                       [&](int r, auto&& fn) {
                         if (rcut[r + 1] <= rcut[r]) return;
@@ -1008,6 +1009,7 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
                       P.gRed);
     const std::vector<int64_t> gcut = even_cuts(P.n_pose);
     csr_target_ranges(P.n_pose, gcut, [&](int r, auto&& fn) { emit_grad(fn, gcut[r], gcut[r + 1]); }, P.gGred);
+    }
   }
   plan_mark("reduced system targets", tmark);
 
@@ -1034,7 +1036,7 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
     return DYNOHIP_ESTRUCT;
   }
   plan_mark("tile schedule", tmark);
-  if (with_schedule) compute_red_slots(P);
+  if (with_schedule && !structure_only) compute_red_slots(P);
   plan_mark("reduced target slots", tmark);
   return DYNOHIP_OK;
 }

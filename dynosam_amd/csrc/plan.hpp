@@ -239,8 +239,12 @@ void compute_red_slots(Plan& P);
 // returns DYNOHIP_OK or an error code with `err` filled. nranks > 1 builds
 // the partitioned tile schedule of `rank` (the graph is the global one);
 // with_schedule = false stops after the reduced-system structure.
+// structure_only = true builds no gather lists and no lone-point groups:
+// the point chains, the reduced system's pose-pair blocks and (with
+// with_schedule) the tile schedule only, which is all the partitioned plan
+// needs of the global graph.
 int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t* kind, size_t n, Plan& plan,
-               std::string& err, int nranks = 1, int rank = 0, bool with_schedule = true);
+               std::string& err, int nranks = 1, int rank = 0, bool with_schedule = true, bool structure_only = false);
 
 // Partitioned full-batch solve: what one rank holds (partition.cpp).
 struct Partition {

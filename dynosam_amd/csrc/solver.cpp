@@ -554,7 +554,7 @@ int upload_partition(dynohip_solver* s) {
 // sum over ranks (partitioned); no-op on an ordinary handle
 int comm_sum(dynohip_solver* s, double* buf, size_t n, int on_device) {
   if (s->nranks <= 1 || n == 0) return 0;
-  if (!s->comm || s->comm(s->comm_ctx, buf, n, on_device) != 0)
+  if (!s->comm || s->comm(s->comm_ctx, buf, n, on_device, static_cast<void*>(s->stream)) != 0)
     return set_err(s, DYNOHIP_EHIP, "partition exchange (all-reduce of %zu doubles) failed", n);
   return 0;
 }
@@ -644,9 +644,9 @@ int enqueue_try(dynohip_solver* s, double lambda) {
     launch_tile_forward(s->bd, s->sd, P.flevel, P.fpanels, s->linv.p, s->gred.p, s->contrib.p, y, s->failp, st,
                         s->side, s->ev_main, s->ev_side);
     launch_sep_rhs(s->n_seprhs, s->seprhs_tile.p, s->seprhs_start.p, s->seprhs_slot.p, s->gred.p, s->contrib.p, st);
-    // exchange: the separator system summed over ranks
+    // exchange: the separator system summed over ranks, ordered on the
+    // solver's stream by the callback (no host synchronisation here)
     if (sep_copy(s, true)) return DYNOHIP_EHIP;
-    HIPCHK(s, hipStreamSynchronize(st));
     int rc = comm_sum(s, s->xbuf.p, s->xbuf.n, 1);
     if (rc) return rc;
     if (sep_copy(s, false)) return DYNOHIP_EHIP;

@@ -25,6 +25,9 @@
 // level. The leaf size is picked by a small cost model of the launch
 // sequence.
 #include <algorithm>
+#include <chrono>
+#include <climits>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -131,6 +134,13 @@ void schedule(int NT, const std::vector<std::vector<int32_t>>& adj, const std::v
   }
   S.pos.assign(NT, 0);
   for (int p = 0; p < NT; ++p) S.pos[S.order[p]] = p;
+  auto tm0 = std::chrono::steady_clock::now();
+  auto tmark = [&](const char* what) {
+    static const bool on = std::getenv("DYNOHIP_SCHED_TIMING") != nullptr;
+    const auto t = std::chrono::steady_clock::now();
+    if (on) std::fprintf(stderr, "  [sched leaf %d] %-24s %8.2f ms\n", leaf, what, std::chrono::duration<double, std::milli>(t - tm0).count());
+    tm0 = t;
+  };
   // ---- symbolic factorisation (elimination tree merge) in position space
   S.st.assign(NT, {});
   for (int cp = 0; cp < NT; ++cp) {
@@ -157,6 +167,7 @@ void schedule(int NT, const std::vector<std::vector<int32_t>>& adj, const std::v
     ns += static_cast<int32_t>(S.st[cp].size());
   }
   S.n_slots = ns;
+  tmark("symbolic");
   // ---- tasks with levels (1-based; 0 = available at start). Every stored
   // tile collects its update contributions (column c, ready level R_c).
   // Contributions ready one level before the tile's panel are applied by
@@ -168,48 +179,75 @@ void schedule(int NT, const std::vector<std::vector<int32_t>>& adj, const std::v
     int32_t R, a, b;  // ready level, operand slots (A B^T)
     int32_t own;      // owner of the source column
   };
-  std::vector<std::vector<Contrib>> contrib(ns);
+  // every slot's contributions in generation (column) order, as a linked
+  // list over one pool (no per-slot allocation), and the largest ready level
+  struct CNode {
+    Contrib c;
+    int32_t next;
+  };
+  std::vector<CNode> cpool;
+  std::vector<int32_t> chead(ns, -1), ctail(ns, -1), cmaxR(ns, 0);
+  auto add_contrib = [&](int32_t sl, const Contrib& c) {
+    const int32_t id = static_cast<int32_t>(cpool.size());
+    cpool.push_back({c, -1});
+    if (ctail[sl] < 0) chead[sl] = id;
+    else cpool[ctail[sl]].next = id;
+    ctail[sl] = id;
+    cmaxR[sl] = std::max(cmaxR[sl], c.R);
+  };
   std::vector<int32_t> lvlP(ns, 0);
+  // a task; its operand pairs are ranges of one pool (a column's panels
+  // share their diagonal tile's pending pairs)
   struct LT {
     int32_t lvl;
     TileTask t;
-    std::vector<int32_t> pd, po;  // pairs
-    int32_t own = 0;              // rank running the task (-1: after the exchange)
+    int32_t pd_off, pd_n, po_off, po_n;  // pairs [off, off + n) of ppool (in pairs)
+    int32_t own;                          // rank running the task (-1: after the exchange)
   };
   std::vector<LT> tasks;
+  std::vector<int32_t> ppool;   // 2 ints per pair
   const double T3 = static_cast<double>(kTile) * kTile * kTile;
   double flops = 0.0;
+  std::vector<Contrib> all, cs, mine;
+  std::vector<int32_t> owners;
+  auto pool_pairs = [&]() { return static_cast<int32_t>(ppool.size() / 2); };
   // split contributions (sorted by R) into update tasks finishing before
-  // level P and the pairs the panel at level P absorbs
+  // level P and the pairs the panel at level P absorbs (appended to ppool
+  // last: [*aoff, *aoff + *an))
   // Partitioned: a separator tile (target owner -1) takes the contributions
   // of interior columns as update tasks of their rank, never absorbed by its
   // panel, so that the tile leaves phase 0 as that rank's partial Schur
   // complement.
-  auto plan_tile = [&](int32_t sl, int32_t P, std::vector<int32_t>& absorbed, int32_t town) {
-    auto& all = contrib[sl];
+  auto plan_tile = [&](int32_t sl, int32_t P, int32_t* aoff, int32_t* an, int32_t town) {
+    all.clear();
+    for (int32_t id = chead[sl]; id >= 0; id = cpool[id].next) all.push_back(cpool[id].c);
     std::sort(all.begin(), all.end(), [](const Contrib& x, const Contrib& y) { return x.R < y.R; });
-    std::vector<Contrib> cs;
+    auto emit_updates = [&](const std::vector<Contrib>& v, size_t& q, int32_t limitR, int32_t own) {
+      while (q < v.size() && v[q].R <= limitR) {
+        const int32_t t = v[q].R + 1;
+        LT u{t, TileTask{1, -1, -1, sl, -1, 0, 0, 0, 0, 0}, 0, 0, pool_pairs(), 0, own};
+        while (q < v.size() && v[q].R <= t - 1) {
+          ppool.push_back(v[q].a);
+          ppool.push_back(v[q].b);
+          ++q;
+        }
+        u.po_n = pool_pairs() - u.po_off;
+        tasks.push_back(u);
+      }
+    };
+    cs.clear();
     if (town < 0) {
-      std::vector<int32_t> owners;
+      owners.clear();
       for (const Contrib& c : all)
         if (c.own >= 0) owners.push_back(c.own);
       std::sort(owners.begin(), owners.end());
       owners.erase(std::unique(owners.begin(), owners.end()), owners.end());
       for (int32_t o : owners) {
         size_t q = 0;
-        std::vector<Contrib> mine;
+        mine.clear();
         for (const Contrib& c : all)
           if (c.own == o) mine.push_back(c);
-        while (q < mine.size()) {
-          const int32_t t = mine[q].R + 1;
-          LT u{t, TileTask{1, -1, -1, sl, -1, 0, 0, 0, 0, 0}, {}, {}, o};
-          while (q < mine.size() && mine[q].R <= t - 1) {
-            u.po.push_back(mine[q].a);
-            u.po.push_back(mine[q].b);
-            ++q;
-          }
-          tasks.push_back(std::move(u));
-        }
+        emit_updates(mine, q, INT32_MAX, o);
       }
       for (const Contrib& c : all)
         if (c.own < 0) cs.push_back(c);
@@ -217,74 +255,75 @@ void schedule(int NT, const std::vector<std::vector<int32_t>>& adj, const std::v
       cs = all;
     }
     size_t q = 0;
-    while (q < cs.size() && cs[q].R <= P - 2) {
-      const int32_t t = cs[q].R + 1;
-      LT u{t, TileTask{1, -1, -1, sl, -1, 0, 0, 0, 0, 0}, {}, {}, town};
-      while (q < cs.size() && cs[q].R <= t - 1) {
-        u.po.push_back(cs[q].a);
-        u.po.push_back(cs[q].b);
-        ++q;
-      }
-      tasks.push_back(std::move(u));
-    }
+    emit_updates(cs, q, P - 2, town);
+    *aoff = pool_pairs();
     for (; q < cs.size(); ++q) {
-      absorbed.push_back(cs[q].a);
-      absorbed.push_back(cs[q].b);
+      ppool.push_back(cs[q].a);
+      ppool.push_back(cs[q].b);
     }
+    *an = pool_pairs() - *aoff;
   };
   for (int cp = 0; cp < NT; ++cp) {
     const auto& s = S.st[cp];
-    const int32_t dslot = S.slot(cp, cp);
-    int32_t Rd = 0;
-    for (const Contrib& c : contrib[dslot]) Rd = std::max(Rd, c.R);
-    const int32_t Pd = Rd + 1;
+    const int32_t dslot = S.slot_base[cp];   // s[0] == cp
+    const int32_t Pd = cmaxR[dslot] + 1;
     const int32_t cown = S.owner[cp];
-    std::vector<int32_t> pd;
-    plan_tile(dslot, Pd, pd, cown);
+    int32_t pd_off = 0, pd_n = 0;
+    plan_tile(dslot, Pd, &pd_off, &pd_n, cown);
     flops += T3 / 3.0;
-    for (int32_t rp : s) {
-      const int32_t sl = S.slot(rp, cp);
-      LT t{Pd, TileTask{0, S.order[cp], S.order[rp], sl, dslot, 0, 0, 0, 0, 0}, pd, {}, cown};
+    for (size_t x = 0; x < s.size(); ++x) {
+      const int32_t rp = s[x];
+      const int32_t sl = S.slot_base[cp] + static_cast<int32_t>(x);
+      LT t{Pd, TileTask{0, S.order[cp], S.order[rp], sl, dslot, 0, 0, 0, 0, 0}, pd_off, pd_n, 0, 0, cown};
       if (rp != cp) {
-        int32_t Ro = 0;
-        for (const Contrib& c : contrib[sl]) Ro = std::max(Ro, c.R);
-        t.lvl = std::max(Pd, Ro + 1);
-        plan_tile(sl, t.lvl, t.po, cown);
+        t.lvl = std::max(Pd, cmaxR[sl] + 1);
+        plan_tile(sl, t.lvl, &t.po_off, &t.po_n, cown);
         flops += T3;
       }
       lvlP[sl] = t.lvl;
-      tasks.push_back(std::move(t));
+      tasks.push_back(t);
     }
-    for (size_t x = 1; x < s.size(); ++x)
+    for (size_t x = 1; x < s.size(); ++x) {
+      const int32_t sa = S.slot_base[cp] + static_cast<int32_t>(x);
       for (size_t y = 1; y <= x; ++y) {
-        const int32_t sa = S.slot(s[x], cp), sb = S.slot(s[y], cp);
-        contrib[S.slot(s[x], s[y])].push_back({std::max(lvlP[sa], lvlP[sb]), sa, sb, cown});
+        const int32_t sb = S.slot_base[cp] + static_cast<int32_t>(y);
+        add_contrib(S.slot(s[x], s[y]), {std::max(lvlP[sa], lvlP[sb]), sa, sb, cown});
         flops += 2.0 * T3;
       }
+    }
   }
   S.flops = flops;
+  tmark("contributions/tasks");
   // by level; within a level panels first, then updates (wide levels run
-  // their updates as a separate, concurrent kernel)
-  std::stable_sort(tasks.begin(), tasks.end(), [](const LT& x, const LT& y) {
-    return x.lvl != y.lvl ? x.lvl < y.lvl : x.t.kind < y.t.kind;
-  });
+  // their updates as a separate, concurrent kernel): a stable counting sort
+  int32_t maxlvl = 0;
+  for (const LT& t : tasks) maxlvl = std::max(maxlvl, t.lvl);
+  std::vector<int32_t> bstart(2 * (static_cast<size_t>(maxlvl) + 1) + 1, 0);
+  for (const LT& t : tasks) bstart[2 * t.lvl + t.t.kind + 1]++;
+  for (size_t k = 1; k < bstart.size(); ++k) bstart[k] += bstart[k - 1];
+  std::vector<int32_t> perm(tasks.size());
+  for (size_t q = 0; q < tasks.size(); ++q) perm[bstart[2 * tasks[q].lvl + tasks[q].t.kind]++] = static_cast<int32_t>(q);
   S.ftask.clear();
   S.flevel.clear();
   S.pairs.clear();
   S.task_owner.clear();
+  S.ftask.reserve(tasks.size());
+  S.task_owner.reserve(tasks.size());
+  S.pairs.reserve(ppool.size());
   int cur = 0;
-  for (LT& t : tasks) {
+  for (int32_t qi : perm) {
+    LT& t = tasks[qi];
     while (cur < t.lvl) {
       S.flevel.push_back(static_cast<int32_t>(S.ftask.size()));
       ++cur;
     }
-    auto put = [&](const std::vector<int32_t>& v, int32_t& beg, int32_t& end) {
+    auto put = [&](int32_t off, int32_t n, int32_t& beg, int32_t& end) {
       beg = static_cast<int32_t>(S.pairs.size() / 2);
-      S.pairs.insert(S.pairs.end(), v.begin(), v.end());
+      S.pairs.insert(S.pairs.end(), ppool.begin() + 2 * off, ppool.begin() + 2 * (off + n));
       end = static_cast<int32_t>(S.pairs.size() / 2);
     };
-    put(t.pd, t.t.pd_beg, t.t.pd_end);
-    put(t.po, t.t.po_beg, t.t.po_end);
+    put(t.pd_off, t.pd_n, t.t.pd_beg, t.t.pd_end);
+    put(t.po_off, t.po_n, t.t.po_beg, t.t.po_end);
     S.ftask.push_back(t.t);
     S.task_owner.push_back(t.own);
   }
@@ -292,6 +331,7 @@ void schedule(int NT, const std::vector<std::vector<int32_t>>& adj, const std::v
   S.fpanels.assign(S.flevel.size() - 1, 0);
   for (size_t l = 0; l + 1 < S.flevel.size(); ++l)
     for (int32_t q = S.flevel[l]; q < S.flevel[l + 1]; ++q) S.fpanels[l] += S.ftask[q].kind == 0;
+  tmark("sort/flatten");
   // ---- backward substitution levels
   std::vector<int32_t> blv(NT, 0);
   int maxb = 0;
@@ -339,6 +379,7 @@ void schedule(int NT, const std::vector<std::vector<int32_t>>& adj, const std::v
   }
   for (size_t l = 0; l + 1 < S.blevel.size(); ++l) cost += 4.0;
   S.cost = cost;
+  tmark("backward/cost");
 }
 
 int g_leaf_override = -1;
@@ -417,6 +458,13 @@ void filter_tasks(const std::vector<TileTask>& all, const std::vector<int32_t>& 
 
 bool build_tile_schedule(Plan& P) {
   const int NT = P.NT;
+  auto bt0 = std::chrono::steady_clock::now();
+  auto bmark = [&](const char* what) {
+    static const bool on = std::getenv("DYNOHIP_SCHED_TIMING") != nullptr;
+    const auto t = std::chrono::steady_clock::now();
+    if (on) std::fprintf(stderr, "  [tiles] %-28s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(t - bt0).count());
+    bt0 = t;
+  };
   std::vector<std::vector<int32_t>> adj(NT);
   std::vector<int32_t> maxnb(NT);
   for (int t = 0; t < NT; ++t) maxnb[t] = t;
@@ -436,26 +484,37 @@ bool build_tile_schedule(Plan& P) {
     v.erase(std::unique(v.begin(), v.end()), v.end());
   }
   const int nr = std::max(1, P.nranks);
+  bmark("adjacency");
   Sched best;
-  schedule(NT, adj, maxnb, g_leaf_override > 0 ? g_leaf_override : 0, best, nr);
-  if (!best.ok) return false;
-  if (g_leaf_override < 0) {
-    // the candidate leaf sizes are independent schedules: built on threads,
-    // then the cheapest kept in list order (the same choice as a serial scan)
-    std::vector<int> leaves;
+  if (g_leaf_override >= 0) {
+    schedule(NT, adj, maxnb, g_leaf_override, best, nr);
+    if (!best.ok) return false;
+  } else {
+    // frame order (leaf 0) and the nested-dissection leaf sizes are
+    // independent schedules: built on threads, then the cheapest kept in
+    // list order, frame order first (the same choice as a serial scan).
+    // Leaves below 16 tiles are not candidates of large systems: the cost
+    // model never picks them there, and their deep dissections are the
+    // costliest schedules to build.
+    std::vector<int> leaves{0};
     for (int leaf : {4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128, 192, 256}) {
       if (leaf * nr >= NT) break;
+      if (NT > 512 && leaf < 16) continue;
       leaves.push_back(leaf);
     }
     std::vector<Sched> cand(leaves.size());
     std::vector<std::thread> th;
     for (size_t c = 1; c < leaves.size(); ++c)
       th.emplace_back([&, c] { schedule(NT, adj, maxnb, leaves[c], cand[c], nr); });
-    if (!leaves.empty()) schedule(NT, adj, maxnb, leaves[0], cand[0], nr);
+    schedule(NT, adj, maxnb, leaves[0], cand[0], nr);
     for (auto& t : th) t.join();
-    for (auto& c : cand)
-      if (c.ok && c.cost < best.cost) best = std::move(c);
+    if (!cand[0].ok) return false;
+    size_t bi = 0;
+    for (size_t c = 1; c < cand.size(); ++c)
+      if (cand[c].ok && cand[c].cost < cand[bi].cost) bi = c;
+    best = std::move(cand[bi]);
   }
+  bmark("schedules");
   P.nd_leaf = best.leaf;
   P.tile_pos = best.pos;
   P.n_slots = best.n_slots;
@@ -497,6 +556,7 @@ bool build_tile_schedule(Plan& P) {
     }
     P.bplevel.push_back(static_cast<int32_t>(P.bpart.size()));
   }
+  bmark("backward parts");
   // per-row lookup for the assembly: stored tile (row tile, column tile)
   std::vector<std::vector<std::pair<int32_t, int32_t>>> rows(NT);
   for (int cp = 0; cp < NT; ++cp)
@@ -564,7 +624,9 @@ bool build_tile_schedule(Plan& P) {
       }
     }
   }
+  bmark("rows, partition");
   build_dataflow_deps(P, P.ftask, P.flevel, P.fdep_start, P.fdep);
+  bmark("dataflow deps");
   return true;
 }
 

@@ -35,7 +35,11 @@ class _DeviceArray:
 
 class TorchAllReduce:
     """dynohip_allreduce_fn over torch.distributed: in-place sum over the
-    group, returning only once the result is in the buffer."""
+    group. Device buffers: with RCCL (backend "nccl") the all-reduce is
+    enqueued on the solver's own stream (torch.cuda.ExternalStream), so it
+    is ordered after the kernels that wrote the buffer and before the ones
+    that read the result, with no host synchronisation; with gloo the stream
+    is synchronised and the buffer staged through host memory."""
 
     def __init__(self, device, group=None):
         import torch
@@ -50,7 +54,7 @@ class TorchAllReduce:
         self.doubles = 0
         self.fn = _abi.ALLREDUCE_FN(self._call)
 
-    def _call(self, _ctx, buf, n, on_device):
+    def _call(self, _ctx, buf, n, on_device, stream):
         try:
             torch, dist = self.torch, self.dist
             self.calls += 1
@@ -58,13 +62,16 @@ class TorchAllReduce:
             if on_device:
                 ptr = C.cast(buf, C.c_void_p).value
                 t = torch.as_tensor(_DeviceArray(ptr, n), device=self.device)
+                ext = torch.cuda.ExternalStream(int(stream or 0), device=self.device)
                 if self.on_gpu:
-                    dist.all_reduce(t, group=self.group)
+                    with torch.cuda.stream(ext):   # stream-ordered, returns before completion
+                        dist.all_reduce(t, group=self.group)
                 else:
+                    ext.synchronize()
                     h = t.cpu()
                     dist.all_reduce(h, group=self.group)
                     t.copy_(h)
-                torch.cuda.synchronize(self.device)
+                    torch.cuda.synchronize(self.device)
             else:
                 arr = np.ctypeslib.as_array(buf, shape=(int(n),))
                 if self.on_gpu:
@@ -108,7 +115,7 @@ class PartitionedSolver(Solver):
         mine = (owner == self.rank) | ((owner < 0) & (self.rank == 0))
         mask = np.repeat(mine, sizes)
         part = np.where(mask, data, 0.0)
-        rc = self._allreduce.fn(None, part.ctypes.data_as(C.POINTER(C.c_double)), part.shape[0], 0)
+        rc = self._allreduce.fn(None, part.ctypes.data_as(C.POINTER(C.c_double)), part.shape[0], 0, None)
         if rc != 0:
             raise RuntimeError("all-reduce of the gathered values failed")
         return part

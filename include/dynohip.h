@@ -295,11 +295,20 @@ int dynohip_plan_schedule(const dynohip_graph_view* g, const uint64_t* keys, con
 /* BASELINE configs[4]). One handle per rank, one rank per GPU.         */
 /* ------------------------------------------------------------------ */
 /* Sums `n` doubles over all ranks, in place, identically on every rank
-   (an all-reduce). on_device = 1: `buf` is device memory of the handle's
-   device and its producers have completed; the function must return only
-   once the result is in `buf`. on_device = 0: host memory. Returns 0 on
-   success. Typically torch.distributed.all_reduce over RCCL. */
-typedef int (*dynohip_allreduce_fn)(void* ctx, double* buf, size_t n, int on_device);
+   (an all-reduce). Returns 0 on success.
+   on_device = 1: `buf` is device memory of the handle's device, written by
+   work enqueued on `stream` (the handle's hipStream_t) that may not have
+   run yet. The function must ORDER the reduction on that stream: it runs
+   after the work already enqueued there, and work enqueued there after the
+   call sees the result (e.g. ncclAllReduce(buf, buf, n, ncclDouble,
+   ncclSum, comm, (hipStream_t)stream), or torch.distributed.all_reduce
+   under torch.cuda.ExternalStream(stream)); it may return before the
+   reduction completes. A host-staged implementation synchronises `stream`
+   first. The solver does not synchronise around this call.
+   on_device = 0: host memory, the result must be in `buf` on return
+   (`stream` is the same stream, for implementations that stage through
+   the device). Typically torch.distributed.all_reduce over RCCL. */
+typedef int (*dynohip_allreduce_fn)(void* ctx, double* buf, size_t n, int on_device, void* stream);
 
 /* Marks the handle as rank `rank` of `nranks` (a power of two >= 2; 1 =
    ordinary single-GPU handle). Call before dynohip_set_values; every rank

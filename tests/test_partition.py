@@ -270,7 +270,7 @@ def _allreduce_worker(rank, world, port, out_path):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     ar = TorchAllReduce("cpu")
     buf = np.arange(8, dtype=np.float64) * (rank + 1)
-    rc = ar.fn(None, buf.ctypes.data_as(C.POINTER(C.c_double)), buf.shape[0], 0)
+    rc = ar.fn(None, buf.ctypes.data_as(C.POINTER(C.c_double)), buf.shape[0], 0, None)
     res = [None] * world
     dist.all_gather_object(res, (rc, buf.tolist(), ar.calls, ar.doubles))
     if rank == 0:
