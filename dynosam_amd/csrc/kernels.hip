@@ -455,9 +455,27 @@ __device__ __forceinline__ double group_apply(const GroupDev& g, int b, F&& f) {
   }
 }
 
+// sum of p[0, n) in a fixed order: thread j adds p[j], p[j + 256], ... in
+// turn, then the block sum. Coherent: the partials of other workgroups, read
+// with sc1 buffer loads (past the non-coherent L2) issued eight at a time
+// ahead of the adds (an atomic load per element serialises the round trips).
 __device__ __forceinline__ double sum_strided(const double* __restrict__ p, int n, bool coherent) {
   double v = 0.0;
-  for (int i = threadIdx.x; i < n; i += kBlock) v += coherent ? ld_sc1(p + i) : p[i];
+  if (coherent) {
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(p), 0, n * static_cast<int>(sizeof(double)), 0x00020000);
+    for (int i0 = threadIdx.x; i0 < n; i0 += 8 * kBlock) {
+      double x[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k)   // past n the buffer's range check returns 0
+        x[k] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, (i0 + k * kBlock) * 8, 0, 16));
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (i0 + k * kBlock < n) v += x[k];
+    }
+  } else {
+    for (int i = threadIdx.x; i < n; i += kBlock) v += p[i];
+  }
   return block_sum(v);
 }
 
@@ -1502,17 +1520,24 @@ __global__ __launch_bounds__(kBlock) void k_wdx(ChainDev cd, int n_edge, const d
   }
 }
 
-// dp = C^-1 (gp - W dX), the W dX products from k_wdx
-__device__ void backsub_thread(const ChainDev& cd, const double* __restrict__ arena, const double* __restrict__ t,
-                               double* __restrict__ dpt, int c) {
+// dp = C^-1 (gp - W dX), the W dX products from k_wdx. Every back-
+// substitution below also returns its points' share of the linearised cost
+// change (LinChangeDev): t^T v + dp^T g_p + lambda ||dp||^2, t = sum W dX
+// (summed apart from the solve's own g_p - t_1 - t_2 ... so dp is unchanged).
+__device__ __forceinline__ double dot3(const double* a, const double* b) { return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]; }
+
+__device__ double backsub_thread(const ChainDev& cd, const double* __restrict__ arena, const double* __restrict__ t,
+                                 double* __restrict__ dpt, int c, double lambda) {
   const int i0 = cd.comp_start[c], i1 = cd.comp_start[c + 1];
-  double z[3];
+  double z[3], acc = 0.0;
   for (int i = i0; i < i1; ++i) {
     const double* gp = arena + cd.off_gp + 3ll * i;
-    double g[3] = {gp[0], gp[1], gp[2]};
+    double g[3] = {gp[0], gp[1], gp[2]}, ts[3] = {0.0, 0.0, 0.0};
     for (int e = cd.pt_edge_start[i]; e < cd.pt_edge_start[i + 1]; ++e) {
       g[0] -= t[3ll * e]; g[1] -= t[3ll * e + 1]; g[2] -= t[3ll * e + 2];
+      ts[0] += t[3ll * e]; ts[1] += t[3ll * e + 1]; ts[2] += t[3ll * e + 2];
     }
+    acc += dot3(ts, arena + cd.off_v + 3ll * i);
     if (i > i0) sub_mx<1>(arena + cd.off_M + 9ll * i, z, g);
     lsolve<1>(arena + cd.off_L + 9ll * i, g);
     z[0] = g[0]; z[1] = g[1]; z[2] = g[2];
@@ -1525,22 +1550,29 @@ __device__ void backsub_thread(const ChainDev& cd, const double* __restrict__ ar
     ltsolve<1>(arena + cd.off_L + 9ll * i, x);
     dpt[3ll * i] = x[0]; dpt[3ll * i + 1] = x[1]; dpt[3ll * i + 2] = x[2];
     xn[0] = x[0]; xn[1] = x[1]; xn[2] = x[2];
+    acc += dot3(x, arena + cd.off_gp + 3ll * i) + lambda * dot3(x, x);
   }
+  return acc;
 }
 
-__device__ void backsub_group(const ChainDev& cd, const double* __restrict__ arena, const double* __restrict__ t,
-                              double* __restrict__ dpt, int c, int lane) {
+__device__ double backsub_group(const ChainDev& cd, const double* __restrict__ arena, const double* __restrict__ t,
+                                double* __restrict__ dpt, int c, int lane, double lambda) {
   const int i0 = cd.comp_start[c], n = cd.comp_start[c + 1] - i0;
-  double zp[3] = {0, 0, 0}, g[3] = {0, 0, 0};
+  double zp[3] = {0, 0, 0}, g[3] = {0, 0, 0}, gp[3] = {0, 0, 0};
   double L[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, M[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  double acc = 0.0;
   int last = 0;
   for (int s0 = 0; s0 < n; s0 += kGrp) {
     const int i = s0 + lane;
     if (i < n) {
       ldk(arena + cd.off_gp + 3ll * (i0 + i), g);
+      gp[0] = g[0]; gp[1] = g[1]; gp[2] = g[2];
+      double ts[3] = {0.0, 0.0, 0.0};
       for (int e = cd.pt_edge_start[i0 + i]; e < cd.pt_edge_start[i0 + i + 1]; ++e) {
         g[0] -= t[3ll * e]; g[1] -= t[3ll * e + 1]; g[2] -= t[3ll * e + 2];
+        ts[0] += t[3ll * e]; ts[1] += t[3ll * e + 1]; ts[2] += t[3ll * e + 2];
       }
+      acc += dot3(ts, arena + cd.off_v + 3ll * (i0 + i));
       ldk(arena + cd.off_L + 9ll * (i0 + i), L);
       if (i > 0) ldk(arena + cd.off_M + 9ll * (i0 + i), M);
     }
@@ -1561,6 +1593,7 @@ __device__ void backsub_group(const ChainDev& cd, const double* __restrict__ are
     const int i = s0 + lane;
     if (s0 != last && i < n) {
       ldk(dpt + 3ll * (i0 + i), g);
+      ldk(arena + cd.off_gp + 3ll * (i0 + i), gp);
       ldk(arena + cd.off_L + 9ll * (i0 + i), L);
       if (i > 0) ldk(arena + cd.off_M + 9ll * (i0 + i), M);
     }
@@ -1574,19 +1607,21 @@ __device__ void backsub_group(const ChainDev& cd, const double* __restrict__ are
         double* d = dpt + 3ll * (i0 + i);
         d[0] = x[0]; d[1] = x[1]; d[2] = x[2];
         if (i > 0) mtx<1>(M, x, tn);
+        acc += dot3(x, gp) + lambda * dot3(x, x);
       }
       grp_bcast(tn, tt, k);
     }
   }
+  return acc;
 }
 
 // dp = D^-1 (g_p - sum_a W_a dX_a) for the lone points of one group block
 // (plan.hpp LoneGroup): a lane per (point, neighbour a) forms W_a dX_a from
 // its edge, the m lanes of a point are summed by shuffles in neighbour order
 // (the same lane layout as lone_point_block), then the point's lane solves.
-__device__ void backsub_lone_block(const ChainDev& cd, const int32_t* __restrict__ lone_blk, int g,
-                                   const double* __restrict__ arena, const double* __restrict__ dpose,
-                                   double* __restrict__ dpt) {
+__device__ double backsub_lone_block(const ChainDev& cd, const int32_t* __restrict__ lone_blk, int g,
+                                     const double* __restrict__ arena, const double* __restrict__ dpose,
+                                     double* __restrict__ dpt, double lambda) {
   const int32_t* blk = lone_blk + static_cast<int64_t>(g) * kLoneBlk;
   const int m = blk[0], npt = blk[1];
   const int lane = threadIdx.x & 63, per = 64 / m, uu = lane / m, a = lane - uu * m;
@@ -1609,6 +1644,7 @@ __device__ void backsub_lone_block(const ChainDev& cd, const int32_t* __restrict
 #pragma unroll
     for (int r = 0; r < 3; ++r) s[r] += __shfl(t[r], src);
   }
+  double acc = 0.0;
   if (valid && a == 0) {
     const int pt = blk[4 + u];
     const double* gp = arena + cd.off_gp + 3ll * pt;
@@ -1617,35 +1653,55 @@ __device__ void backsub_lone_block(const ChainDev& cd, const int32_t* __restrict
     lsolve<1>(L, x);
     ltsolve<1>(L, x);
     dpt[3ll * pt] = x[0]; dpt[3ll * pt + 1] = x[1]; dpt[3ll * pt + 2] = x[2];
+    acc = dot3(s, arena + cd.off_v + 3ll * pt) + dot3(x, gp) + lambda * dot3(x, x);
   }
+  return acc;
 }
 
 // Blocks: [0, nbg) 16-lane groups over the long chains, [nbg, nbg + nbs) a
 // thread per lone point (when they are not grouped), then the lone-point
-// group blocks (when they are)
+// group blocks (when they are), then (with the cost change) blocks over the
+// pose dimensions: dx^T g_red + lambda ||dx||^2
 __global__ __launch_bounds__(kBlock) void k_backsub(ChainDev cd, const double* __restrict__ arena,
                                                     const double* __restrict__ t, double* __restrict__ dpt, int nbg,
-                                                    int nbs, const double* __restrict__ dpose,
-                                                    const int32_t* __restrict__ lone_blk) {
+                                                    int nbs, int nlone, const double* __restrict__ dpose,
+                                                    const int32_t* __restrict__ lone_blk, LinChangeDev lc) {
   const int blk = blockIdx.x;
+  const double lam = lc.lambda;
+  double acc = 0.0;
   if (blk < nbg) {
     const int c = (blk * kBlock + static_cast<int>(threadIdx.x)) / kGrp;
-    if (c < cd.n_long) backsub_group(cd, arena, t, dpt, c, threadIdx.x % kGrp);
-    return;
+    if (c < cd.n_long) acc = backsub_group(cd, arena, t, dpt, c, threadIdx.x % kGrp, lam);
+  } else if (blk < nbg + nbs) {
+    const int c = cd.n_long + (blk - nbg) * kBlock + static_cast<int>(threadIdx.x);
+    if (c < cd.n_comp) acc = backsub_thread(cd, arena, t, dpt, c, lam);
+  } else if (blk < nbg + nbs + nlone) {
+    acc = backsub_lone_block(cd, lone_blk, blk - nbg - nbs, arena, dpose, dpt, lam);
+  } else {
+    const int i = (blk - nbg - nbs - nlone) * kBlock + static_cast<int>(threadIdx.x);
+    if (i < lc.n_x) acc = dpose[i] * lc.gred[i] + lam * (dpose[i] * dpose[i]);
   }
-  if (blk >= nbg + nbs) {
-    backsub_lone_block(cd, lone_blk, blk - nbg - nbs, arena, dpose, dpt);
-    return;
-  }
-  const int c = cd.n_long + (blk - nbg) * kBlock + static_cast<int>(threadIdx.x);
-  if (c < cd.n_comp) backsub_thread(cd, arena, t, dpt, c);
+  if (!lc.out) return;
+  // the block's partial; k_retract's last block sums them in block order
+  // (a last-arriver sum here, with its write-through store and atomic per
+  // block, measured 12 us slower at C2 than the sum in the next launch)
+  const double bs = block_sum(acc);
+  if (threadIdx.x == 0) lc.partials[blk] = bs;
 }
 
 // ---------------------------------------------------------------- retract
+// The extra last block (sum_n > 0) adds the back-substitution's cost-change
+// partials in block order into *sum_out.
 __global__ __launch_bounds__(kBlock) void k_retract(int n_pose, int n_pt, const double* __restrict__ pose,
                                                     const double* __restrict__ pt, const double* __restrict__ dpose,
                                                     const double* __restrict__ dpt, double* __restrict__ pose_out,
-                                                    double* __restrict__ pt_out) {
+                                                    double* __restrict__ pt_out, const double* __restrict__ sum_in,
+                                                    int sum_n, double* __restrict__ sum_out) {
+  if (sum_n > 0 && blockIdx.x == gridDim.x - 1) {
+    const double r = sum_strided(sum_in, sum_n, false);
+    if (threadIdx.x == 0) *sum_out = r;
+    return;
+  }
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n_pose) {
     P3 T;
@@ -1864,22 +1920,35 @@ void launch_lone_schur(const LoneSchurDev& d, double* arena, hipStream_t s) {
     k_lone_schur<<<d.n_group, kBlock, sizeof(double) * kLoneSub * lone_point_doubles(d.max_m), s>>>(d, arena);
 }
 
+int backsub_blocks(const ChainDev& c, int n_lone, int n_x) {
+  const int nbg = nblocks(static_cast<int64_t>(c.n_long) * kGrp);
+  const int nbs = n_lone > 0 ? 0 : nblocks(c.n_comp - c.n_long);
+  return nbg + nbs + n_lone + nblocks(n_x);
+}
+
 void launch_backsub(const ChainDev& c, int n_edge, const double* arena, const double* dpose, double* wdx, double* dpt,
-                    hipStream_t s, int n_lone, const int32_t* lone_blk) {
-  if (c.n_comp == 0) return;
+                    hipStream_t s, int n_lone, const int32_t* lone_blk, const LinChangeDev* lc) {
+  if (c.n_comp == 0 && !lc) return;
   // grouped lone points form their W dX themselves: k_wdx stops at their first edge
   const int n_wdx = n_lone > 0 ? c.e_lone0 : n_edge;
   if (n_wdx > 0) k_wdx<<<nblocks(n_wdx), kBlock, 0, s>>>(c, n_wdx, arena, dpose, wdx);
   const int nbg = nblocks(static_cast<int64_t>(c.n_long) * kGrp);
   const int nbs = n_lone > 0 ? 0 : nblocks(c.n_comp - c.n_long);
-  k_backsub<<<nbg + nbs + n_lone, kBlock, 0, s>>>(c, arena, wdx, dpt, nbg, nbs, dpose, lone_blk);
+  LinChangeDev d;
+  if (lc) d = *lc;
+  const int nb = nbg + nbs + n_lone + (lc ? nblocks(d.n_x) : 0);
+  if (nb == 0) return;
+  k_backsub<<<nb, kBlock, 0, s>>>(c, arena, wdx, dpt, nbg, nbs, n_lone, dpose, lone_blk, d);
 }
 
 void launch_retract(int n_pose, int n_pt, const double* pose, const double* pt, const double* dpose,
-                    const double* dpt, double* pose_out, double* pt_out, hipStream_t s) {
+                    const double* dpt, double* pose_out, double* pt_out, hipStream_t s, const double* sum_in,
+                    int sum_n, double* sum_out) {
   const int n = n_pose + n_pt;
-  if (n == 0) return;
-  k_retract<<<nblocks(n), kBlock, 0, s>>>(n_pose, n_pt, pose, pt, dpose, dpt, pose_out, pt_out);
+  if (!sum_out) sum_n = 0;
+  if (n == 0 && sum_n == 0) return;
+  k_retract<<<nblocks(n) + (sum_n > 0 ? 1 : 0), kBlock, 0, s>>>(n_pose, n_pt, pose, pt, dpose, dpt, pose_out, pt_out,
+                                                                sum_in, sum_n, sum_out);
 }
 
 }  // namespace dynohip

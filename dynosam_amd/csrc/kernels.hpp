@@ -148,9 +148,31 @@ void launch_chain_solve_y(const ChainDev& c, double* arena, hipStream_t s);
 // launch_chain_factor: reads L and v of the lone points)
 void launch_lone_schur(const LoneSchurDev& d, double* arena, hipStream_t s);
 int debug_lone_clock(void* out);   // -DDYNOHIP_LONE_CLOCK builds: the stamps of the last launch
-// dpt = C^-1 (gp - W dpose); wdx: scratch of 3 doubles per point-pose edge
+// The linearised cost change of the step, formed by the back-substitution
+// from the solve itself instead of re-reading the Jacobian records
+// (JacobianFactor::error over the graph, LevenbergMarquardtOptimizer.cpp
+// tryLambda). With (H + lambda I) delta = g (GTSAM's default damping, lambda
+// on every dimension) and L(delta) = 0.5 ||J delta - b||^2:
+//   L(0) - L(delta) = 0.5 (delta^T g + lambda ||delta||^2),
+//   delta^T g = dx^T g_red + sum over points (t^T v + dp^T g_p),
+// t = W dx, v = C^-1 g_p (k_chain_factor), g_red the reduced gradient
+// (g_x = g_red + W^T v). Each block of the launch leaves its partial of
+// delta^T g + lambda ||delta||^2 in `partials`; launch_retract's extra block
+// sums them in block order.
+struct LinChangeDev {
+  double* partials = nullptr;   // one slot per block of the launch (backsub_blocks)
+  double* out = nullptr;        // non-null: form the partials
+  const double* gred = nullptr;
+  int n_x = 0;                  // pose dimensions (6 n_pose), x in pose order
+  double lambda = 0.0;
+};
+// blocks of the back-substitution launch (the partial slots LinChangeDev needs)
+int backsub_blocks(const ChainDev& c, int n_lone, int n_x);
+// dpt = C^-1 (gp - W dpose); wdx: scratch of 3 doubles per point-pose edge;
+// lc (optional): the linearised cost change as above
 void launch_backsub(const ChainDev& c, int n_edge, const double* arena, const double* dpose, double* wdx, double* dpt,
-                    hipStream_t s, int n_lone = 0, const int32_t* lone_blk = nullptr);
+                    hipStream_t s, int n_lone = 0, const int32_t* lone_blk = nullptr,
+                    const LinChangeDev* lc = nullptr);
 
 // factor the tiles and solve (L L^T) x = r (forward substitution fused
 // into the factorisation: contrib holds L(i,k) y_k per stored tile). Linv
@@ -172,7 +194,9 @@ void launch_tile_cholesky_solve(const TileDev& b, const TileSchedDev& sd, const 
                                 double* Linv, const double* r, double* contrib, double* y, double* x, int* fail,
                                 hipStream_t s, hipStream_t side, hipEvent_t ev_main, hipEvent_t ev_side);
 
+// (sum_n > 0: one more block sums sum_in[0, sum_n) in order into *sum_out)
 void launch_retract(int n_pose, int n_pt, const double* pose, const double* pt, const double* dpose,
-                    const double* dpt, double* pose_out, double* pt_out, hipStream_t s);
+                    const double* dpt, double* pose_out, double* pt_out, hipStream_t s,
+                    const double* sum_in = nullptr, int sum_n = 0, double* sum_out = nullptr);
 
 }  // namespace dynohip

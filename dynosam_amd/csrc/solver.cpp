@@ -279,7 +279,12 @@ struct dynohip_solver {
   DevBuf<unsigned> fsync;   // [0] dataflow task queue head, [4..] per-slot write counters
   DevBuf<unsigned> done;
   DevBuf<double> partials, result;
+  DevBuf<double> lcpart;     // block partials of the linearised cost change (k_backsub)
   DevBuf<unsigned> sumctr;   // arrival counter of the folded reductions
+  // the linearised cost change: from the solve (k_backsub, default) or, with
+  // DYNOHIP_LINERR_DIRECT=1 and on partitioned handles, as GTSAM forms it,
+  // 0.5 ||J delta - b||^2 re-evaluated over the Jacobian records (k_linerr)
+  bool linerr_direct = false;
   // inside `result`: doubles [0..3] results, [4] the solve's fail flag (int),
   // [5] the fail bits being accumulated (moved to [4] and cleared by the error sum)
   int* failp = nullptr;
@@ -468,6 +473,8 @@ int upload_plan(dynohip_solver* s) {
   ld.off_L = P.off_L;
   ld.off_gp = P.off_gp;
   ld.off_I6 = P.off_I6;
+  HIPCHK(s, s->lcpart.alloc(static_cast<size_t>(backsub_blocks(
+                                c, P.lone_all_grouped ? static_cast<int>(P.lgroup.size()) : 0, 6 * P.n_pose)) + 1));
   TileDev& b = s->bd;
   b.NT = P.NT;
   b.n_red = P.n_red;
@@ -611,8 +618,13 @@ void enqueue_linearize(dynohip_solver* s, const double* pose, const double* pt, 
                       s->lone_blk.p);
 }
 
+// result[0] of a try holds the linearised cost change (x2) rather than the
+// new linear error
+bool lin_change_mode(const dynohip_solver* s) { return s->nranks == 1 && !s->linerr_direct; }
+
 // damped solve + linearised error + retract + error for one lambda.
-// result[0] = new linear error, result[1] = new nonlinear error; fail flag.
+// result[0] = new linear error (or 2x the cost change, lin_change_mode),
+// result[1] = new nonlinear error; fail flag.
 int enqueue_try(dynohip_solver* s, double lambda) {
   const bool timed = s->timing;
   Plan& P = s->plan;
@@ -668,11 +680,26 @@ int enqueue_try(dynohip_solver* s, double lambda) {
   }
   if (timed) (void)hipEventRecord(s->ev[6], st);
   // pose deltas are x[0 .. 6 n_pose) in pose-index order
-  launch_backsub(s->cd, P.n_edge, A, x, s->wdx.p, s->dpt.p, st,
-                 P.lone_all_grouped ? static_cast<int>(P.lgroup.size()) : 0, s->lone_blk.p);
-  enqueue_linerr(s, x, s->dpt.p, s->partials.p, s->result.p);
+  const int n_lone = P.lone_all_grouped ? static_cast<int>(P.lgroup.size()) : 0;
+  if (lin_change_mode(s)) {
+    // result[0] = delta^T g + lambda ||delta||^2 (twice the linearised cost change)
+    LinChangeDev lc;
+    lc.partials = s->lcpart.p;
+    lc.out = s->result.p;
+    lc.gred = s->gred.p;
+    lc.n_x = 6 * P.n_pose;
+    lc.lambda = lambda;
+    launch_backsub(s->cd, P.n_edge, A, x, s->wdx.p, s->dpt.p, st, n_lone, s->lone_blk.p, &lc);
+  } else {
+    // result[0] = the linear error at delta
+    launch_backsub(s->cd, P.n_edge, A, x, s->wdx.p, s->dpt.p, st, n_lone, s->lone_blk.p);
+    enqueue_linerr(s, x, s->dpt.p, s->partials.p, s->result.p);
+  }
   if (timed) (void)hipEventRecord(s->ev[7], st);
-  launch_retract(P.n_pose, P.n_pt, s->pose.p, s->pt.p, x, s->dpt.p, s->pose_c.p, s->pt_c.p, st);
+  const bool lcm = lin_change_mode(s);
+  if (lcm && backsub_blocks(s->cd, n_lone, 6 * P.n_pose) == 0) HIPCHK(s, hipMemsetAsync(s->result.p, 0, sizeof(double), st));
+  launch_retract(P.n_pose, P.n_pt, s->pose.p, s->pt.p, x, s->dpt.p, s->pose_c.p, s->pt_c.p, st, s->lcpart.p,
+                 lcm ? backsub_blocks(s->cd, n_lone, 6 * P.n_pose) : 0, lcm ? s->result.p : nullptr);
   enqueue_error(s, s->pose_c.p, s->pt_c.p, s->partials.p + s->partial_slots, s->result.p + 1);
   if (timed) (void)hipEventRecord(s->ev[8], st);
   return 0;
@@ -835,9 +862,12 @@ int lm_iterate(dynohip_solver* s) {
     bool step_ok = false, stop = false;
     double modelFidelity = 0.0, newError = INFINITY;
     if (solved) {
-      const double newLin = res[0];
+      // linearizedCostChange (LevenbergMarquardtOptimizer.cpp tryLambda): from
+      // the solve, or oldLinearizedError - newLinearizedError as GTSAM forms it
+      const bool from_solve = lin_change_mode(s);
+      const double linChange = from_solve ? 0.5 * res[0] : oldLin - res[0];
+      const double newLin = from_solve ? oldLin - linChange : res[0];
       te.new_linear_error = newLin;
-      const double linChange = oldLin - newLin;
       if (linChange >= 0) {
         newError = res[1];
         te.new_error = newError;
@@ -946,6 +976,7 @@ int dynohip_create(int device_id, dynohip_solver** out) {
   }
   dynohip_solver* s = new dynohip_solver();
   s->device = device_id;
+  if (const char* e = std::getenv("DYNOHIP_LINERR_DIRECT")) s->linerr_direct = std::atoi(e) != 0;
   s->stream = r.stream;
   s->side = r.side;
   s->ev_main = r.ev_main;

@@ -197,6 +197,37 @@ def test_free_running_optimize(gpu_available, name, kw):
         assert a["lam"] == b["lam"]
 
 
+@pytest.mark.parametrize("name", ["T2", "C1", "C2"])
+def test_cost_change_from_solve_matches_direct(gpu_available, name, monkeypatch):
+    """The linearised cost change formed by the back-substitution from the
+    solve, 0.5 (delta^T g + lambda ||delta||^2), against GTSAM's form
+    0.5 ||b||^2 - 0.5 ||J delta - b||^2 over the Jacobian records
+    (DYNOHIP_LINERR_DIRECT=1, k_linerr): the same accept/reject and lambda
+    sequence, and the same linear errors (a rounding-level difference
+    relative to the cost change)."""
+    g, v, _ = synth.generate(name)
+    runs = []
+    for direct in ("0", "1"):
+        monkeypatch.setenv("DYNOHIP_LINERR_DIRECT", direct)
+        s = Solver(0)
+        s.set_graph(g)
+        s.set_values(v)
+        sm = s.optimize()
+        runs.append((sm, s.trace(), s.values_data()))
+        s.close()
+    (sa, ta, va), (sb, tb, vb) = runs
+    assert (sa.iterations, sa.inner_iterations) == (sb.iterations, sb.inner_iterations)
+    assert [e["accepted"] for e in ta] == [e["accepted"] for e in tb]
+    assert [e["lam"] for e in ta] == [e["lam"] for e in tb]
+    for a, b in zip(ta, tb):
+        if not (a["solved"] and b["solved"]):
+            continue
+        ca = a["old_linear_error"] - a["new_linear_error"]
+        cb = b["old_linear_error"] - b["new_linear_error"]
+        assert ca == pytest.approx(cb, rel=1e-6, abs=1e-9 * a["old_linear_error"])
+    assert rel(va, vb) < 1e-9
+
+
 def test_cliques_fixture_matches_golden(gpu_available):
     """The reference's exact-input testCliques graph (test_rgbd_backend.cc:272-486),
     read from the graph-file fixture; GPU run vs the committed oracle trace."""
