@@ -106,6 +106,7 @@ struct TileSchedDev {
   unsigned epoch = 0;          // stamp of the current solve (never 0)
   const int32_t* fdep_start = nullptr;  // dataflow dependencies (Plan::fdep)
   const int32_t* fdep = nullptr;
+  const int32_t* forder = nullptr;  // the dataflow queue: task ids in the order workgroups take them
   unsigned* wcnt = nullptr;    // per-slot write counters, zeroed before each solve
   unsigned* fqueue = nullptr;  // task queue head, zeroed before each solve
   bool persistent_factor = true;  // one dataflow launch instead of one launch per level

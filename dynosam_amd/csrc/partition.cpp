@@ -166,6 +166,7 @@ int build_partitioned_plan(const dynohip_graph_view& g, const uint64_t* keys, co
   L.fpanels = std::move(G.fpanels);
   L.fdep_start = std::move(G.fdep_start);
   L.fdep = std::move(G.fdep);
+  L.fqueue = std::move(G.fqueue);
   L.btask = std::move(G.btask);
   L.blevel = std::move(G.blevel);
   L.bent = std::move(G.bent);
@@ -180,6 +181,7 @@ int build_partitioned_plan(const dynohip_graph_view& g, const uint64_t* keys, co
   L.fpanels1 = std::move(G.fpanels1);
   L.fdep_start1 = std::move(G.fdep_start1);
   L.fdep1 = std::move(G.fdep1);
+  L.fqueue1 = std::move(G.fqueue1);
   L.sep_slot_ranges = std::move(G.sep_slot_ranges);
   L.sep_tile_ranges = std::move(G.sep_tile_ranges);
   L.band_D = std::move(G.band_D);
@@ -235,6 +237,12 @@ extern "C" int dynohip_plan_export(const dynohip_graph_view* g, const uint64_t* 
   else if (nm == "pairs") vec(P.pairs);
   else if (nm == "ftask") raw(P.ftask.data(), P.ftask.size() * sizeof(TileTask));
   else if (nm == "flevel") vec(P.flevel);
+  else if (nm == "fdep_start") vec(P.fdep_start);
+  else if (nm == "fdep") vec(P.fdep);
+  else if (nm == "fqueue") vec(P.fqueue);
+  else if (nm == "fdep_start1") vec(P.fdep_start1);
+  else if (nm == "fdep1") vec(P.fdep1);
+  else if (nm == "fqueue1") vec(P.fqueue1);
   else if (nm == "ftask1") raw(P.ftask1.data(), P.ftask1.size() * sizeof(TileTask));
   else if (nm == "flevel1") vec(P.flevel1);
   else if (nm == "bpart") raw(P.bpart.data(), P.bpart.size() * sizeof(BackPart));

@@ -207,6 +207,9 @@ struct Plan {
   // i != k write their dst slot once each)
   std::vector<int32_t> fdep_start;
   std::vector<int32_t> fdep;
+  // the dataflow kernel's queue: task ids in the order the workgroups take
+  // them, a list schedule of the dependency graph (tiles.cpp queue_order)
+  std::vector<int32_t> fqueue;
   std::vector<BackTask> btask;
   std::vector<int32_t> blevel;
   std::vector<int32_t> bent;            // pairs (slot, row tile)
@@ -222,7 +225,7 @@ struct Plan {
   int nranks = 1, rank = 0;
   std::vector<int32_t> tile_owner;      // per tile: owning rank, -1 = top separator
   std::vector<TileTask> ftask1;
-  std::vector<int32_t> flevel1, fpanels1, fdep_start1, fdep1;
+  std::vector<int32_t> flevel1, fpanels1, fdep_start1, fdep1, fqueue1;
   std::vector<int32_t> sep_slot_ranges; // [beg, end) slot ranges of the separator columns
   std::vector<int32_t> sep_tile_ranges; // [beg, end) tile ranges (natural order) of the separators
 };

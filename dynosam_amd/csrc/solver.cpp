@@ -275,7 +275,7 @@ struct dynohip_solver {
   DevBuf<BackPart> bpart;
   DevBuf<double> bpartials;
   DevBuf<int> arrive;
-  DevBuf<int32_t> fdep_start, fdep;
+  DevBuf<int32_t> fdep_start, fdep, fqueue;
   DevBuf<unsigned> fsync;   // [0] dataflow task queue head, [4..] per-slot write counters
   DevBuf<unsigned> done;
   DevBuf<double> partials, result;
@@ -328,7 +328,7 @@ struct dynohip_solver {
   std::vector<uint8_t> value_kind;   // global value kinds
   DevBuf<uint8_t> damp;
   DevBuf<TileTask> ftask1;
-  DevBuf<int32_t> fdep_start1, fdep1, seprhs_tile, seprhs_start, seprhs_slot;
+  DevBuf<int32_t> fdep_start1, fdep1, fqueue1, seprhs_tile, seprhs_start, seprhs_slot;
   DevBuf<double> xbuf;
   TileSchedDev sd1;
   int n_seprhs = 0;
@@ -421,6 +421,7 @@ int upload_plan(dynohip_solver* s) {
   HIPCHK(s, hipMemsetAsync(s->arrive.p, 0, (static_cast<size_t>(P.NT) + 1) * sizeof(int), st));
   HIPCHK(s, s->fdep_start.upload(P.fdep_start, st));
   HIPCHK(s, s->fdep.upload(P.fdep, st));
+  HIPCHK(s, s->fqueue.upload(P.fqueue, st));
   HIPCHK(s, s->fsync.alloc((static_cast<size_t>(P.n_slots) + 4 + 3) / 4 * 4));
   HIPCHK(s, hipMemsetAsync(s->fsync.p, 0, s->fsync.n * sizeof(unsigned), st));
   HIPCHK(s, s->done.alloc(static_cast<size_t>(P.NT) + 1));
@@ -492,6 +493,7 @@ int upload_plan(dynohip_solver* s) {
   s->sd.bent = s->bent.p;
   s->sd.fdep_start = s->fdep_start.p;
   s->sd.fdep = s->fdep.p;
+  s->sd.forder = s->fqueue.p;
   s->sd.fqueue = s->fsync.p;
   s->sd.wcnt = s->fsync.p + 4;
   // debug: DYNOHIP_POISON_MASK fills the selected device buffers with NaN
@@ -527,10 +529,12 @@ int upload_partition(dynohip_solver* s) {
   HIPCHK(s, s->ftask1.upload(P.ftask1, st));
   HIPCHK(s, s->fdep_start1.upload(P.fdep_start1, st));
   HIPCHK(s, s->fdep1.upload(P.fdep1, st));
+  HIPCHK(s, s->fqueue1.upload(P.fqueue1, st));
   s->sd1 = s->sd;
   s->sd1.ftask = s->ftask1.p;
   s->sd1.fdep_start = s->fdep_start1.p;
   s->sd1.fdep = s->fdep1.p;
+  s->sd1.forder = s->fqueue1.p;
   // separator right-hand-side rows: this rank's interior contributions
   std::vector<int32_t> tl, ts(1, 0), sl;
   for (size_t r = 0; r + 1 < P.sep_tile_ranges.size(); r += 2)

@@ -958,7 +958,8 @@ constexpr int kSpinLimitF = 1 << 22;
 __global__ __launch_bounds__(256) void k_factor_persist(TileDev b, const TileTask* __restrict__ tasks, int ntasks,
                                                         const int32_t* __restrict__ pairs,
                                                         const int32_t* __restrict__ dep_start,
-                                                        const int32_t* __restrict__ dep, unsigned* wcnt,
+                                                        const int32_t* __restrict__ dep,
+                                                        const int32_t* __restrict__ order, unsigned* wcnt,
                                                         unsigned* queue, double* __restrict__ Linv,
                                                         const double* __restrict__ r, double* __restrict__ contrib,
                                                         double* __restrict__ y, int* fail) {
@@ -969,8 +970,9 @@ __global__ __launch_bounds__(256) void k_factor_persist(TileDev b, const TileTas
   for (;;) {
     if (tid == 0) s_q = static_cast<int>(__hip_atomic_fetch_add(queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     __syncthreads();
-    const int q = __builtin_amdgcn_readfirstlane(s_q);
-    if (q >= ntasks) break;
+    const int qpos = __builtin_amdgcn_readfirstlane(s_q);
+    if (qpos >= ntasks) break;
+    const int q = order[qpos];   // task id (schedule order); clocks and dependencies are per id
     const TileTask tk = tasks[q];
     TCLK(0, q, rtc());
     TCLK(5, q, blockIdx.x);
@@ -1256,7 +1258,8 @@ void launch_tile_forward(const TileDev& b, const TileSchedDev& sd, const std::ve
   const int ntasks = flevel.empty() ? 0 : flevel.back();
   if (sd.persistent_factor && ntasks > 0) {
     k_factor_persist<<<std::min(ntasks, sd.workers), 256, 0, s>>>(b, sd.ftask, ntasks, sd.pairs, sd.fdep_start, sd.fdep,
-                                                                  sd.wcnt, sd.fqueue, Linv, r, contrib, y, fail);
+                                                                  sd.forder, sd.wcnt, sd.fqueue, Linv, r, contrib, y,
+                                                                  fail);
   }
   for (size_t lv = 0; lv + 1 < flevel.size() && !sd.persistent_factor; ++lv) {
     const int n = flevel[lv + 1] - flevel[lv];

@@ -26,6 +26,7 @@
 // sequence.
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <climits>
 #include <cstdio>
 #include <cstdlib>
@@ -383,6 +384,12 @@ void schedule(int NT, const std::vector<std::vector<int32_t>>& adj, const std::v
 }
 
 int g_leaf_override = -1;
+// workgroups of the dataflow launch the queue order is simulated on
+// (0: level order, the schedule's own order; DYNOHIP_QUEUE_ORDER=level)
+int g_queue_workers = [] {
+  const char* e = std::getenv("DYNOHIP_QUEUE_ORDER");
+  return (e && std::string(e) == "level") ? 0 : 256;
+}();
 
 // Per task, the slots it reads or writes and how many writes each must have
 // received first: the writes of earlier levels (the level schedule is a valid
@@ -430,6 +437,118 @@ void build_dataflow_deps(const Plan& P, const std::vector<TileTask>& ftask, cons
       if (t.kind == 1 || t.i != t.k) written[t.dst]++;
     }
   }
+}
+
+// The dataflow kernel's queue order. Workgroups take tasks in queue order
+// and wait, holding their CU, until the task's inputs are written. In level
+// order, a wide graph (NS: 14.6k tasks, 256 workgroups) fills every
+// workgroup with tasks of later levels that wait while ready tasks queue
+// behind them: 20 us of queueing per task on average, most of it on the
+// critical path (tools/task_clock.py, profiles/r03/task_clock_NS.txt). The
+// queue is therefore a list schedule of the dependency graph simulated on
+// `workers` workgroups: a task is ready a hand-off after its inputs' writers
+// end, among the ready tasks the one with the longest remaining path starts
+// first (estimated costs below), and the queue lists tasks by simulated
+// start. That is a topological order of the dependencies (each
+// starts after its inputs' writers end), so the launch stays deadlock-free.
+// estimated costs (us, MI355X task clock): a panel and an update task
+// without operand pairs, a 64^3 operand pair, a write-to-reader hand-off
+constexpr double kQPanel = 16.0, kQUpdate = 5.5, kQPair = 1.7, kQHandoff = 2.5;
+std::vector<int32_t> queue_order(const Plan& P, const std::vector<TileTask>& ftask,
+                                 const std::vector<int32_t>& flevel, const std::vector<int32_t>& fdep_start,
+                                 const std::vector<int32_t>& fdep, int workers) {
+  const int n = static_cast<int>(ftask.size());
+  std::vector<int32_t> order(n);
+  for (int q = 0; q < n; ++q) order[q] = q;
+  if (n == 0 || workers <= 0) return order;
+  std::vector<double> dur(n);
+  for (int q = 0; q < n; ++q) {
+    const TileTask& t = ftask[q];
+    const int np = (t.pd_end - t.pd_beg) + (t.po_end - t.po_beg);
+    dur[q] = (t.kind == 0 ? kQPanel : kQUpdate) + kQPair * np;
+  }
+  // predecessor lists (the writer of each awaited write, counted in level order)
+  std::vector<int32_t> wcount(P.n_slots, 0), wstart(P.n_slots + 1, 0);
+  for (int q = 0; q < n; ++q)
+    if (ftask[q].kind == 1 || ftask[q].i != ftask[q].k) wstart[ftask[q].dst + 1]++;
+  for (int sl = 0; sl < P.n_slots; ++sl) wstart[sl + 1] += wstart[sl];
+  std::vector<int32_t> writer(wstart[P.n_slots]);
+  const int nlev = static_cast<int>(flevel.size()) - 1;
+  for (int l = 0; l < nlev; ++l)
+    for (int32_t q = flevel[l]; q < flevel[l + 1]; ++q)
+      if (ftask[q].kind == 1 || ftask[q].i != ftask[q].k) writer[wstart[ftask[q].dst] + wcount[ftask[q].dst]++] = q;
+  std::vector<int32_t> npred(n, 0), sstart(n + 1, 0);
+  for (int q = 0; q < n; ++q)
+    for (int32_t j = fdep_start[q]; j < fdep_start[q + 1]; ++j) sstart[writer[wstart[fdep[2 * j]] + fdep[2 * j + 1] - 1] + 1]++;
+  for (int q = 0; q < n; ++q) sstart[q + 1] += sstart[q];
+  std::vector<int32_t> succ(sstart[n]), sfill(sstart.begin(), sstart.end() - 1);
+  for (int q = 0; q < n; ++q)
+    for (int32_t j = fdep_start[q]; j < fdep_start[q + 1]; ++j) {
+      succ[sfill[writer[wstart[fdep[2 * j]] + fdep[2 * j + 1] - 1]]++] = q;
+      npred[q]++;
+    }
+  // remaining path length, hand-offs included (tasks are in a topological
+  // order already: levels)
+  std::vector<double> rem(n, 0.0);
+  for (int q = n - 1; q >= 0; --q) {
+    double m = 0.0;
+    for (int32_t j = sstart[q]; j < sstart[q + 1]; ++j) m = std::max(m, kQHandoff + rem[succ[j]]);
+    rem[q] = dur[q] + m;
+  }
+  // list scheduling: ready heap by remaining path; tasks whose inputs are
+  // written wait out the hand-off in a heap by ready time; running heap by end
+  auto by_rem = [&](int32_t a, int32_t b) { return rem[a] < rem[b] || (rem[a] == rem[b] && a > b); };
+  using TQ = std::pair<double, int32_t>;
+  auto later = [](const TQ& a, const TQ& b) { return a.first > b.first || (a.first == b.first && a.second > b.second); };
+  std::vector<int32_t> ready;
+  std::vector<TQ> running, pending;
+  std::vector<double> start(n, 0.0), rdy(n, 0.0);
+  for (int q = 0; q < n; ++q)
+    if (npred[q] == 0) ready.push_back(q);
+  std::make_heap(ready.begin(), ready.end(), by_rem);
+  double now = 0.0;
+  int free_w = std::max(1, workers), done = 0;
+  while (done < n) {
+    while (!pending.empty() && pending.front().first <= now) {
+      std::pop_heap(pending.begin(), pending.end(), later);
+      ready.push_back(pending.back().second);
+      std::push_heap(ready.begin(), ready.end(), by_rem);
+      pending.pop_back();
+    }
+    while (free_w > 0 && !ready.empty()) {
+      std::pop_heap(ready.begin(), ready.end(), by_rem);
+      const int32_t q = ready.back();
+      ready.pop_back();
+      start[q] = now;
+      running.push_back({now + dur[q], q});
+      std::push_heap(running.begin(), running.end(), later);
+      --free_w;
+    }
+    // next event: a task ends or a hand-off completes
+    const double t_end = running.empty() ? INFINITY : running.front().first;
+    const double t_rdy = pending.empty() ? INFINITY : pending.front().first;
+    if (!(std::min(t_end, t_rdy) < INFINITY)) break;   // (cannot happen: the graph is acyclic)
+    if (t_rdy < t_end) {
+      now = t_rdy;
+      continue;
+    }
+    std::pop_heap(running.begin(), running.end(), later);
+    const TQ fin = running.back();
+    running.pop_back();
+    now = fin.first;
+    ++free_w;
+    ++done;
+    for (int32_t j = sstart[fin.second]; j < sstart[fin.second + 1]; ++j) {
+      const int32_t sq = succ[j];
+      rdy[sq] = std::max(rdy[sq], now + kQHandoff);
+      if (--npred[sq] == 0) {
+        pending.push_back({rdy[sq], sq});
+        std::push_heap(pending.begin(), pending.end(), later);
+      }
+    }
+  }
+  std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return start[a] < start[b]; });
+  return order;
 }
 
 // keep the tasks whose owner is `who`, in schedule order, with their levels
@@ -590,6 +709,7 @@ bool build_tile_schedule(Plan& P) {
     filter_tasks(all, lev, best.task_owner, P.rank, P.ftask, P.flevel, P.fpanels);
     filter_tasks(all, lev, best.task_owner, -1, P.ftask1, P.flevel1, P.fpanels1);
     build_dataflow_deps(P, P.ftask1, P.flevel1, P.fdep_start1, P.fdep1);
+    P.fqueue1 = queue_order(P, P.ftask1, P.flevel1, P.fdep_start1, P.fdep1, g_queue_workers);
     // backward: separator columns first (they are the top of the tree), then
     // this rank's interior, in the global level order
     std::vector<BackPart> keep;
@@ -627,6 +747,8 @@ bool build_tile_schedule(Plan& P) {
   bmark("rows, partition");
   build_dataflow_deps(P, P.ftask, P.flevel, P.fdep_start, P.fdep);
   bmark("dataflow deps");
+  P.fqueue = queue_order(P, P.ftask, P.flevel, P.fdep_start, P.fdep, g_queue_workers);
+  bmark("queue order");
   return true;
 }
 

@@ -176,3 +176,49 @@ def test_nested_dissection_shortens_critical_path():
     assert band["n_flevel"] - 1 == band["n_tiles"]   # one column per level
     assert nd["n_flevel"] < band["n_flevel"] // 2
     assert sorted(nd["tile_pos"]) == list(range(nd["n_tiles"]))
+
+
+def queue_is_topological(ftask, fdep_start, fdep, queue):
+    """Every dependency of a task (the writer of the awaited write of a slot,
+    writes counted in schedule order) comes earlier in the dataflow queue."""
+    n = ftask.shape[0]
+    assert sorted(queue.tolist()) == list(range(n))
+    pos = np.empty(n, dtype=np.int64)
+    pos[queue] = np.arange(n)
+    writer, cnt = {}, {}
+    for q in range(n):
+        if ftask[q, 0] == 1 or ftask[q, 1] != ftask[q, 2]:
+            c = cnt.get(int(ftask[q, 3]), 0) + 1
+            cnt[int(ftask[q, 3])] = c
+            writer[(int(ftask[q, 3]), c)] = q
+    for q in range(n):
+        for j in range(fdep_start[q], fdep_start[q + 1]):
+            assert pos[writer[(int(fdep[j, 0]), int(fdep[j, 1]))]] < pos[q]
+
+
+@pytest.mark.parametrize("name", ["C1", "C2"])
+def test_dataflow_queue_order_is_topological(name):
+    """tiles.cpp queue_order: the list-scheduled queue of k_factor_persist is
+    a permutation of the tasks in a topological order of the dataflow
+    dependencies (the launch's deadlock freedom), and not the level order."""
+    from dynosam_amd.optimizer import plan_export
+    g, v, _ = synth.generate(name)
+    ft = plan_export(g, v, "ftask").reshape(-1, 10)
+    fs = plan_export(g, v, "fdep_start")
+    fd = plan_export(g, v, "fdep").reshape(-1, 2)
+    qu = plan_export(g, v, "fqueue")
+    queue_is_topological(ft, fs, fd, qu)
+    if name == "C2":
+        assert not np.array_equal(qu, np.arange(ft.shape[0]))
+
+
+def test_partitioned_queue_orders_are_topological():
+    from dynosam_amd.optimizer import plan_export
+    g, v, _ = synth.generate("C2")
+    for rank in range(2):
+        for sfx in ("", "1"):
+            ft = plan_export(g, v, "ftask" + sfx, nranks=2, rank=rank).reshape(-1, 10)
+            fs = plan_export(g, v, "fdep_start" + sfx, nranks=2, rank=rank)
+            fd = plan_export(g, v, "fdep" + sfx, nranks=2, rank=rank).reshape(-1, 2)
+            qu = plan_export(g, v, "fqueue" + sfx, nranks=2, rank=rank)
+            queue_is_topological(ft, fs, fd, qu)

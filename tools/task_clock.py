@@ -72,6 +72,38 @@ def main():
     out["panel"].update({"pre_us_mean": float((t[2] - t[1])[pan].mean()),
                          "factor_us_mean": float((t[3] - t[2])[pan].mean()),
                          "post_us_mean": float((t[4] - t[3])[pan].mean())})
+    # worker occupancy, and the real dependency chain (Plan::fdep: the task
+    # that made the last write a task waits for)
+    busy = float((t[4] - t[1]).sum())
+    out["busy_frac_exec"] = busy / (span * (worker.max() + 1))
+    out["busy_frac_held"] = float((t[4] - t[0]).sum()) / (span * (worker.max() + 1))
+    fs = plan_export(graph, values, "fdep_start")
+    fd = plan_export(graph, values, "fdep").reshape(-1, 2)
+    writer, cnt = {}, {}
+    for q in range(nt):
+        if kind[q] == 1 or kk[q] != ii[q]:
+            c = cnt.get(int(ft[q, 3]), 0) + 1
+            cnt[int(ft[q, 3])] = c
+            writer[(int(ft[q, 3]), c)] = q
+    ready = np.zeros(nt)
+    dpred = -np.ones(nt, dtype=np.int64)
+    for q in range(nt):
+        for j in range(fs[q], fs[q + 1]):
+            w_ = writer[(int(fd[j, 0]), int(fd[j, 1]))]
+            if t[4, w_] > ready[q]:
+                ready[q], dpred[q] = t[4, w_], w_
+    late_pick = np.maximum(0.0, t[0] - ready)   # ready before a worker took it
+    out["ready_before_pick_us"] = {"mean": float(late_pick.mean()), "max": float(late_pick.max()),
+                                   "tasks_over_2us": int((late_pick > 2.0).sum())}
+    dchain = []
+    cur = int(np.argmax(t[4]))
+    while cur >= 0:
+        dchain.append(cur)
+        cur = int(dpred[cur])
+    dchain.reverse()
+    out["dep_chain"] = [{"q": int(q), "kind": int(kind[q]), "k": int(kk[q]), "i": int(ii[q]),
+                         "pick": float(t[0, q]), "ready": float(ready[q]), "deps_met": float(t[1, q]),
+                         "end": float(t[4, q])} for q in dchain]
     # chain ending last
     chain = []
     cur = int(np.argmax(t[4]))
@@ -97,7 +129,9 @@ def main():
            "factor": sum(c.get("factor", 0) for c in chain), "post": sum(c.get("post", 0) for c in chain),
            "update_exec": sum(c["exec"] for c in chain if c["kind"] == 1)}
     out["chain_totals_us"] = tot
-    print(json.dumps({k: v for k, v in out.items() if k != "chain"}, indent=1))
+    print(json.dumps({k: v for k, v in out.items() if k not in ("chain", "dep_chain")}, indent=1))
+    for c in out["dep_chain"]:
+        print("dep " + " ".join(f"{k}={v:.1f}" if isinstance(v, float) else f"{k}={v}" for k, v in c.items()))
     for c in chain:
         print(" ".join(f"{k}={v:.1f}" if isinstance(v, float) else f"{k}={v}" for k, v in c.items()))
     if len(sys.argv) > 2:
