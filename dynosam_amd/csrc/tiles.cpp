@@ -453,6 +453,7 @@ void build_dataflow_deps(const Plan& P, const std::vector<TileTask>& ftask, cons
 // starts after its inputs' writers end), so the launch stays deadlock-free.
 // estimated costs (us, MI355X task clock): a panel and an update task
 // without operand pairs, a 64^3 operand pair, a write-to-reader hand-off
+// (the NS rate moved < 0.5% over panel 16-20, update 5.5-11, hand-off 2.5-6)
 constexpr double kQPanel = 16.0, kQUpdate = 5.5, kQPair = 1.7, kQHandoff = 2.5;
 std::vector<int32_t> queue_order(const Plan& P, const std::vector<TileTask>& ftask,
                                  const std::vector<int32_t>& flevel, const std::vector<int32_t>& fdep_start,
