@@ -423,6 +423,11 @@ struct SumDev {
   int* fail_src = nullptr;   // optional: moved to *fail_dst and cleared by the finisher
   int* fail_dst = nullptr;
   int total = 0;
+  // optional second sum, by the launch's first workgroup: extra_in[0,
+  // extra_n) in order into *extra_out (written by an earlier launch: plain loads)
+  const double* extra_in = nullptr;
+  int extra_n = 0;
+  double* extra_out = nullptr;
 };
 
 __device__ __forceinline__ double ld_sc1(const double* p) {
@@ -479,6 +484,12 @@ __device__ __forceinline__ double sum_strided(const double* __restrict__ p, int 
   return block_sum(v);
 }
 
+__device__ __forceinline__ void finish_extra(const SumDev& sd) {
+  if (sd.extra_n <= 0) return;
+  const double x = sum_strided(sd.extra_in, sd.extra_n, false);
+  if (threadIdx.x == 0) *sd.extra_out = x;
+}
+
 __device__ __forceinline__ void group_finish(double e, const GroupDev& g, const SumDev& sd) {
   const double s = block_sum(e);
   double* slot = sd.partials + g.pbase + blockIdx.x;
@@ -516,6 +527,9 @@ __global__ __launch_bounds__(kBlock) void k_linearize(GroupDev g, const double* 
 template <unsigned M>
 __global__ __launch_bounds__(kBlock) void k_error(GroupDev g, const double* __restrict__ pose,
                                                   const double* __restrict__ pt, SumDev sd) {
+  // the extra sum (inputs from an earlier launch) by the first workgroup,
+  // off the finishing block's path
+  if (blockIdx.x == 0) finish_extra(sd);
   const double e = group_apply<M>(g, gridDim.x - 1 - blockIdx.x, [&](auto tc, int i) {
     return error_one<decltype(tc)::value>(g.t[decltype(tc)::value], i, pose, pt);
   });
@@ -538,6 +552,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce(SumDev sd) {
     *sd.out = s;
     move_fail(sd);
   }
+  finish_extra(sd);
 }
 
 // ---------------------------------------------------------------- gathers
@@ -1503,11 +1518,14 @@ __global__ __launch_bounds__(kBlock) void k_lone_schur(LoneSchurDev d, double* _
   LCLK(4);
 }
 
-// t_e = W_e dX_pose(e) for every point-pose edge (edge-parallel)
-__global__ __launch_bounds__(kBlock) void k_wdx(ChainDev cd, int n_edge, const double* __restrict__ arena,
-                                                const double* __restrict__ dpose, double* __restrict__ t) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n_edge) return;
+// dp = C^-1 (gp - W dX), the products W dX formed per edge (edge_wdx). Every back-
+// substitution below also returns its points' share of the linearised cost
+// change (LinChangeDev): t^T v + dp^T g_p + lambda ||dp||^2, t = sum W dX
+// (summed apart from the solve's own g_p - t_1 - t_2 ... so dp is unchanged).
+__device__ __forceinline__ double dot3(const double* a, const double* b) { return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]; }
+// t_e = W_e dX_pose(e) of one point-pose edge (formerly k_wdx's product)
+__device__ __forceinline__ void edge_wdx(const ChainDev& cd, const double* __restrict__ arena,
+                                         const double* __restrict__ dpose, int e, double* te) {
   double W[18], dx[6];
   ldk(arena + cd.off_W + 18ll * e, W);
   ldk(dpose + 6ll * cd.edge_pose[e], dx);
@@ -1516,26 +1534,29 @@ __global__ __launch_bounds__(kBlock) void k_wdx(ChainDev cd, int n_edge, const d
     double v = 0.0;
 #pragma unroll
     for (int k = 0; k < 6; ++k) v += W[6 * r + k] * dx[k];
-    t[3ll * e + r] = v;
+    te[r] = v;
   }
 }
+// Point3 retract: p + dp
+__device__ __forceinline__ void retract_point(const LinChangeDev& lc, int64_t p, const double* dp) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k) lc.pt_out[3 * p + k] = lc.pt[3 * p + k] + dp[k];
+}
 
-// dp = C^-1 (gp - W dX), the W dX products from k_wdx. Every back-
-// substitution below also returns its points' share of the linearised cost
-// change (LinChangeDev): t^T v + dp^T g_p + lambda ||dp||^2, t = sum W dX
-// (summed apart from the solve's own g_p - t_1 - t_2 ... so dp is unchanged).
-__device__ __forceinline__ double dot3(const double* a, const double* b) { return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]; }
-
-__device__ double backsub_thread(const ChainDev& cd, const double* __restrict__ arena, const double* __restrict__ t,
-                                 double* __restrict__ dpt, int c, double lambda) {
+__device__ double backsub_thread(const ChainDev& cd, const double* __restrict__ arena,
+                                 const double* __restrict__ dpose, double* __restrict__ dpt, int c,
+                                 const LinChangeDev& lc) {
+  const double lambda = lc.lambda;
   const int i0 = cd.comp_start[c], i1 = cd.comp_start[c + 1];
   double z[3], acc = 0.0;
   for (int i = i0; i < i1; ++i) {
     const double* gp = arena + cd.off_gp + 3ll * i;
     double g[3] = {gp[0], gp[1], gp[2]}, ts[3] = {0.0, 0.0, 0.0};
     for (int e = cd.pt_edge_start[i]; e < cd.pt_edge_start[i + 1]; ++e) {
-      g[0] -= t[3ll * e]; g[1] -= t[3ll * e + 1]; g[2] -= t[3ll * e + 2];
-      ts[0] += t[3ll * e]; ts[1] += t[3ll * e + 1]; ts[2] += t[3ll * e + 2];
+      double te[3];
+      edge_wdx(cd, arena, dpose, e, te);
+      g[0] -= te[0]; g[1] -= te[1]; g[2] -= te[2];
+      ts[0] += te[0]; ts[1] += te[1]; ts[2] += te[2];
     }
     acc += dot3(ts, arena + cd.off_v + 3ll * i);
     if (i > i0) sub_mx<1>(arena + cd.off_M + 9ll * i, z, g);
@@ -1552,11 +1573,16 @@ __device__ double backsub_thread(const ChainDev& cd, const double* __restrict__ 
     xn[0] = x[0]; xn[1] = x[1]; xn[2] = x[2];
     acc += dot3(x, arena + cd.off_gp + 3ll * i) + lambda * dot3(x, x);
   }
+  // (after the recurrence: its loads stay off the dependent chain)
+  if (lc.pt_out)
+    for (int i = i0; i < i1; ++i) retract_point(lc, i, dpt + 3ll * i);
   return acc;
 }
 
-__device__ double backsub_group(const ChainDev& cd, const double* __restrict__ arena, const double* __restrict__ t,
-                                double* __restrict__ dpt, int c, int lane, double lambda) {
+__device__ double backsub_group(const ChainDev& cd, const double* __restrict__ arena,
+                                const double* __restrict__ dpose, double* __restrict__ dpt, int c, int lane,
+                                const LinChangeDev& lc) {
+  const double lambda = lc.lambda;
   const int i0 = cd.comp_start[c], n = cd.comp_start[c + 1] - i0;
   double zp[3] = {0, 0, 0}, g[3] = {0, 0, 0}, gp[3] = {0, 0, 0};
   double L[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, M[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -1569,8 +1595,10 @@ __device__ double backsub_group(const ChainDev& cd, const double* __restrict__ a
       gp[0] = g[0]; gp[1] = g[1]; gp[2] = g[2];
       double ts[3] = {0.0, 0.0, 0.0};
       for (int e = cd.pt_edge_start[i0 + i]; e < cd.pt_edge_start[i0 + i + 1]; ++e) {
-        g[0] -= t[3ll * e]; g[1] -= t[3ll * e + 1]; g[2] -= t[3ll * e + 2];
-        ts[0] += t[3ll * e]; ts[1] += t[3ll * e + 1]; ts[2] += t[3ll * e + 2];
+        double te[3];
+        edge_wdx(cd, arena, dpose, e, te);
+        g[0] -= te[0]; g[1] -= te[1]; g[2] -= te[2];
+        ts[0] += te[0]; ts[1] += te[1]; ts[2] += te[2];
       }
       acc += dot3(ts, arena + cd.off_v + 3ll * (i0 + i));
       ldk(arena + cd.off_L + 9ll * (i0 + i), L);
@@ -1612,6 +1640,9 @@ __device__ double backsub_group(const ChainDev& cd, const double* __restrict__ a
       grp_bcast(tn, tt, k);
     }
   }
+  // the lane's own points, after the recurrence (it wrote their dp itself)
+  if (lc.pt_out)
+    for (int i = lane; i < n; i += kGrp) retract_point(lc, i0 + i, dpt + 3ll * (i0 + i));
   return acc;
 }
 
@@ -1621,7 +1652,8 @@ __device__ double backsub_group(const ChainDev& cd, const double* __restrict__ a
 // (the same lane layout as lone_point_block), then the point's lane solves.
 __device__ double backsub_lone_block(const ChainDev& cd, const int32_t* __restrict__ lone_blk, int g,
                                      const double* __restrict__ arena, const double* __restrict__ dpose,
-                                     double* __restrict__ dpt, double lambda) {
+                                     double* __restrict__ dpt, const LinChangeDev& lc) {
+  const double lambda = lc.lambda;
   const int32_t* blk = lone_blk + static_cast<int64_t>(g) * kLoneBlk;
   const int m = blk[0], npt = blk[1];
   const int lane = threadIdx.x & 63, per = 64 / m, uu = lane / m, a = lane - uu * m;
@@ -1654,54 +1686,60 @@ __device__ double backsub_lone_block(const ChainDev& cd, const int32_t* __restri
     ltsolve<1>(L, x);
     dpt[3ll * pt] = x[0]; dpt[3ll * pt + 1] = x[1]; dpt[3ll * pt + 2] = x[2];
     acc = dot3(s, arena + cd.off_v + 3ll * pt) + dot3(x, gp) + lambda * dot3(x, x);
+    if (lc.pt_out) retract_point(lc, pt, x);
   }
   return acc;
 }
 
-// Blocks: [0, nbg) 16-lane groups over the long chains, [nbg, nbg + nbs) a
-// thread per lone point (when they are not grouped), then the lone-point
-// group blocks (when they are), then (with the cost change) blocks over the
-// pose dimensions: dx^T g_red + lambda ||dx||^2
+// Blocks: (with the try tail, LinChangeDev) first a thread per pose, then
+// [0, nbg) 16-lane groups over the long chains, [nbg, nbg + nbs) a thread
+// per lone point (when they are not grouped), then the lone-point group
+// blocks (when they are)
 __global__ __launch_bounds__(kBlock) void k_backsub(ChainDev cd, const double* __restrict__ arena,
-                                                    const double* __restrict__ t, double* __restrict__ dpt, int nbg,
+                                                    double* __restrict__ dpt, int nbg,
                                                     int nbs, int nlone, const double* __restrict__ dpose,
                                                     const int32_t* __restrict__ lone_blk, LinChangeDev lc) {
-  const int blk = blockIdx.x;
-  const double lam = lc.lambda;
+  // pose blocks first (a few, compute-heavy), then the chains (the longest)
+  const int npb = lc.out ? (lc.n_pose + kBlock - 1) / kBlock : 0;
+  const int blk = static_cast<int>(blockIdx.x) - npb;
   double acc = 0.0;
-  if (blk < nbg) {
+  if (blk < 0) {
+    // a thread per pose: its share of dx^T g_red + lambda ||dx||^2, and
+    // Pose3 retract X * Exp(dx)
+    const int p = static_cast<int>(blockIdx.x) * kBlock + static_cast<int>(threadIdx.x);
+    if (p < lc.n_pose) {
+      double xi[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        xi[k] = dpose[6ll * p + k];
+        acc += xi[k] * lc.gred[6ll * p + k] + lc.lambda * (xi[k] * xi[k]);
+      }
+      P3 T;
+      load_pose(lc.pose + 12ll * p, T);
+      store_pose(lc.pose_out + 12ll * p, pose_retract(T, xi));
+    }
+  } else if (blk < nbg) {
     const int c = (blk * kBlock + static_cast<int>(threadIdx.x)) / kGrp;
-    if (c < cd.n_long) acc = backsub_group(cd, arena, t, dpt, c, threadIdx.x % kGrp, lam);
+    if (c < cd.n_long) acc = backsub_group(cd, arena, dpose, dpt, c, threadIdx.x % kGrp, lc);
   } else if (blk < nbg + nbs) {
     const int c = cd.n_long + (blk - nbg) * kBlock + static_cast<int>(threadIdx.x);
-    if (c < cd.n_comp) acc = backsub_thread(cd, arena, t, dpt, c, lam);
-  } else if (blk < nbg + nbs + nlone) {
-    acc = backsub_lone_block(cd, lone_blk, blk - nbg - nbs, arena, dpose, dpt, lam);
+    if (c < cd.n_comp) acc = backsub_thread(cd, arena, dpose, dpt, c, lc);
   } else {
-    const int i = (blk - nbg - nbs - nlone) * kBlock + static_cast<int>(threadIdx.x);
-    if (i < lc.n_x) acc = dpose[i] * lc.gred[i] + lam * (dpose[i] * dpose[i]);
+    acc = backsub_lone_block(cd, lone_blk, blk - nbg - nbs, arena, dpose, dpt, lc);
   }
   if (!lc.out) return;
-  // the block's partial; k_retract's last block sums them in block order
-  // (a last-arriver sum here, with its write-through store and atomic per
-  // block, measured 12 us slower at C2 than the sum in the next launch)
+  // the block's partial; launch_error's finishing block sums them in block
+  // order (a last-arriver sum here, with its write-through store and atomic
+  // per block, measured 12 us slower at C2 than the sum in a later launch)
   const double bs = block_sum(acc);
-  if (threadIdx.x == 0) lc.partials[blk] = bs;
+  if (threadIdx.x == 0) lc.partials[blockIdx.x] = bs;
 }
 
 // ---------------------------------------------------------------- retract
-// The extra last block (sum_n > 0) adds the back-substitution's cost-change
-// partials in block order into *sum_out.
 __global__ __launch_bounds__(kBlock) void k_retract(int n_pose, int n_pt, const double* __restrict__ pose,
                                                     const double* __restrict__ pt, const double* __restrict__ dpose,
                                                     const double* __restrict__ dpt, double* __restrict__ pose_out,
-                                                    double* __restrict__ pt_out, const double* __restrict__ sum_in,
-                                                    int sum_n, double* __restrict__ sum_out) {
-  if (sum_n > 0 && blockIdx.x == gridDim.x - 1) {
-    const double r = sum_strided(sum_in, sum_n, false);
-    if (threadIdx.x == 0) *sum_out = r;
-    return;
-  }
+                                                    double* __restrict__ pt_out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n_pose) {
     P3 T;
@@ -1785,12 +1823,16 @@ SumDev sum_for(const GroupPlan& gp, int g, double* partials, unsigned* counter, 
 }
 
 // no factors: the sum is 0
-void launch_empty_sum(double* partials, double* out, int* fail_src, int* fail_dst, hipStream_t s) {
+void launch_empty_sum(double* partials, double* out, int* fail_src, int* fail_dst, hipStream_t s,
+                      const double* extra_in = nullptr, int extra_n = 0, double* extra_out = nullptr) {
   SumDev sd;
   sd.partials = partials;
   sd.out = out;
   sd.fail_src = fail_src;
   sd.fail_dst = fail_dst;
+  sd.extra_in = extra_in;
+  sd.extra_n = extra_out ? extra_n : 0;
+  sd.extra_out = extra_out;
   k_reduce<<<1, kBlock, 0, s>>>(sd);
 }
 }  // namespace
@@ -1809,7 +1851,8 @@ void launch_linearize(const TypeDev* td, const double* pose, const double* pt, d
 }
 
 void launch_error(const TypeDev* td, const double* pose, const double* pt, double* partials, unsigned* counter,
-                  double* out, int* fail_src, int* fail_dst, hipStream_t s) {
+                  double* out, int* fail_src, int* fail_dst, hipStream_t s, const double* extra_in, int extra_n,
+                  double* extra_out) {
   const GroupPlan gp = plan_groups(td);
   for (int g = 0; g < kNGroups; ++g) {
     if (gp.blocks[g] == 0) continue;
@@ -1817,10 +1860,13 @@ void launch_error(const TypeDev* td, const double* pose, const double* pt, doubl
     if (sd.out) {
       sd.fail_src = fail_src;
       sd.fail_dst = fail_dst;
+      sd.extra_in = extra_in;
+      sd.extra_n = extra_out ? extra_n : 0;
+      sd.extra_out = extra_out;
     }
     DH_GROUP_DISPATCH(g, k_error, gp.blocks[g], gp.dev[g], pose, pt, sd);
   }
-  if (gp.last < 0) launch_empty_sum(partials, out, fail_src, fail_dst, s);
+  if (gp.last < 0) launch_empty_sum(partials, out, fail_src, fail_dst, s, extra_in, extra_n, extra_out);
 }
 
 void launch_linerr(const TypeDev* td, const double* arena, const double* dpose, const double* dpt, double* partials,
@@ -1920,35 +1966,29 @@ void launch_lone_schur(const LoneSchurDev& d, double* arena, hipStream_t s) {
     k_lone_schur<<<d.n_group, kBlock, sizeof(double) * kLoneSub * lone_point_doubles(d.max_m), s>>>(d, arena);
 }
 
-int backsub_blocks(const ChainDev& c, int n_lone, int n_x) {
+int backsub_blocks(const ChainDev& c, int n_lone, int n_pose) {
   const int nbg = nblocks(static_cast<int64_t>(c.n_long) * kGrp);
   const int nbs = n_lone > 0 ? 0 : nblocks(c.n_comp - c.n_long);
-  return nbg + nbs + n_lone + nblocks(n_x);
+  return nbg + nbs + n_lone + nblocks(n_pose);
 }
 
-void launch_backsub(const ChainDev& c, int n_edge, const double* arena, const double* dpose, double* wdx, double* dpt,
+void launch_backsub(const ChainDev& c, const double* arena, const double* dpose, double* dpt,
                     hipStream_t s, int n_lone, const int32_t* lone_blk, const LinChangeDev* lc) {
   if (c.n_comp == 0 && !lc) return;
-  // grouped lone points form their W dX themselves: k_wdx stops at their first edge
-  const int n_wdx = n_lone > 0 ? c.e_lone0 : n_edge;
-  if (n_wdx > 0) k_wdx<<<nblocks(n_wdx), kBlock, 0, s>>>(c, n_wdx, arena, dpose, wdx);
   const int nbg = nblocks(static_cast<int64_t>(c.n_long) * kGrp);
   const int nbs = n_lone > 0 ? 0 : nblocks(c.n_comp - c.n_long);
   LinChangeDev d;
   if (lc) d = *lc;
-  const int nb = nbg + nbs + n_lone + (lc ? nblocks(d.n_x) : 0);
+  const int nb = nbg + nbs + n_lone + (lc ? nblocks(d.n_pose) : 0);
   if (nb == 0) return;
-  k_backsub<<<nb, kBlock, 0, s>>>(c, arena, wdx, dpt, nbg, nbs, n_lone, dpose, lone_blk, d);
+  k_backsub<<<nb, kBlock, 0, s>>>(c, arena, dpt, nbg, nbs, n_lone, dpose, lone_blk, d);
 }
 
 void launch_retract(int n_pose, int n_pt, const double* pose, const double* pt, const double* dpose,
-                    const double* dpt, double* pose_out, double* pt_out, hipStream_t s, const double* sum_in,
-                    int sum_n, double* sum_out) {
+                    const double* dpt, double* pose_out, double* pt_out, hipStream_t s) {
   const int n = n_pose + n_pt;
-  if (!sum_out) sum_n = 0;
-  if (n == 0 && sum_n == 0) return;
-  k_retract<<<nblocks(n) + (sum_n > 0 ? 1 : 0), kBlock, 0, s>>>(n_pose, n_pt, pose, pt, dpose, dpt, pose_out, pt_out,
-                                                                sum_in, sum_n, sum_out);
+  if (n == 0) return;
+  k_retract<<<nblocks(n), kBlock, 0, s>>>(n_pose, n_pt, pose, pt, dpose, dpt, pose_out, pt_out);
 }
 
 }  // namespace dynohip

@@ -124,8 +124,11 @@ int error_blocks(const TypeDev* td);
 void launch_linearize(const TypeDev* td, const double* pose, const double* pt, double* arena, double* partials,
                       unsigned* counter, double* out, hipStream_t s);
 // fail_src (optional): accumulated failure bits, moved to *fail_dst and cleared
+// extra_* (optional): the finishing block also sums extra_in[0, extra_n) in
+// order into *extra_out (the back-substitution's cost-change partials)
 void launch_error(const TypeDev* td, const double* pose, const double* pt, double* partials, unsigned* counter,
-                  double* out, int* fail_src, int* fail_dst, hipStream_t s);
+                  double* out, int* fail_src, int* fail_dst, hipStream_t s, const double* extra_in = nullptr,
+                  int extra_n = 0, double* extra_out = nullptr);
 void launch_linerr(const TypeDev* td, const double* arena, const double* dpose, const double* dpt, double* partials,
                    unsigned* counter, double* out, hipStream_t s);
 
@@ -149,29 +152,36 @@ void launch_chain_solve_y(const ChainDev& c, double* arena, hipStream_t s);
 // launch_chain_factor: reads L and v of the lone points)
 void launch_lone_schur(const LoneSchurDev& d, double* arena, hipStream_t s);
 int debug_lone_clock(void* out);   // -DDYNOHIP_LONE_CLOCK builds: the stamps of the last launch
-// The linearised cost change of the step, formed by the back-substitution
-// from the solve itself instead of re-reading the Jacobian records
-// (JacobianFactor::error over the graph, LevenbergMarquardtOptimizer.cpp
-// tryLambda). With (H + lambda I) delta = g (GTSAM's default damping, lambda
-// on every dimension) and L(delta) = 0.5 ||J delta - b||^2:
+// The tail of a try in the back-substitution launch (LevenbergMarquardt-
+// Optimizer.cpp tryLambda): the candidate values and the linearised cost
+// change, formed from the solve itself instead of re-reading the Jacobian
+// records (JacobianFactor::error over the graph). With (H + lambda I) delta
+// = g (GTSAM's default damping, lambda on every dimension) and
+// L(delta) = 0.5 ||J delta - b||^2:
 //   L(0) - L(delta) = 0.5 (delta^T g + lambda ||delta||^2),
 //   delta^T g = dx^T g_red + sum over points (t^T v + dp^T g_p),
 // t = W dx, v = C^-1 g_p (k_chain_factor), g_red the reduced gradient
 // (g_x = g_red + W^T v). Each block of the launch leaves its partial of
-// delta^T g + lambda ||delta||^2 in `partials`; launch_retract's extra block
-// sums them in block order.
+// delta^T g + lambda ||delta||^2 in `partials` (launch_error's finishing block
+// sums them in block order); the point lanes write pt_out = pt + dp and the
+// pose blocks (a thread per pose) pose_out = pose * Exp(dx), so no separate
+// retraction launch runs.
 struct LinChangeDev {
   double* partials = nullptr;   // one slot per block of the launch (backsub_blocks)
-  double* out = nullptr;        // non-null: form the partials
+  double* out = nullptr;        // non-null: this tail runs (the sum lands here)
   const double* gred = nullptr;
-  int n_x = 0;                  // pose dimensions (6 n_pose), x in pose order
+  int n_pose = 0;               // x in pose order, 6 per pose
   double lambda = 0.0;
+  const double* pose = nullptr;
+  const double* pt = nullptr;
+  double* pose_out = nullptr;
+  double* pt_out = nullptr;
 };
 // blocks of the back-substitution launch (the partial slots LinChangeDev needs)
-int backsub_blocks(const ChainDev& c, int n_lone, int n_x);
-// dpt = C^-1 (gp - W dpose); wdx: scratch of 3 doubles per point-pose edge;
+int backsub_blocks(const ChainDev& c, int n_lone, int n_pose);
+// dpt = C^-1 (gp - W dpose);
 // lc (optional): the linearised cost change as above
-void launch_backsub(const ChainDev& c, int n_edge, const double* arena, const double* dpose, double* wdx, double* dpt,
+void launch_backsub(const ChainDev& c, const double* arena, const double* dpose, double* dpt,
                     hipStream_t s, int n_lone = 0, const int32_t* lone_blk = nullptr,
                     const LinChangeDev* lc = nullptr);
 
@@ -195,9 +205,7 @@ void launch_tile_cholesky_solve(const TileDev& b, const TileSchedDev& sd, const 
                                 double* Linv, const double* r, double* contrib, double* y, double* x, int* fail,
                                 hipStream_t s, hipStream_t side, hipEvent_t ev_main, hipEvent_t ev_side);
 
-// (sum_n > 0: one more block sums sum_in[0, sum_n) in order into *sum_out)
 void launch_retract(int n_pose, int n_pt, const double* pose, const double* pt, const double* dpose,
-                    const double* dpt, double* pose_out, double* pt_out, hipStream_t s,
-                    const double* sum_in = nullptr, int sum_n = 0, double* sum_out = nullptr);
+                    const double* dpt, double* pose_out, double* pt_out, hipStream_t s);
 
 }  // namespace dynohip

@@ -269,7 +269,7 @@ struct dynohip_solver {
   DevBuf<uint32_t> nbedge_w;
   DevBuf<int32_t> lone_blk;
   LoneSchurDev ld;
-  DevBuf<double> slots, gred, xy, dpt, wdx, linv, contrib;
+  DevBuf<double> slots, gred, xy, dpt, linv, contrib;
   DevBuf<int32_t> tile_pos, row_start, row_col, row_slot, bent, pairs;
   DevBuf<TileTask> ftask;
   DevBuf<BackPart> bpart;
@@ -432,7 +432,6 @@ int upload_plan(dynohip_solver* s) {
   HIPCHK(s, s->xy.alloc(2 * (nrp > 0 ? nrp : 1)));
   HIPCHK(s, s->linv.alloc(static_cast<size_t>(P.NT) * kTile * kTile + 1));
   HIPCHK(s, s->dpt.alloc(3ull * P.n_pt + 1));
-  HIPCHK(s, s->wdx.alloc(3ull * P.n_edge + 1));
   ChainDev& c = s->cd;
   c.n_comp = P.n_comp;
   c.n_nb = static_cast<int>(P.nb_pose.size());
@@ -475,7 +474,7 @@ int upload_plan(dynohip_solver* s) {
   ld.off_gp = P.off_gp;
   ld.off_I6 = P.off_I6;
   HIPCHK(s, s->lcpart.alloc(static_cast<size_t>(backsub_blocks(
-                                c, P.lone_all_grouped ? static_cast<int>(P.lgroup.size()) : 0, 6 * P.n_pose)) + 1));
+                                c, P.lone_all_grouped ? static_cast<int>(P.lgroup.size()) : 0, P.n_pose)) + 1));
   TileDev& b = s->bd;
   b.NT = P.NT;
   b.n_red = P.n_red;
@@ -498,7 +497,7 @@ int upload_plan(dynohip_solver* s) {
   s->sd.wcnt = s->fsync.p + 4;
   // debug: DYNOHIP_POISON_MASK fills the selected device buffers with NaN
   // bytes after a re-plan (bit 0 arena, 1 partials, 2 slots, 3 gred, 4 xy,
-  // 5 dpt, 6 wdx, 7 linv, 8 contrib, 9 bpartials, 10 pose_c/pt_c), so a read
+  // 5 dpt, (6 unused), 7 linv, 8 contrib, 9 bpartials, 10 pose_c/pt_c), so a read
   // of a never-written element shows up
   if (const char* pm = std::getenv("DYNOHIP_POISON_MASK")) {
     const unsigned mask = static_cast<unsigned>(std::strtoul(pm, nullptr, 0));
@@ -511,7 +510,6 @@ int upload_plan(dynohip_solver* s) {
     poison(3, s->gred.p, s->gred.n * 8);
     poison(4, s->xy.p, s->xy.n * 8);
     poison(5, s->dpt.p, s->dpt.n * 8);
-    poison(6, s->wdx.p, s->wdx.n * 8);
     poison(7, s->linv.p, s->linv.n * 8);
     poison(8, s->contrib.p, s->contrib.n * 8);
     poison(9, s->bpartials.p, s->bpartials.n * 8);
@@ -593,9 +591,12 @@ int sep_copy(dynohip_solver* s, bool pack) {
 }
 
 // error at (pose, pt) into result[slot]
-void enqueue_error(dynohip_solver* s, const double* pose, const double* pt, double* partials, double* out) {
+// extra_n > 0: the finishing block also sums the cost-change partials of the
+// back-substitution into result[0] (lin_change_mode)
+void enqueue_error(dynohip_solver* s, const double* pose, const double* pt, double* partials, double* out,
+                   int extra_n = 0) {
   launch_error(s->td, pose, pt, partials, s->sumctr.p, out, s->failp, reinterpret_cast<int*>(s->result.p + 4),
-               s->stream);
+               s->stream, s->lcpart.p, extra_n, extra_n > 0 ? s->result.p : nullptr);
 }
 
 void enqueue_linerr(dynohip_solver* s, const double* dpose, const double* dpt, double* partials, double* out) {
@@ -687,24 +688,28 @@ int enqueue_try(dynohip_solver* s, double lambda) {
   const int n_lone = P.lone_all_grouped ? static_cast<int>(P.lgroup.size()) : 0;
   if (lin_change_mode(s)) {
     // result[0] = delta^T g + lambda ||delta||^2 (twice the linearised cost change)
+    // (and the candidate values: pose_c, pt_c)
     LinChangeDev lc;
     lc.partials = s->lcpart.p;
     lc.out = s->result.p;
     lc.gred = s->gred.p;
-    lc.n_x = 6 * P.n_pose;
+    lc.n_pose = P.n_pose;
     lc.lambda = lambda;
-    launch_backsub(s->cd, P.n_edge, A, x, s->wdx.p, s->dpt.p, st, n_lone, s->lone_blk.p, &lc);
+    lc.pose = s->pose.p;
+    lc.pt = s->pt.p;
+    lc.pose_out = s->pose_c.p;
+    lc.pt_out = s->pt_c.p;
+    launch_backsub(s->cd, A, x, s->dpt.p, st, n_lone, s->lone_blk.p, &lc);
   } else {
     // result[0] = the linear error at delta
-    launch_backsub(s->cd, P.n_edge, A, x, s->wdx.p, s->dpt.p, st, n_lone, s->lone_blk.p);
+    launch_backsub(s->cd, A, x, s->dpt.p, st, n_lone, s->lone_blk.p);
     enqueue_linerr(s, x, s->dpt.p, s->partials.p, s->result.p);
   }
   if (timed) (void)hipEventRecord(s->ev[7], st);
-  const bool lcm = lin_change_mode(s);
-  if (lcm && backsub_blocks(s->cd, n_lone, 6 * P.n_pose) == 0) HIPCHK(s, hipMemsetAsync(s->result.p, 0, sizeof(double), st));
-  launch_retract(P.n_pose, P.n_pt, s->pose.p, s->pt.p, x, s->dpt.p, s->pose_c.p, s->pt_c.p, st, s->lcpart.p,
-                 lcm ? backsub_blocks(s->cd, n_lone, 6 * P.n_pose) : 0, lcm ? s->result.p : nullptr);
-  enqueue_error(s, s->pose_c.p, s->pt_c.p, s->partials.p + s->partial_slots, s->result.p + 1);
+  const int nlc = lin_change_mode(s) ? backsub_blocks(s->cd, n_lone, P.n_pose) : 0;
+  if (!lin_change_mode(s)) launch_retract(P.n_pose, P.n_pt, s->pose.p, s->pt.p, x, s->dpt.p, s->pose_c.p, s->pt_c.p, st);
+  else if (nlc == 0) HIPCHK(s, hipMemsetAsync(s->result.p, 0, sizeof(double), st));
+  enqueue_error(s, s->pose_c.p, s->pt_c.p, s->partials.p + s->partial_slots, s->result.p + 1, nlc);
   if (timed) (void)hipEventRecord(s->ev[8], st);
   return 0;
 }
