@@ -455,13 +455,17 @@ void build_dataflow_deps(const Plan& P, const std::vector<TileTask>& ftask, cons
 // without operand pairs, a 64^3 operand pair, a write-to-reader hand-off
 // (the NS rate moved < 0.5% over panel 16-20, update 5.5-11, hand-off 2.5-6)
 constexpr double kQPanel = 16.0, kQUpdate = 5.5, kQPair = 1.7, kQHandoff = 2.5;
+constexpr int kQueueSimMax = 100000;
 std::vector<int32_t> queue_order(const Plan& P, const std::vector<TileTask>& ftask,
                                  const std::vector<int32_t>& flevel, const std::vector<int32_t>& fdep_start,
                                  const std::vector<int32_t>& fdep, int workers) {
   const int n = static_cast<int>(ftask.size());
   std::vector<int32_t> order(n);
   for (int q = 0; q < n; ++q) order[q] = q;
-  if (n == 0 || workers <= 0) return order;
+  // (above kQueueSimMax tasks the simulation's host time, ~0.7 us per task,
+  // is not spent: C5's 538k tasks would add 0.37 s of planning, and the
+  // one-GPU measurements that favour it are at NS, 14.6k tasks)
+  if (n == 0 || workers <= 0 || n > kQueueSimMax) return order;
   std::vector<double> dur(n);
   for (int q = 0; q < n; ++q) {
     const TileTask& t = ftask[q];
