@@ -749,9 +749,6 @@ __global__ __launch_bounds__(kBlock) void k_gather_point(PointGatherDev p, const
 }
 
 // a wave per 6x6 target
-#ifndef DYNOHIP_BAND_S
-#define DYNOHIP_BAND_S 1
-#endif
 __device__ __forceinline__ void gather_band(const GatherDev& g, const int32_t* __restrict__ tA,
                                             const int32_t* __restrict__ tB, const uint32_t* __restrict__ tslot, int blk,
                                             const double* __restrict__ arena, const TileDev& b, double lambda,
@@ -763,7 +760,7 @@ __device__ __forceinline__ void gather_band(const GatherDev& g, const int32_t* _
   const int A = tA[t], B = tB[t];
   const uint32_t ts[4] = {tslot[4 * t], tslot[4 * t + 1], tslot[4 * t + 2], tslot[4 * t + 3]};
   double acc[36], a18[18], a9[9], a5[5], a3[3], a2[2], a1[1];
-  group_accumulate<6, 6, 64, DYNOHIP_BAND_S>(g.start, g.ent, t, q, arena, acc);
+  group_accumulate<6, 6, 64, 1>(g.start, g.ent, t, q, arena, acc);
   rs_step<36, 32>(acc, a18, q & 32);
   rs_step<18, 16>(a18, a9, q & 16);
   rs_step<9, 8>(a9, a5, q & 8);
