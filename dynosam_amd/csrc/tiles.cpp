@@ -384,12 +384,13 @@ void schedule(int NT, const std::vector<std::vector<int32_t>>& adj, const std::v
 }
 
 int g_leaf_override = -1;
-// workgroups of the dataflow launch the queue order is simulated on
-// (0: level order, the schedule's own order; DYNOHIP_QUEUE_ORDER=level)
-int g_queue_workers = [] {
+// workgroups of the dataflow launch the queue order is simulated on (0:
+// level order, the schedule's own order; DYNOHIP_QUEUE_ORDER=level, read at
+// every plan build)
+int queue_workers() {
   const char* e = std::getenv("DYNOHIP_QUEUE_ORDER");
   return (e && std::string(e) == "level") ? 0 : 256;
-}();
+}
 
 // Per task, the slots it reads or writes and how many writes each must have
 // received first: the writes of earlier levels (the level schedule is a valid
@@ -714,7 +715,7 @@ bool build_tile_schedule(Plan& P) {
     filter_tasks(all, lev, best.task_owner, P.rank, P.ftask, P.flevel, P.fpanels);
     filter_tasks(all, lev, best.task_owner, -1, P.ftask1, P.flevel1, P.fpanels1);
     build_dataflow_deps(P, P.ftask1, P.flevel1, P.fdep_start1, P.fdep1);
-    P.fqueue1 = queue_order(P, P.ftask1, P.flevel1, P.fdep_start1, P.fdep1, g_queue_workers);
+    P.fqueue1 = queue_order(P, P.ftask1, P.flevel1, P.fdep_start1, P.fdep1, queue_workers());
     // backward: separator columns first (they are the top of the tree), then
     // this rank's interior, in the global level order
     std::vector<BackPart> keep;
@@ -752,7 +753,7 @@ bool build_tile_schedule(Plan& P) {
   bmark("rows, partition");
   build_dataflow_deps(P, P.ftask, P.flevel, P.fdep_start, P.fdep);
   bmark("dataflow deps");
-  P.fqueue = queue_order(P, P.ftask, P.flevel, P.fdep_start, P.fdep, g_queue_workers);
+  P.fqueue = queue_order(P, P.ftask, P.flevel, P.fdep_start, P.fdep, queue_workers());
   bmark("queue order");
   return true;
 }

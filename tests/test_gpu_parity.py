@@ -654,3 +654,27 @@ def test_mixed_lone_points_conditioned(gpu_available):
         if np.linalg.norm(o.values_data() - start) == 0:
             continue
         assert rel(s.values_data(), o.values_data()) < PER_ITER_TOL, it
+
+
+def test_queue_order_is_bit_identical(gpu_available, monkeypatch):
+    """The dataflow factorisation's queue order (list-scheduled by default,
+    DYNOHIP_QUEUE_ORDER=level for the schedule's level order) changes only
+    which workgroup runs a task when: every tile still receives its updates
+    in the fixed order of the dependency counts, so the LM run is
+    bit-identical."""
+    g, v, _ = synth.generate("C2")
+    out = []
+    for order in ("level", "sim"):
+        if order == "level":
+            monkeypatch.setenv("DYNOHIP_QUEUE_ORDER", "level")
+        else:
+            monkeypatch.delenv("DYNOHIP_QUEUE_ORDER", raising=False)
+        s = Solver(0)
+        s.set_graph(g)
+        s.set_values(v)
+        sm = s.optimize()
+        out.append((sm.iterations, sm.inner_iterations, sm.final_error, s.values_data()))
+        s.close()
+    (ia, na, ea, va), (ib, nb, eb, vb) = out
+    assert (ia, na, ea) == (ib, nb, eb)
+    assert np.array_equal(va, vb)
