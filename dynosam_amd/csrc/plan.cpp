@@ -218,9 +218,12 @@ void parallel_for(int64_t n, Body&& body) {
   PlanPool::get().run(nw, [&](int r) { body(n * r / nw, n * (r + 1) / nw); });
 }
 
-// even cut of [0, n) into the planner's worker count
+// even cut of [0, n) targets into the planner's workers, one per 1024
+// targets at most (a sliding window's few hundred targets take one: each
+// worker of a target-range CSR enumerates every source, so a small graph
+// paid the pool dispatch for nothing — window planning 6.2 -> 2.6 ms here)
 std::vector<int64_t> even_cuts(int64_t n) {
-  const int nw = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(PlanPool::get().workers(), n / 64 + 1)));
+  const int nw = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(PlanPool::get().workers(), n / 1024 + 1)));
   std::vector<int64_t> c(nw + 1);
   for (int r = 0; r <= nw; ++r) c[r] = n * r / nw;
   return c;
