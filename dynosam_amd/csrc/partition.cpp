@@ -210,10 +210,16 @@ extern "C" int dynohip_plan_export(const dynohip_graph_view* g, const uint64_t* 
   Partition part;
   GraphStore lg;
   std::string err;
-  const int rc = nranks > 1 ? build_partitioned_plan(*g, keys, kind, n, nranks, rank, P, part, lg, err)
-                            : build_plan(*g, keys, kind, n, P, err);
-  if (rc) return rc;
-  const std::string nm(name);
+  std::string nm(name);
+  // "<name>@recycled": the plan built twice into one Plan object (the second
+  // build reuses the first's arrays, plan_recycle), then exported
+  const bool twice = nm.size() > 9 && nm.compare(nm.size() - 9, 9, "@recycled") == 0;
+  if (twice) nm.resize(nm.size() - 9);
+  for (int b = 0; b < (twice ? 2 : 1); ++b) {
+    const int rc = nranks > 1 ? build_partitioned_plan(*g, keys, kind, n, nranks, rank, P, part, lg, err)
+                              : build_plan(*g, keys, kind, n, P, err);
+    if (rc) return rc;
+  }
   std::vector<int32_t> tmp;
   const int32_t* src = nullptr;
   size_t cnt = 0;
@@ -287,6 +293,45 @@ extern "C" int dynohip_plan_export(const dynohip_graph_view* g, const uint64_t* 
       tmp.push_back(static_cast<int32_t>(P.types[t].base));
       tmp.push_back(static_cast<int32_t>(P.types[t].stride));
     }
+    vec(tmp);
+  }
+  else if (nm == "digest") {
+    // FNV-1a of every plan array and scalar, one 64-bit digest per field as
+    // two int32 (tests/test_plan_digest.py: a plan built on one planner
+    // worker equals the plan built on many, field by field)
+    auto fnv = [&](const void* p, size_t bytes) {
+      uint64_t h = 1469598103934665603ull;
+      const auto* b = static_cast<const unsigned char*>(p);
+      for (size_t i = 0; i < bytes; ++i) h = (h ^ b[i]) * 1099511628211ull;
+      tmp.push_back(static_cast<int32_t>(h & 0xffffffffu));
+      tmp.push_back(static_cast<int32_t>(h >> 32));
+    };
+    auto v = [&](const auto& x) { fnv(x.data(), x.size() * sizeof(x[0])); };
+    const int64_t sc[] = {P.n_pose, P.n_pt, P.n_comp, P.max_chain, P.n_edge, P.lone_max_m, P.lone_all_grouped,
+                          static_cast<int64_t>(P.off_I6), static_cast<int64_t>(P.off_D), static_cast<int64_t>(P.off_E),
+                          static_cast<int64_t>(P.off_gp), static_cast<int64_t>(P.off_W), static_cast<int64_t>(P.off_Y),
+                          static_cast<int64_t>(P.off_v), static_cast<int64_t>(P.off_L), static_cast<int64_t>(P.off_M),
+                          static_cast<int64_t>(P.arena_size), P.n_red, P.NT, P.max_D, P.nd_leaf, P.n_slots,
+                          P.n_partials};
+    fnv(sc, sizeof(sc));
+    v(P.user_kind); v(P.user_idx); v(P.pose_key); v(P.pt_key);
+    v(P.comp_start); v(P.comp_nb_start); v(P.nb_pose); v(P.nb_comp); v(P.comp_y_base);
+    v(P.nbedge_start); v(P.nbedge_pt); v(P.nbedge_w);
+    v(P.edge_pt); v(P.edge_pose); v(P.pt_edge_start);
+    for (int t = 0; t < kNTypes; ++t) {
+      const int64_t ts[] = {P.types[t].n, static_cast<int64_t>(P.types[t].base), P.types[t].stride};
+      fnv(ts, sizeof(ts));
+      v(P.types[t].idx); v(P.types[t].meas); v(P.types[t].isig); v(P.types[t].hk);
+    }
+    for (const GatherList* G : {&P.gD, &P.gE, &P.gGp, &P.gW, &P.gRed, &P.gGred}) { v(G->start); v(G->ent); }
+    v(P.red_A); v(P.red_B); v(P.red_slot);
+    v(P.lgroup); v(P.lone_pose); v(P.lone_blk);
+    v(P.band_D); v(P.tile_pos); v(P.row_start); v(P.row_col); v(P.row_slot);
+    v(P.ftask); v(P.pairs); v(P.flevel); v(P.fpanels); v(P.fdep_start); v(P.fdep); v(P.fqueue);
+    v(P.btask); v(P.blevel); v(P.bent); v(P.bpart); v(P.bplevel);
+    v(P.tile_owner); v(P.ftask1); v(P.flevel1); v(P.fpanels1); v(P.fdep_start1); v(P.fdep1); v(P.fqueue1);
+    v(P.sep_slot_ranges); v(P.sep_tile_ranges);
+    v(part.value_owner); v(part.damp_row);
     vec(tmp);
   }
   else if (nm == "value_owner") vec(part.value_owner);

@@ -3,6 +3,7 @@
 #include <cstdlib>
 // plan.cpp — factor graph -> device layout / gather lists (see plan.hpp).
 #include "plan.hpp"
+#include "plan_pool.hpp"
 
 #include <algorithm>
 #include <cmath>
@@ -10,6 +11,7 @@
 #include <numeric>
 #include <unistd.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
@@ -99,79 +101,6 @@ class KeyIndex {
   size_t mask_;
   std::vector<uint64_t> keys_;
   std::vector<int32_t> vals_;
-};
-
-// The planner's workers: threads created once per process and reused by
-// every plan (a plan runs a dozen parallel sections; creating 16 threads for
-// each cost milliseconds). run(nw, body) calls body(0..nw-1), body(0) on the
-// calling thread, and returns when all are done. Never destroyed: the threads
-// block on the condition variable until the process exits.
-class PlanPool {
- public:
-  static PlanPool& get() {
-    // a forked child has none of the parent's threads: it starts its own pool
-    static PlanPool* p = nullptr;
-    static pid_t owner = 0;
-    static std::mutex mu;
-    std::lock_guard<std::mutex> lk(mu);
-    if (!p || owner != getpid()) {
-      p = new PlanPool();
-      owner = getpid();
-    }
-    return *p;
-  }
-  int workers() const { return nmax_; }
-  template <typename Body>
-  void run(int nw, Body&& body) {
-    nw = std::max(1, std::min(nw, nmax_));
-    if (nw == 1) {
-      body(0);
-      return;
-    }
-    std::unique_lock<std::mutex> call(call_mu_);   // one parallel section at a time
-    std::function<void(int)> fn = [&body](int r) { body(r); };
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      fn_ = &fn;
-      nw_ = nw;
-      pending_ = nw - 1;
-      ++gen_;
-    }
-    cv_.notify_all();
-    body(0);
-    std::unique_lock<std::mutex> lk(mu_);
-    done_cv_.wait(lk, [&] { return pending_ == 0; });
-    fn_ = nullptr;
-  }
-
- private:
-  PlanPool() {
-    const unsigned hc = std::thread::hardware_concurrency();
-    nmax_ = static_cast<int>(std::max(1u, std::min(16u, hc ? hc : 1u)));
-    for (int r = 1; r < nmax_; ++r) std::thread([this, r] { loop(r); }).detach();
-  }
-  void loop(int r) {
-    uint64_t seen = 0;
-    for (;;) {
-      std::function<void(int)>* fn;
-      {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return gen_ != seen; });
-        seen = gen_;
-        if (r >= nw_) continue;
-        fn = fn_;
-      }
-      (*fn)(r);
-      std::lock_guard<std::mutex> lk(mu_);
-      if (--pending_ == 0) done_cv_.notify_one();
-    }
-  }
-  int nmax_ = 1;
-  std::mutex call_mu_, mu_;
-  std::condition_variable cv_, done_cv_;
-  std::function<void(int)>* fn_ = nullptr;
-  int nw_ = 0, pending_ = 0;
-  uint64_t gen_ = 0;
 };
 
 // CSR by target ranges: worker r owns the targets [tcut[r], tcut[r+1]) and
@@ -265,10 +194,43 @@ void compute_red_slots(Plan& P) {
   });
 }
 
+void plan_recycle(Plan& P) {
+  Plan f;
+  // every array: cleared (size 0, capacity kept) and moved into the fresh plan
+  auto k = [](auto& dst, auto& src) {
+    src.clear();
+    dst.swap(src);
+  };
+  k(f.user_kind, P.user_kind); k(f.user_idx, P.user_idx); k(f.pose_key, P.pose_key); k(f.pt_key, P.pt_key);
+  k(f.comp_start, P.comp_start); k(f.comp_nb_start, P.comp_nb_start); k(f.nb_pose, P.nb_pose);
+  k(f.nb_comp, P.nb_comp); k(f.comp_y_base, P.comp_y_base); k(f.nbedge_start, P.nbedge_start);
+  k(f.nbedge_pt, P.nbedge_pt); k(f.nbedge_w, P.nbedge_w);
+  k(f.edge_pt, P.edge_pt); k(f.edge_pose, P.edge_pose); k(f.pt_edge_start, P.pt_edge_start);
+  for (int t = 0; t < kNTypes; ++t) {
+    k(f.types[t].idx, P.types[t].idx); k(f.types[t].meas, P.types[t].meas);
+    k(f.types[t].isig, P.types[t].isig); k(f.types[t].hk, P.types[t].hk);
+  }
+  GatherList Plan::*gl[] = {&Plan::gD, &Plan::gE, &Plan::gGp, &Plan::gW, &Plan::gRed, &Plan::gGred};
+  for (auto m : gl) {
+    k((f.*m).start, (P.*m).start);
+    k((f.*m).ent, (P.*m).ent);
+  }
+  k(f.red_A, P.red_A); k(f.red_B, P.red_B); k(f.red_slot, P.red_slot);
+  k(f.lgroup, P.lgroup); k(f.lone_pose, P.lone_pose); k(f.lone_blk, P.lone_blk);
+  k(f.band_D, P.band_D); k(f.tile_pos, P.tile_pos); k(f.row_start, P.row_start); k(f.row_col, P.row_col);
+  k(f.row_slot, P.row_slot); k(f.ftask, P.ftask); k(f.pairs, P.pairs); k(f.flevel, P.flevel);
+  k(f.fpanels, P.fpanels); k(f.fdep_start, P.fdep_start); k(f.fdep, P.fdep); k(f.fqueue, P.fqueue);
+  k(f.btask, P.btask); k(f.blevel, P.blevel); k(f.bent, P.bent); k(f.bpart, P.bpart); k(f.bplevel, P.bplevel);
+  k(f.tile_owner, P.tile_owner); k(f.ftask1, P.ftask1); k(f.flevel1, P.flevel1); k(f.fpanels1, P.fpanels1);
+  k(f.fdep_start1, P.fdep_start1); k(f.fdep1, P.fdep1); k(f.fqueue1, P.fqueue1);
+  k(f.sep_slot_ranges, P.sep_slot_ranges); k(f.sep_tile_ranges, P.sep_tile_ranges);
+  P = std::move(f);
+}
+
 int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t* kind, size_t n, Plan& P,
                std::string& err, int nranks, int rank, bool with_schedule, bool structure_only) {
   double tmark = plan_now();
-  P = Plan();
+  plan_recycle(P);
   P.nranks = nranks;
   P.rank = rank;
   // ---- values: key lookup ----
@@ -279,6 +241,7 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
   }
   P.user_kind.assign(kind, kind + n);
   P.user_idx.assign(n, -1);
+  plan_mark("value key index", tmark);
 
   const dynohip_factor_block* blocks[kNTypes] = {&g.pose_to_point, &g.landmark_motion_ternary, &g.between,
                                                  &g.prior, &g.landmark_motion_pose, &g.landmark_pose_smoothing};
@@ -293,7 +256,8 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
     }
     fuser[t].resize(b->n * kNKeys[t]);
     // fast path on the workers; any failure is re-found below, in order, for its message
-    std::vector<uint8_t> bad(1, 0);
+    // (bad[0]: a key; bad[1]: a sigma; bad[2]: a measurement)
+    std::vector<uint8_t> bad(3, 0);
     parallel_for(static_cast<int64_t>(b->n), [&](int64_t i0, int64_t i1) {
       for (int64_t i = i0; i < i1; ++i)
         for (int s = 0; s < kNKeys[t]; ++s) {
@@ -305,6 +269,12 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
           }
           fuser[t][i * kNKeys[t] + s] = u;
         }
+      bool sig_ok = true, meas_ok = true;
+      for (int64_t i = i0 * kDim[t]; i < i1 * kDim[t]; ++i)
+        sig_ok &= b->sigmas[i] > 0.0 && std::isfinite(b->sigmas[i]);
+      for (int64_t i = i0 * kMeasDim[t]; i < i1 * kMeasDim[t]; ++i) meas_ok &= std::isfinite(b->measured[i]) != 0;
+      if (!sig_ok) __atomic_store_n(&bad[1], 1, __ATOMIC_RELAXED);
+      if (!meas_ok) __atomic_store_n(&bad[2], 1, __ATOMIC_RELAXED);
     });
     if (bad[0])
     for (size_t i = 0; i < b->n; ++i)
@@ -323,10 +293,8 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
         }
         fuser[t][i * kNKeys[t] + s] = u;
       }
-    for (size_t i = 0; i < b->n * kDim[t]; ++i)
-      if (!(b->sigmas[i] > 0.0) || !std::isfinite(b->sigmas[i])) { err = "non-positive sigma"; return DYNOHIP_EINVAL; }
-    for (size_t i = 0; i < b->n * kMeasDim[t]; ++i)
-      if (!std::isfinite(b->measured[i])) { err = "non-finite measurement"; return DYNOHIP_ENONFINITE; }
+    if (bad[1]) { err = "non-positive sigma"; return DYNOHIP_EINVAL; }
+    if (bad[2]) { err = "non-finite measurement"; return DYNOHIP_ENONFINITE; }
   }
 
   plan_mark("before poses: frame order", tmark);
@@ -456,16 +424,18 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
     tp.stride = static_cast<uint32_t>((kDim[t] * (kCols[t] + 1) + 1) & ~1);
     tp.base = arena;
     arena += static_cast<uint64_t>(tp.stride) * tp.n;
+    // uninitialised, then filled (copies included) on the workers
     tp.idx.resize(b->n * kNKeys[t]);
-    tp.meas.assign(b->measured ? b->measured : nullptr, b->measured ? b->measured + b->n * kMeasDim[t] : nullptr);
+    tp.meas.resize(b->measured ? b->n * kMeasDim[t] : 0);
     tp.isig.resize(b->n * kDim[t]);
+    tp.hk.resize(b->n);
     parallel_for(static_cast<int64_t>(b->n), [&](int64_t i0, int64_t i1) {
       for (int64_t i = i0 * kNKeys[t]; i < i1 * kNKeys[t]; ++i) tp.idx[i] = P.user_idx[fuser[t][i]];
       for (int64_t i = i0 * kDim[t]; i < i1 * kDim[t]; ++i) tp.isig[i] = 1.0 / b->sigmas[i];
+      if (!tp.meas.empty())
+        std::memcpy(tp.meas.data() + i0 * kMeasDim[t], b->measured + i0 * kMeasDim[t], (i1 - i0) * kMeasDim[t] * sizeof(double));
+      for (int64_t i = i0; i < i1; ++i) tp.hk[i] = b->huber_k ? b->huber_k[i] : 0.0;
     });
-    tp.hk.assign(b->n, 0.0);
-    if (b->huber_k)
-      for (size_t i = 0; i < b->n; ++i) tp.hk[i] = b->huber_k[i];
   }
 
   plan_mark("before point-pose edges", tmark);
@@ -473,24 +443,28 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
   {
     // bucket (point, pose) incidences by point, then sort + unique each
     // point's (short) pose list: the (point, pose)-sorted unique edge list
+    // (counted and placed on the workers with atomic cursors: the order
+    // inside a point's list does not matter, it is sorted next)
     std::vector<int32_t> cnt(P.n_pt + 1, 0);
     auto each = [&](auto&& fn) {
       for (int t = 0; t < kNTypes; ++t) {
         const TypePlan& tp = P.types[t];
         const int nk = kNKeys[t];
-        for (int i = 0; i < tp.n; ++i)
-          for (int sa = 0; sa < nk; ++sa)
-            if (kSlotKind[t][sa] == 1)
-              for (int sb = 0; sb < nk; ++sb)
-                if (kSlotKind[t][sb] == 0) fn(tp.idx[i * nk + sa], tp.idx[i * nk + sb]);
+        parallel_for(tp.n, [&](int64_t i0, int64_t i1) {
+          for (int64_t i = i0; i < i1; ++i)
+            for (int sa = 0; sa < nk; ++sa)
+              if (kSlotKind[t][sa] == 1)
+                for (int sb = 0; sb < nk; ++sb)
+                  if (kSlotKind[t][sb] == 0) fn(tp.idx[i * nk + sa], tp.idx[i * nk + sb]);
+        });
       }
     };
-    each([&](int32_t pt, int32_t) { cnt[pt + 1]++; });
+    each([&](int32_t pt, int32_t) { __atomic_fetch_add(&cnt[pt + 1], 1, __ATOMIC_RELAXED); });
     for (int i = 0; i < P.n_pt; ++i) cnt[i + 1] += cnt[i];
-    std::vector<int32_t> poses(cnt[P.n_pt]);
+    std::vector<int32_t, default_init_allocator<int32_t>> poses(cnt[P.n_pt]);
     {
       std::vector<int32_t> cur(cnt.begin(), cnt.end() - 1);
-      each([&](int32_t pt, int32_t pose) { poses[cur[pt]++] = pose; });
+      each([&](int32_t pt, int32_t pose) { poses[__atomic_fetch_add(&cur[pt], 1, __ATOMIC_RELAXED)] = pose; });
     }
     // per point (in parallel): sort + unique its poses in place, then the
     // prefix of the unique counts places every point's edges
@@ -538,42 +512,73 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
 
   plan_mark("before component neighbour poses and Y layout", tmark);
   // ---- component neighbour poses and Y layout ----
-  P.comp_nb_start.assign(1, 0);
   P.comp_y_base.resize(P.n_comp);
   P.off_Y = arena;
-  P.nbedge_start.assign(1, 0);
-  P.nb_pose.reserve(P.n_edge);
-  P.nb_comp.reserve(P.n_edge);
-  P.nbedge_pt.reserve(P.n_edge);
-  P.nbedge_w.reserve(P.n_edge);
-  P.nbedge_start.reserve(static_cast<size_t>(P.n_edge) + 1);
-  std::vector<int32_t> nb;
   // chains of >= 2 points come first (longest first), the lone points last
   int32_t c_lone = 0;
   while (c_lone < P.n_comp && P.comp_start[c_lone + 1] - P.comp_start[c_lone] >= 2) ++c_lone;
-  for (int c = 0; c < c_lone; ++c) {
-    nb.clear();
-    for (int32_t i = P.comp_start[c]; i < P.comp_start[c + 1]; ++i)
-      for (int32_t e = P.pt_edge_start[i]; e < P.pt_edge_start[i + 1]; ++e) nb.push_back(P.edge_pose[e]);
-    std::sort(nb.begin(), nb.end());
-    nb.erase(std::unique(nb.begin(), nb.end()), nb.end());
-    const int nc = P.comp_start[c + 1] - P.comp_start[c];
-    const int m = static_cast<int>(nb.size());
-    P.comp_y_base[c] = static_cast<int64_t>(arena);
-    arena += 18ull * nc * m;
-    for (int b = 0; b < m; ++b) {
-      P.nb_pose.push_back(nb[b]);
-      P.nb_comp.push_back(c);
-      for (int32_t i = P.comp_start[c]; i < P.comp_start[c + 1]; ++i) {
-        const int32_t e = find_edge(i, nb[b]);
-        if (e < P.pt_edge_start[i + 1] && P.edge_pose[e] == nb[b]) {
-          P.nbedge_pt.push_back(i - P.comp_start[c]);
-          P.nbedge_w.push_back(static_cast<uint32_t>(P.off_W + 18ull * e));
-        }
+  {
+    // A chain's (neighbour pose, local point, edge) incidences sorted by
+    // (pose, point): the distinct poses are its neighbour poses (ascending)
+    // and each pose's run lists its edges in point order. Counted on the
+    // workers, placed by a prefix over the chains, then filled on the
+    // workers: the arrays equal the sequential layout.
+    struct Inc {
+      uint64_t key;   // pose << 32 | local point
+      int32_t e;
+    };
+    auto incidences = [&](int c, std::vector<Inc>& inc) {
+      inc.clear();
+      for (int32_t i = P.comp_start[c]; i < P.comp_start[c + 1]; ++i)
+        for (int32_t e = P.pt_edge_start[i]; e < P.pt_edge_start[i + 1]; ++e)
+          inc.push_back(Inc{(static_cast<uint64_t>(P.edge_pose[e]) << 32) | static_cast<uint32_t>(i - P.comp_start[c]), e});
+      std::sort(inc.begin(), inc.end(), [](const Inc& a, const Inc& b) { return a.key < b.key; });
+    };
+    std::vector<int32_t> chain_m(static_cast<size_t>(c_lone) + 1, 0);
+    parallel_chunks(c_lone, 1, [&](int64_t c0, int64_t c1) {
+      std::vector<Inc> inc;
+      for (int64_t c = c0; c < c1; ++c) {
+        incidences(static_cast<int>(c), inc);
+        int32_t m = 0;
+        for (size_t k = 0; k < inc.size(); ++k) m += k == 0 || (inc[k].key >> 32) != (inc[k - 1].key >> 32);
+        chain_m[c + 1] = m;
       }
-      P.nbedge_start.push_back(static_cast<int32_t>(P.nbedge_pt.size()));
+    });
+    for (int c = 0; c < c_lone; ++c) {
+      const int nc = P.comp_start[c + 1] - P.comp_start[c];
+      P.comp_y_base[c] = static_cast<int64_t>(arena);
+      arena += 18ull * nc * chain_m[c + 1];
+      chain_m[c + 1] += chain_m[c];
     }
-    P.comp_nb_start.push_back(static_cast<int32_t>(P.nb_pose.size()));
+    P.comp_nb_start.assign(chain_m.begin(), chain_m.end());
+    const int32_t n_nb = chain_m[c_lone];
+    // a chain's points' edges are contiguous from its first point's first edge
+    const int32_t n_nbe = c_lone > 0 ? P.pt_edge_start[P.comp_start[c_lone]] : 0;
+    P.nb_pose.resize(n_nb);
+    P.nb_comp.resize(n_nb);
+    P.nbedge_start.resize(static_cast<size_t>(n_nb) + 1);
+    P.nbedge_start[0] = 0;
+    P.nbedge_pt.resize(n_nbe);
+    P.nbedge_w.resize(n_nbe);
+    parallel_chunks(c_lone, 1, [&](int64_t c0, int64_t c1) {
+      std::vector<Inc> inc;
+      for (int64_t c = c0; c < c1; ++c) {
+        incidences(static_cast<int>(c), inc);
+        int32_t b = chain_m[c] - 1;
+        const int32_t q0 = P.pt_edge_start[P.comp_start[c]];
+        for (size_t k = 0; k < inc.size(); ++k) {
+          if (k == 0 || (inc[k].key >> 32) != (inc[k - 1].key >> 32)) {
+            if (k > 0) P.nbedge_start[b + 1] = q0 + static_cast<int32_t>(k);
+            ++b;
+            P.nb_pose[b] = static_cast<int32_t>(inc[k].key >> 32);
+            P.nb_comp[b] = static_cast<int32_t>(c);
+          }
+          P.nbedge_pt[q0 + k] = static_cast<int32_t>(inc[k].key & 0xffffffffu);
+          P.nbedge_w[q0 + k] = static_cast<uint32_t>(P.off_W + 18ull * inc[k].e);
+        }
+        if (!inc.empty()) P.nbedge_start[b + 1] = q0 + static_cast<int32_t>(inc.size());
+      }
+    });
   }
   {
     // a lone point's neighbour poses are its (sorted, unique) edges, one edge
@@ -624,27 +629,55 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
   // target still lists its entries in factor order.
   bool chain_ok = true;
   if (!structure_only) {
+    // A stable counting sort by point on the workers: worker w counts its
+    // contiguous range of the enumeration per point, a prefix over (point,
+    // worker) gives each worker its write offsets inside every point's run.
     std::vector<int64_t> rstart(static_cast<size_t>(P.n_pt) + 1, 0);
+    int64_t tfirst[kNTypes + 1];
+    tfirst[0] = 0;
     for (int t = 0; t < kNTypes; ++t) {
-      const TypePlan& tp = P.types[t];
-      const int nk = kNKeys[t];
-      for (int s = 0; s < nk; ++s)
-        if (kSlotKind[t][s] == 1)
-          for (int i = 0; i < tp.n; ++i) rstart[tp.idx[i * nk + s] + 1]++;
+      bool has_pt = false;
+      for (int s = 0; s < kNKeys[t]; ++s) has_pt |= kSlotKind[t][s] == 1;
+      tfirst[t + 1] = tfirst[t] + (has_pt ? P.types[t].n : 0);
     }
-    for (int32_t pt = 0; pt < P.n_pt; ++pt) rstart[pt + 1] += rstart[pt];
-    std::vector<uint64_t, default_init_allocator<uint64_t>> refs(rstart[P.n_pt]);
-    {
-      std::vector<int64_t> cur(rstart.begin(), rstart.end() - 1);
+    const int64_t ntot = tfirst[kNTypes];
+    auto walk = [&](int64_t g0, int64_t g1, auto&& fn) {   // fn(point, reference), enumeration order
       for (int t = 0; t < kNTypes; ++t) {
+        const int64_t a = std::max(g0, tfirst[t]), b = std::min(g1, tfirst[t + 1]);
         const TypePlan& tp = P.types[t];
         const int nk = kNKeys[t];
-        for (int i = 0; i < tp.n; ++i)
+        for (int64_t g = a; g < b; ++g) {
+          const int i = static_cast<int>(g - tfirst[t]);
           for (int s = 0; s < nk; ++s)
-            if (kSlotKind[t][s] == 1)
-              refs[cur[tp.idx[i * nk + s]]++] = (static_cast<uint64_t>(i) << 8) | (t << 4) | s;
+            if (kSlotKind[t][s] == 1) fn(tp.idx[i * nk + s], (static_cast<uint64_t>(i) << 8) | (t << 4) | s);
+        }
       }
-    }
+    };
+    const int nwr = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(PlanPool::get().workers(), ntot / 16384 + 1)));
+    const size_t npt = static_cast<size_t>(P.n_pt);
+    std::vector<int32_t, default_init_allocator<int32_t>> hist(static_cast<size_t>(nwr) * npt);
+    PlanPool::get().run(nwr, [&](int w) {
+      int32_t* h = hist.data() + w * npt;
+      std::fill(h, h + npt, 0);
+      walk(ntot * w / nwr, ntot * (w + 1) / nwr, [&](int32_t pt, uint64_t) { h[pt]++; });
+    });
+    parallel_for(P.n_pt, [&](int64_t p0, int64_t p1) {
+      for (int64_t pt = p0; pt < p1; ++pt) {
+        int32_t run = 0;
+        for (int w = 0; w < nwr; ++w) {
+          const int32_t c = hist[w * npt + pt];
+          hist[w * npt + pt] = run;
+          run += c;
+        }
+        rstart[pt + 1] = run;
+      }
+    });
+    for (int32_t pt = 0; pt < P.n_pt; ++pt) rstart[pt + 1] += rstart[pt];
+    std::vector<uint64_t, default_init_allocator<uint64_t>> refs(rstart[P.n_pt]);
+    PlanPool::get().run(nwr, [&](int w) {
+      int32_t* h = hist.data() + w * npt;
+      walk(ntot * w / nwr, ntot * (w + 1) / nwr, [&](int32_t pt, uint64_t r) { refs[rstart[pt] + h[pt]++] = r; });
+    });
     // a chain link (two point slots) must join consecutive points of one
     // component; its E entry goes to the lower point
     for (int t = 0; t < kNTypes; ++t) {
@@ -661,6 +694,7 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
       }
     }
     if (!chain_ok) { err = "internal: chain link not adjacent"; return DYNOHIP_ESTRUCT; }
+    plan_mark("point references by point", tmark);
     // the entries of points [p0, p1); `which` selects D (0), E (1), g_p (2) or W (3)
     auto emit_point = [&](int which, int32_t p0, int32_t p1, auto&& fn) {
       for (int32_t pt = p0; pt < p1; ++pt)
@@ -722,6 +756,7 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
         ok[q] = good;
       }
     });
+    plan_mark("lone-point eligibility", tmark);
     std::vector<int32_t> fstart(static_cast<size_t>(P.n_pose) + 1, 0), byfirst;
     for (int32_t q = 0; q < n_lone; ++q)
       if (ok[q]) fstart[P.edge_pose[P.pt_edge_start[p_lone + q]] + 1]++;

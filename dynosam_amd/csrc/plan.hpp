@@ -140,9 +140,9 @@ struct TypePlan {
   uint64_t base = 0;     // arena offset of the first record
   uint32_t stride = 0;   // doubles per record
   std::vector<int32_t> idx;   // n * nkeys (pose index or point index per slot)
-  std::vector<double> meas;   // n * meas_dim
-  std::vector<double> isig;   // n * dim (1/sigma)
-  std::vector<double> hk;     // n (Huber k, <= 0 Gaussian)
+  std::vector<double, default_init_allocator<double>> meas;    // n * meas_dim
+  std::vector<double, default_init_allocator<double>> isig;    // n * dim (1/sigma)
+  std::vector<double, default_init_allocator<double>> hk;      // n (Huber k, <= 0 Gaussian)
 };
 
 struct Plan {
@@ -229,6 +229,11 @@ struct Plan {
   std::vector<int32_t> sep_slot_ranges; // [beg, end) slot ranges of the separator columns
   std::vector<int32_t> sep_tile_ranges; // [beg, end) tile ranges (natural order) of the separators
 };
+
+// Resets `P` to a default Plan but keeps the capacity of its arrays: the
+// next build_plan of a similar graph refills memory that is already mapped
+// and touched instead of faulting fresh pages in (and freeing the old ones).
+void plan_recycle(Plan& P);
 
 // Orders the tiles (nested dissection over frame order), computes the
 // tile-level fill and the task DAG with its level schedule. With

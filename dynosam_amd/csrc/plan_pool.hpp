@@ -1,0 +1,127 @@
+// plan_pool.hpp — the host planner's worker threads (plan.cpp, tiles.cpp).
+#pragma once
+
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdint>
+#include <cstdlib>
+#include <functional>
+#include <mutex>
+#include <thread>
+
+namespace dynohip {
+
+// The planner's workers: threads created once per process and reused by
+// every plan (a plan runs a dozen parallel sections; creating 16 threads for
+// each cost milliseconds). run(nw, body) calls body(0..nw-1), body(0) on the
+// calling thread, and returns when all are done. A plan's sections come back
+// to back, so an idle worker spins on the section counter for a while before
+// it blocks on the condition variable (waking a blocked thread costs tens of
+// microseconds per section), and the caller spins until its helpers are
+// done. Never destroyed: the threads block until the process exits.
+class PlanPool {
+ public:
+  static PlanPool& get() {
+    // a forked child has none of the parent's threads: it starts its own pool
+    static PlanPool* p = nullptr;
+    static pid_t owner = 0;
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!p || owner != getpid()) {
+      p = new PlanPool();
+      owner = getpid();
+    }
+    return *p;
+  }
+  int workers() const { return nmax_; }
+  template <typename Body>
+  void run(int nw, Body&& body) {
+    nw = std::max(1, std::min(nw, nmax_));
+    if (nw == 1) {
+      body(0);
+      return;
+    }
+    std::unique_lock<std::mutex> call(call_mu_);   // one parallel section at a time
+    std::function<void(int)> fn = [&body](int r) { body(r); };
+    fn_ = &fn;
+    pending_.store(nw - 1, std::memory_order_relaxed);
+    {
+      // the section word carries its worker count: a worker decides from the
+      // word it saw, never from a later section's
+      std::lock_guard<std::mutex> lk(mu_);
+      gen_.store(((gen_.load(std::memory_order_relaxed) >> 8) + 1) << 8 | static_cast<uint64_t>(nw),
+                 std::memory_order_release);
+    }
+    if (sleepers_.load(std::memory_order_acquire) > 0) cv_.notify_all();
+    body(0);
+    while (pending_.load(std::memory_order_acquire) != 0) pause();
+    fn_ = nullptr;
+  }
+
+ private:
+  static void pause() {
+#if defined(__x86_64__)
+    __builtin_ia32_pause();
+#endif
+  }
+  PlanPool() {
+    const unsigned hc = std::thread::hardware_concurrency();
+    nmax_ = static_cast<int>(std::max(1u, std::min(16u, hc ? hc : 1u)));
+    // DYNOHIP_PLAN_WORKERS caps the pool (1 = the single-threaded build the
+    // parallel sections must reproduce bit for bit; tests/test_plan_digest.py)
+    if (const char* e = std::getenv("DYNOHIP_PLAN_WORKERS"))
+      nmax_ = std::max(1, std::min(nmax_, std::atoi(e)));
+    // DYNOHIP_PLAN_SPIN_US: how long an idle worker spins before it blocks
+    if (const char* e = std::getenv("DYNOHIP_PLAN_SPIN_US")) spin_us_ = std::max(0, std::atoi(e));
+    for (int r = 1; r < nmax_; ++r) std::thread([this, r] { loop(r); }).detach();
+  }
+  void loop(int r) {
+    uint64_t seen = 0;
+    for (;;) {
+      // spin for the next section a while, then block
+      uint64_t g = gen_.load(std::memory_order_acquire);
+      if (g == seen && spin_us_ > 0) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int k = 1; (g = gen_.load(std::memory_order_acquire)) == seen; ++k) {
+          pause();
+          if ((k & 255) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us_)) break;
+        }
+      }
+      if (g == seen) {
+        std::unique_lock<std::mutex> lk(mu_);
+        sleepers_.fetch_add(1, std::memory_order_acq_rel);
+        cv_.wait(lk, [&] { return (g = gen_.load(std::memory_order_acquire)) != seen; });
+        sleepers_.fetch_sub(1, std::memory_order_acq_rel);
+      }
+      seen = g;
+      if (r >= static_cast<int>(g & 255)) continue;
+      (*fn_)(r);
+      pending_.fetch_sub(1, std::memory_order_acq_rel);
+    }
+  }
+  int nmax_ = 1, spin_us_ = 500;
+  std::mutex call_mu_, mu_;
+  std::condition_variable cv_;
+  std::function<void(int)>* fn_ = nullptr;
+  std::atomic<int> pending_{0}, sleepers_{0};
+  std::atomic<uint64_t> gen_{0};
+};
+
+// body(b, e) over chunks of [0, n) handed out one at a time (work of uneven
+// size per item, e.g. chains sorted longest first)
+template <typename Body>
+void parallel_chunks(int64_t n, int64_t chunk, Body&& body) {
+  const int64_t nch = (n + chunk - 1) / chunk;
+  const int nw = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(PlanPool::get().workers(), nch)));
+  std::atomic<int64_t> next{0};
+  PlanPool::get().run(nw, [&](int) {
+    for (int64_t k; (k = next.fetch_add(1, std::memory_order_relaxed)) < nch;)
+      body(k * chunk, std::min(n, (k + 1) * chunk));
+  });
+}
+
+}  // namespace dynohip

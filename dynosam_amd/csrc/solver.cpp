@@ -226,6 +226,44 @@ struct GraphCopy {
   }
 };
 
+// The host side of a destroyed handle (its plan and graph copy) kept for the
+// next handle: a full-batch call per frame creates a handle, plans, solves
+// and destroys it, and freeing then re-faulting tens of MB of host arrays
+// cost milliseconds each way (destroy 3.5 ms at C2). One slot; trimmed by
+// dynohip_pool_trim.
+struct HostCache {
+  static HostCache& get() {
+    static HostCache* c = new HostCache();
+    return *c;
+  }
+  void give(Plan& p, GraphCopy& g) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (has) return;
+    plan = std::move(p);
+    graph = std::move(g);
+    has = true;
+  }
+  void take(Plan& p, GraphCopy& g) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (!has) return;
+    p = std::move(plan);
+    g = std::move(graph);
+    plan = Plan();
+    graph = GraphCopy();
+    has = false;
+  }
+  void trim() {
+    std::lock_guard<std::mutex> lk(mu);
+    plan = Plan();
+    graph = GraphCopy();
+    has = false;
+  }
+  std::mutex mu;
+  Plan plan;
+  GraphCopy graph;
+  bool has = false;
+};
+
 struct TypeBufs {
   DevBuf<int32_t> idx;
   DevBuf<double> meas, isig, hk;
@@ -984,6 +1022,7 @@ int dynohip_create(int device_id, dynohip_solver** out) {
     }
   }
   dynohip_solver* s = new dynohip_solver();
+  HostCache::get().take(s->plan, s->graph);   // stale contents: has_graph / has_plan are false
   s->device = device_id;
   if (const char* e = std::getenv("DYNOHIP_LINERR_DIRECT")) s->linerr_direct = std::atoi(e) != 0;
   s->stream = r.stream;
@@ -1010,6 +1049,8 @@ void dynohip_destroy(dynohip_solver* s) {
   (void)hipSetDevice(s->device);
   if (s->stream) (void)hipStreamSynchronize(s->stream);
   if (s->side) (void)hipStreamSynchronize(s->side);
+  static const bool timing = std::getenv("DYNOHIP_PLAN_TIMING") != nullptr;
+  const auto t0 = std::chrono::steady_clock::now();
   HandleRes r;
   r.device = s->device;
   r.stream = s->stream;
@@ -1020,10 +1061,17 @@ void dynohip_destroy(dynohip_solver* s) {
   for (int k = 0; k < 9; ++k) r.ev[k] = s->ev[k];
   r.hres = s->hres;
   if (r.stream) ResPool::get().give(r);
+  HostCache::get().give(s->plan, s->graph);
+  const auto t1 = std::chrono::steady_clock::now();
   delete s;
+  if (timing)
+    std::fprintf(stderr, "[destroy] sync+pool %.2f ms, delete %.2f ms\n",
+                 std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count());
 }
 
 int dynohip_pool_trim(void) {
+  HostCache::get().trim();
   const size_t n = DevPool::get().trim();
   return static_cast<int>(std::min<size_t>(n >> 20, 0x7fffffff));
 }
@@ -1034,20 +1082,22 @@ int dynohip_set_graph(dynohip_solver* s, const dynohip_graph_view* g) {
   if (!s || !g) return DYNOHIP_EINVAL;
   const dynohip_factor_block* b[kNTypes] = {&g->pose_to_point, &g->landmark_motion_ternary, &g->between,
                                             &g->prior, &g->landmark_motion_pose, &g->landmark_pose_smoothing};
-  GraphCopy gc;
+  for (int t = 0; t < kNTypes; ++t)
+    if (b[t]->n && (!b[t]->keys || !b[t]->sigmas || (kMeasDim[t] && !b[t]->measured)))
+      return set_err(s, DYNOHIP_EINVAL, "factor type %d: null keys/sigmas/measured", t);
+  // copied into the handle's arrays (their capacity is reused across graphs)
+  GraphCopy& gc = s->graph;
+  s->has_graph = false;
   for (int t = 0; t < kNTypes; ++t) {
     const size_t n = b[t]->n;
     gc.n[t] = n;
-    if (n == 0) continue;
-    if (!b[t]->keys || !b[t]->sigmas || (kMeasDim[t] && !b[t]->measured))
-      return set_err(s, DYNOHIP_EINVAL, "factor type %d: null keys/sigmas/measured", t);
     gc.keys[t].assign(b[t]->keys, b[t]->keys + n * kNKeys[t]);
-    if (kMeasDim[t]) gc.meas[t].assign(b[t]->measured, b[t]->measured + n * kMeasDim[t]);
+    if (kMeasDim[t] && n) gc.meas[t].assign(b[t]->measured, b[t]->measured + n * kMeasDim[t]);
+    else gc.meas[t].clear();
     gc.sig[t].assign(b[t]->sigmas, b[t]->sigmas + n * kDim[t]);
     if (b[t]->huber_k) gc.hub[t].assign(b[t]->huber_k, b[t]->huber_k + n);
     else gc.hub[t].assign(n, 0.0);
   }
-  s->graph = std::move(gc);
   s->has_graph = true;
   s->lin_valid = false;
   s->has_plan = false;
@@ -1062,6 +1112,7 @@ int dynohip_set_values(dynohip_solver* s, const uint64_t* keys, const uint8_t* k
   const bool same = s->has_plan && s->value_keys.size() == n &&
                     std::equal(s->value_keys.begin(), s->value_keys.end(), keys);
   if (!same) {
+    const auto tb0 = std::chrono::steady_clock::now();
     s->has_plan = false;
     dynohip_graph_view g = s->graph.view();
     int rc = s->nranks > 1 ? build_partitioned_plan(g, keys, kind, n, s->nranks, s->rank, s->plan, s->part,
@@ -1070,6 +1121,9 @@ int dynohip_set_values(dynohip_solver* s, const uint64_t* keys, const uint8_t* k
     if (rc) return rc;
     static const bool timing = std::getenv("DYNOHIP_PLAN_TIMING") != nullptr;
     const auto t0 = std::chrono::steady_clock::now();
+    if (timing)
+      std::fprintf(stderr, "[plan] build_plan (set_values)     %8.2f ms\n",
+                   std::chrono::duration<double, std::milli>(t0 - tb0).count());
     rc = upload_plan(s);
     if (rc) return rc;
     if (timing) {
@@ -1088,6 +1142,8 @@ int dynohip_set_values(dynohip_solver* s, const uint64_t* keys, const uint8_t* k
     s->base_stats_valid = false;
   }
   s->lin_valid = false;
+  static const bool vtiming = std::getenv("DYNOHIP_PLAN_TIMING") != nullptr;
+  const auto tv0 = std::chrono::steady_clock::now();
   Plan& P = s->plan;
   std::vector<double> hp(12ull * P.n_pose), hq(3ull * P.n_pt);
   size_t off = 0;
@@ -1110,7 +1166,13 @@ int dynohip_set_values(dynohip_solver* s, const uint64_t* keys, const uint8_t* k
   if (!hq.empty()) HIPCHK(s, hipMemcpyAsync(s->pt.p, hq.data(), hq.size() * sizeof(double), hipMemcpyHostToDevice, s->stream));
   HIPCHK(s, hipStreamSynchronize(s->stream));
   s->has_values = true;
-  return dynohip_lm_reset(s, &s->prm);
+  const auto tv1 = std::chrono::steady_clock::now();
+  const int rc = dynohip_lm_reset(s, &s->prm);
+  if (vtiming)
+    std::fprintf(stderr, "[values] scatter+upload %.2f ms, initial error %.2f ms\n",
+                 std::chrono::duration<double, std::milli>(tv1 - tv0).count(),
+                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tv1).count());
+  return rc;
 }
 
 int dynohip_get_values(dynohip_solver* s, double* out, size_t n_doubles) {

@@ -38,6 +38,7 @@
 #include <vector>
 
 #include "plan.hpp"
+#include "plan_pool.hpp"
 
 namespace dynohip {
 
@@ -628,11 +629,9 @@ bool build_tile_schedule(Plan& P) {
       leaves.push_back(leaf);
     }
     std::vector<Sched> cand(leaves.size());
-    std::vector<std::thread> th;
-    for (size_t c = 1; c < leaves.size(); ++c)
-      th.emplace_back([&, c] { schedule(NT, adj, maxnb, leaves[c], cand[c], nr); });
-    schedule(NT, adj, maxnb, leaves[0], cand[0], nr);
-    for (auto& t : th) t.join();
+    parallel_chunks(static_cast<int64_t>(leaves.size()), 1, [&](int64_t c0, int64_t c1) {
+      for (int64_t c = c0; c < c1; ++c) schedule(NT, adj, maxnb, leaves[c], cand[c], nr);
+    });
     if (!cand[0].ok) return false;
     size_t bi = 0;
     for (size_t c = 1; c < cand.size(); ++c)

@@ -1,0 +1,42 @@
+"""The host planner's parallel sections (csrc/plan.cpp: target-range gather
+builds, per-worker counting sorts, chunked layout passes) reproduce the
+single-threaded build bit for bit, and a plan rebuilt into recycled arrays
+equals a fresh one: every plan field's digest
+(dynohip_plan_export "digest") with the pool capped at one worker
+(DYNOHIP_PLAN_WORKERS=1, in a child process: the pool is process-wide) equals
+the digest with the default pool. Host only."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_plan_is_independent_of_planner_workers(tmp_path):
+    path = str(tmp_path / "one_worker.npz")
+    env = dict(os.environ, DYNOHIP_PLAN_WORKERS="1")
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "plan_digest.py"), "save", path], env=env,
+                   check=True, timeout=600)
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import plan_digest
+    many = plan_digest.digests()
+    one = np.load(path)
+    assert sorted(many) == sorted(one.files)
+    for k, x in many.items():
+        y = one[k]
+        assert x.shape == y.shape, k
+        diff = np.nonzero((x.reshape(-1, 2) != y.reshape(-1, 2)).any(1))[0]
+        assert diff.size == 0, "%s: fields %s differ" % (k, diff.tolist())
+
+
+def test_recycled_plan_equals_fresh_plan():
+    """build_plan into a Plan that held a plan already (plan_recycle keeps
+    its arrays' capacity) gives the same plan as a fresh build."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import plan_digest
+    fresh, again = plan_digest.digests(), plan_digest.digests("@recycled")
+    for k, x in fresh.items():
+        diff = np.nonzero((x.reshape(-1, 2) != again[k].reshape(-1, 2)).any(1))[0]
+        assert diff.size == 0, "%s: fields %s differ" % (k, diff.tolist())
