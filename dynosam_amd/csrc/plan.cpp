@@ -443,28 +443,26 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
   {
     // bucket (point, pose) incidences by point, then sort + unique each
     // point's (short) pose list: the (point, pose)-sorted unique edge list
-    // (counted and placed on the workers with atomic cursors: the order
-    // inside a point's list does not matter, it is sorted next)
+    // (serial: shared counters on the workers measured slower on the GPU
+    // box's host, whose cores do not share one cache)
     std::vector<int32_t> cnt(P.n_pt + 1, 0);
     auto each = [&](auto&& fn) {
       for (int t = 0; t < kNTypes; ++t) {
         const TypePlan& tp = P.types[t];
         const int nk = kNKeys[t];
-        parallel_for(tp.n, [&](int64_t i0, int64_t i1) {
-          for (int64_t i = i0; i < i1; ++i)
-            for (int sa = 0; sa < nk; ++sa)
-              if (kSlotKind[t][sa] == 1)
-                for (int sb = 0; sb < nk; ++sb)
-                  if (kSlotKind[t][sb] == 0) fn(tp.idx[i * nk + sa], tp.idx[i * nk + sb]);
-        });
+        for (int i = 0; i < tp.n; ++i)
+          for (int sa = 0; sa < nk; ++sa)
+            if (kSlotKind[t][sa] == 1)
+              for (int sb = 0; sb < nk; ++sb)
+                if (kSlotKind[t][sb] == 0) fn(tp.idx[i * nk + sa], tp.idx[i * nk + sb]);
       }
     };
-    each([&](int32_t pt, int32_t) { __atomic_fetch_add(&cnt[pt + 1], 1, __ATOMIC_RELAXED); });
+    each([&](int32_t pt, int32_t) { cnt[pt + 1]++; });
     for (int i = 0; i < P.n_pt; ++i) cnt[i + 1] += cnt[i];
     std::vector<int32_t, default_init_allocator<int32_t>> poses(cnt[P.n_pt]);
     {
       std::vector<int32_t> cur(cnt.begin(), cnt.end() - 1);
-      each([&](int32_t pt, int32_t pose) { poses[__atomic_fetch_add(&cur[pt], 1, __ATOMIC_RELAXED)] = pose; });
+      each([&](int32_t pt, int32_t pose) { poses[cur[pt]++] = pose; });
     }
     // per point (in parallel): sort + unique its poses in place, then the
     // prefix of the unique counts places every point's edges
@@ -535,7 +533,7 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
       std::sort(inc.begin(), inc.end(), [](const Inc& a, const Inc& b) { return a.key < b.key; });
     };
     std::vector<int32_t> chain_m(static_cast<size_t>(c_lone) + 1, 0);
-    parallel_chunks(c_lone, 1, [&](int64_t c0, int64_t c1) {
+    parallel_chunks(c_lone, 16, [&](int64_t c0, int64_t c1) {
       std::vector<Inc> inc;
       for (int64_t c = c0; c < c1; ++c) {
         incidences(static_cast<int>(c), inc);
@@ -560,7 +558,7 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
     P.nbedge_start[0] = 0;
     P.nbedge_pt.resize(n_nbe);
     P.nbedge_w.resize(n_nbe);
-    parallel_chunks(c_lone, 1, [&](int64_t c0, int64_t c1) {
+    parallel_chunks(c_lone, 16, [&](int64_t c0, int64_t c1) {
       std::vector<Inc> inc;
       for (int64_t c = c0; c < c1; ++c) {
         incidences(static_cast<int>(c), inc);
@@ -620,6 +618,116 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
   P.arena_size = arena;
   if (arena >= (1ull << 32)) { err = "graph too large for 32-bit arena offsets"; return DYNOHIP_ESTRUCT; }
 
+  plan_mark("before reduced system structure", tmark);
+  // ---- reduced system structure ----
+  // Pose-pair blocks (A >= B) of the reduced system: every diagonal (for the
+  // damping), the pose pairs of every factor and the neighbour-pose pairs of
+  // every point component, numbered in (B, A) order (band column order).
+  // pair index: dense rows of width (max A - B) + 1 when that is small,
+  // a hash map otherwise. The distinct pairs are the factor pose pairs and
+  // the (a, b) neighbour pairs of every component (each neighbour pose has
+  // at least one edge), so marking does not walk the edge lists.
+  auto each_distinct = [&](auto&& fn) {
+    for (int t = 0; t < kNTypes; ++t) {
+      const TypePlan& tp = P.types[t];
+      const int nk = kNKeys[t];
+      if (kNPoseSlots[t] < 2) continue;
+      for (int i = 0; i < tp.n; ++i)
+        for (int sa = 0; sa < nk; ++sa)
+          if (kSlotKind[t][sa] == 0)
+            for (int sb = 0; sb < nk; ++sb)
+              if (kSlotKind[t][sb] == 0 && tp.idx[i * nk + sa] >= tp.idx[i * nk + sb])
+                fn(tp.idx[i * nk + sa], tp.idx[i * nk + sb]);
+    }
+    for (int c = 0; c < P.n_comp; ++c) {
+      const int32_t nb0 = P.comp_nb_start[c], m = P.comp_nb_start[c + 1] - nb0;
+      for (int a = 0; a < m; ++a)
+        for (int b = 0; b <= a; ++b) fn(P.nb_pose[nb0 + a], P.nb_pose[nb0 + b]);
+    }
+  };
+  int32_t W = 0;
+  for (int t = 0; t < kNTypes; ++t) {
+    const TypePlan& tp = P.types[t];
+    const int nk = kNKeys[t];
+    if (kNPoseSlots[t] < 2) continue;
+    for (int i = 0; i < tp.n; ++i)
+      for (int sa = 0; sa < nk; ++sa)
+        for (int sb = 0; sb < nk; ++sb)
+          if (kSlotKind[t][sa] == 0 && kSlotKind[t][sb] == 0)
+            W = std::max(W, tp.idx[i * nk + sa] - tp.idx[i * nk + sb]);
+  }
+  for (int c = 0; c < P.n_comp; ++c) {  // nb poses are sorted per component
+    const int32_t nb0 = P.comp_nb_start[c], nb1 = P.comp_nb_start[c + 1];
+    if (nb1 > nb0) W = std::max(W, P.nb_pose[nb1 - 1] - P.nb_pose[nb0]);
+  }
+  const int64_t span = static_cast<int64_t>(W) + 1;
+  const bool dense = static_cast<int64_t>(P.n_pose) * span <= (int64_t{1} << 26);
+  std::vector<int32_t> id_dense;
+  std::unordered_map<uint64_t, int32_t> id_map;
+  auto pkey = [](int32_t A, int32_t B) { return (static_cast<uint64_t>(B) << 32) | static_cast<uint32_t>(A); };
+  if (dense) id_dense.assign(static_cast<size_t>(P.n_pose) * span, -1);
+  auto mark = [&](int32_t A, int32_t B) {
+    if (dense) id_dense[static_cast<size_t>(A) * span + (A - B)] = 0;
+    else id_map.emplace(pkey(A, B), 0);
+  };
+  for (int32_t A = 0; A < P.n_pose; ++A) mark(A, A);
+  each_distinct(mark);
+  P.red_A.clear();
+  P.red_B.clear();
+  if (dense) {
+    for (int32_t B = 0; B < P.n_pose; ++B)
+      for (int32_t A = B; A < P.n_pose && A - B < span; ++A) {
+        int32_t& id = id_dense[static_cast<size_t>(A) * span + (A - B)];
+        if (id < 0) continue;
+        id = static_cast<int32_t>(P.red_A.size());
+        P.red_A.push_back(A);
+        P.red_B.push_back(B);
+      }
+  } else {
+    std::vector<uint64_t> ks;
+    ks.reserve(id_map.size());
+    for (const auto& kv : id_map) ks.push_back(kv.first);
+    std::sort(ks.begin(), ks.end());  // (B, A) order
+    for (uint64_t k : ks) {
+      id_map[k] = static_cast<int32_t>(P.red_A.size());
+      P.red_A.push_back(static_cast<int32_t>(k & 0xffffffffu));
+      P.red_B.push_back(static_cast<int32_t>(k >> 32));
+    }
+  }
+  auto tid = [&](int32_t A, int32_t B) -> int32_t {
+    return dense ? id_dense[static_cast<size_t>(A) * span + (A - B)] : id_map.at(pkey(A, B));
+  };
+  // ---- band layout ----
+  P.n_red = 6 * P.n_pose;
+  P.NT = (P.n_red + kTile - 1) / kTile;
+  std::vector<int32_t> rlow(P.NT);
+  for (int j = 0; j < P.NT; ++j) rlow[j] = j;
+  for (size_t t = 0; t < P.red_A.size(); ++t) {
+    const int r1 = (6 * P.red_A[t] + 5) / kTile;
+    const int c0 = (6 * P.red_B[t]) / kTile, c1 = (6 * P.red_B[t] + 5) / kTile;
+    for (int j = c0; j <= c1; ++j) rlow[j] = std::max(rlow[j], r1);
+  }
+  for (int j = 1; j < P.NT; ++j) rlow[j] = std::max(rlow[j], rlow[j - 1]);
+  P.band_D.resize(P.NT);
+  P.max_D = 0;
+  for (int j = 0; j < P.NT; ++j) {
+    P.band_D[j] = rlow[j] - j;
+    P.max_D = std::max(P.max_D, P.band_D[j]);
+  }
+  // The tile schedule depends on the pose-pair structure alone: it is built
+  // on a thread of its own while this one builds the gather lists (the
+  // schedule writes only its own Plan fields; joined before the target slots)
+  bool sched_ok = true;
+  std::thread sched;
+  struct Joiner {
+    std::thread& t;
+    ~Joiner() {
+      if (t.joinable()) t.join();
+    }
+  } sched_join{sched};
+  if (with_schedule) sched = std::thread([&P, &sched_ok] { sched_ok = build_tile_schedule(P, true); });
+  plan_mark("reduced system structure, band", tmark);
+
   plan_mark("before point-side gathers", tmark);
   std::vector<uint8_t> lone_grouped(P.n_pt, 0);   // per point: in a lone-point group
   // ---- point-side gathers (CSR builds run on worker threads) ----
@@ -629,55 +737,29 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
   // target still lists its entries in factor order.
   bool chain_ok = true;
   if (!structure_only) {
-    // A stable counting sort by point on the workers: worker w counts its
-    // contiguous range of the enumeration per point, a prefix over (point,
-    // worker) gives each worker its write offsets inside every point's run.
+    // (a serial counting sort: per-worker histograms scatter into shared
+    // lines and measured slower on the GPU box's host)
     std::vector<int64_t> rstart(static_cast<size_t>(P.n_pt) + 1, 0);
-    int64_t tfirst[kNTypes + 1];
-    tfirst[0] = 0;
     for (int t = 0; t < kNTypes; ++t) {
-      bool has_pt = false;
-      for (int s = 0; s < kNKeys[t]; ++s) has_pt |= kSlotKind[t][s] == 1;
-      tfirst[t + 1] = tfirst[t] + (has_pt ? P.types[t].n : 0);
+      const TypePlan& tp = P.types[t];
+      const int nk = kNKeys[t];
+      for (int s = 0; s < nk; ++s)
+        if (kSlotKind[t][s] == 1)
+          for (int i = 0; i < tp.n; ++i) rstart[tp.idx[i * nk + s] + 1]++;
     }
-    const int64_t ntot = tfirst[kNTypes];
-    auto walk = [&](int64_t g0, int64_t g1, auto&& fn) {   // fn(point, reference), enumeration order
-      for (int t = 0; t < kNTypes; ++t) {
-        const int64_t a = std::max(g0, tfirst[t]), b = std::min(g1, tfirst[t + 1]);
-        const TypePlan& tp = P.types[t];
-        const int nk = kNKeys[t];
-        for (int64_t g = a; g < b; ++g) {
-          const int i = static_cast<int>(g - tfirst[t]);
-          for (int s = 0; s < nk; ++s)
-            if (kSlotKind[t][s] == 1) fn(tp.idx[i * nk + s], (static_cast<uint64_t>(i) << 8) | (t << 4) | s);
-        }
-      }
-    };
-    const int nwr = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(PlanPool::get().workers(), ntot / 16384 + 1)));
-    const size_t npt = static_cast<size_t>(P.n_pt);
-    std::vector<int32_t, default_init_allocator<int32_t>> hist(static_cast<size_t>(nwr) * npt);
-    PlanPool::get().run(nwr, [&](int w) {
-      int32_t* h = hist.data() + w * npt;
-      std::fill(h, h + npt, 0);
-      walk(ntot * w / nwr, ntot * (w + 1) / nwr, [&](int32_t pt, uint64_t) { h[pt]++; });
-    });
-    parallel_for(P.n_pt, [&](int64_t p0, int64_t p1) {
-      for (int64_t pt = p0; pt < p1; ++pt) {
-        int32_t run = 0;
-        for (int w = 0; w < nwr; ++w) {
-          const int32_t c = hist[w * npt + pt];
-          hist[w * npt + pt] = run;
-          run += c;
-        }
-        rstart[pt + 1] = run;
-      }
-    });
     for (int32_t pt = 0; pt < P.n_pt; ++pt) rstart[pt + 1] += rstart[pt];
     std::vector<uint64_t, default_init_allocator<uint64_t>> refs(rstart[P.n_pt]);
-    PlanPool::get().run(nwr, [&](int w) {
-      int32_t* h = hist.data() + w * npt;
-      walk(ntot * w / nwr, ntot * (w + 1) / nwr, [&](int32_t pt, uint64_t r) { refs[rstart[pt] + h[pt]++] = r; });
-    });
+    {
+      std::vector<int64_t> cur(rstart.begin(), rstart.end() - 1);
+      for (int t = 0; t < kNTypes; ++t) {
+        const TypePlan& tp = P.types[t];
+        const int nk = kNKeys[t];
+        for (int i = 0; i < tp.n; ++i)
+          for (int s = 0; s < nk; ++s)
+            if (kSlotKind[t][s] == 1)
+              refs[cur[tp.idx[i * nk + s]]++] = (static_cast<uint64_t>(i) << 8) | (t << 4) | s;
+      }
+    }
     // a chain link (two point slots) must join consecutive points of one
     // component; its E entry goes to the lower point
     for (int t = 0; t < kNTypes; ++t) {
@@ -871,47 +953,44 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
     // enumerations below run once per worker and pass: they skip the grouped
     // ones without visiting them)
     std::vector<int32_t> keep0;
-    keep0.reserve(P.types[0].n);
-    for (int i = 0; i < P.types[0].n; ++i)
-      if (!lone_grouped[P.types[0].idx[2 * i + 1]]) keep0.push_back(i);
-    auto for_factors = [&](int t, auto&& fn) {
-      if (t == 0) {
-        for (int32_t i : keep0) fn(i);
-      } else {
-        for (int i = 0; i < P.types[t].n; ++i) fn(i);
-      }
-    };
-    auto emit_factor_pairs = [&](auto&& pair_fn) {  // pair_fn(A, B, entry)
-      for (int t = 0; t < kNTypes; ++t) {
-        const TypePlan& tp = P.types[t];
-        const int nk = kNKeys[t], d = kDim[t];
-        for_factors(t, [&](int i) {
-          for (int sa = 0; sa < nk; ++sa) {
-            if (kSlotKind[t][sa] != 0) continue;
-            const int32_t A = tp.idx[i * nk + sa];
-            for (int sb = 0; sb < nk; ++sb) {
-              if (kSlotKind[t][sb] != 0) continue;
-              const int32_t B = tp.idx[i * nk + sb];
-              if (A < B) continue;
-              pair_fn(A, B, GEntry{block_off(tp, t, i, sa), block_off(tp, t, i, sb), d, 1});
-            }
-          }
-        });
-      }
-    };
-    // the lone-point groups' partial blocks (after every factor and component)
-    auto emit_group_pairs = [&](int32_t blo, int32_t bhi, auto&& pair_fn) {
-      for (const LoneGroup& G : P.lgroup) {
-        const int32_t* ps = P.lone_pose.data() + G.pose_beg;
-        if (ps[G.m - 1] < blo || ps[0] > bhi) continue;
-        for (int a = 0; a < G.m; ++a)
-          for (int b = 0; b <= a; ++b)
-            pair_fn(ps[a], ps[b], GEntry{static_cast<uint32_t>(P.off_I6), G.out + 36u * (a * (a + 1) / 2 + b), 6, 1});
-      }
-    };
+    {
+      // (an ordered filter on the workers: count per chunk, then fill)
+      const int64_t n0 = P.types[0].n;
+      const int nw = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(PlanPool::get().workers(), n0 / 16384 + 1)));
+      std::vector<int64_t> kc(static_cast<size_t>(nw) + 1, 0);
+      auto keep = [&](int64_t i) { return !lone_grouped[P.types[0].idx[2 * i + 1]]; };
+      PlanPool::get().run(nw, [&](int w) {
+        int64_t c = 0;
+        for (int64_t i = n0 * w / nw; i < n0 * (w + 1) / nw; ++i) c += keep(i);
+        kc[w + 1] = c;
+      });
+      for (int w = 0; w < nw; ++w) kc[w + 1] += kc[w];
+      keep0.resize(kc[nw]);
+      PlanPool::get().run(nw, [&](int w) {
+        int64_t o = kc[w];
+        for (int64_t i = n0 * w / nw; i < n0 * (w + 1) / nw; ++i)
+          if (keep(i)) keep0[o++] = static_cast<int32_t>(i);
+      });
+    }
     auto comp_grouped = [&](int c) {
       return P.comp_start[c + 1] - P.comp_start[c] == 1 && lone_grouped[P.comp_start[c]];
     };
+    // pose pairs (A >= B) of factor i of type t
+    auto factor_pairs = [&](int t, int i, auto&& pair_fn) {  // pair_fn(A, B, entry)
+      const TypePlan& tp = P.types[t];
+      const int nk = kNKeys[t], d = kDim[t];
+      for (int sa = 0; sa < nk; ++sa) {
+        if (kSlotKind[t][sa] != 0) continue;
+        const int32_t A = tp.idx[i * nk + sa];
+        for (int sb = 0; sb < nk; ++sb) {
+          if (kSlotKind[t][sb] != 0) continue;
+          const int32_t B = tp.idx[i * nk + sb];
+          if (A < B) continue;
+          pair_fn(A, B, GEntry{block_off(tp, t, i, sa), block_off(tp, t, i, sb), d, 1});
+        }
+      }
+    };
+    // the neighbour-pose pairs of component c
     auto emit_comp_pairs = [&](int c, auto&& pair_fn) {
       const int32_t nb0 = P.comp_nb_start[c], m = P.comp_nb_start[c + 1] - nb0;
       for (int a = 0; a < m; ++a) {
@@ -926,154 +1005,100 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
         }
       }
     };
-    // gradient gathers per pose: J_A^T b per factor, then -W_A v per
-    // component (components without a neighbour pose in [p0, p1) skipped)
-    auto emit_grad = [&](auto&& fn, int64_t p0, int64_t p1) {
-      for (int t = 0; t < kNTypes; ++t) {
-        const TypePlan& tp = P.types[t];
-        const int nk = kNKeys[t], d = kDim[t];
-        for_factors(t, [&](int i) {
-          for (int sa = 0; sa < nk; ++sa)
-            if (kSlotKind[t][sa] == 0) fn(tp.idx[i * nk + sa], GEntry{block_off(tp, t, i, sa), b_off(tp, t, i), d, 1});
-        });
+    // The sources of both reduced-system lists in enumeration order: the
+    // factors (type-major, each type in factor order; the PoseToPoint factors
+    // of grouped lone points are left out, their blocks come through the
+    // groups), then the components (grouped lone points and components
+    // without neighbour poses emit nothing), then the lone-point groups.
+    int64_t ffirst[kNTypes + 1];
+    ffirst[0] = 0;
+    for (int t = 0; t < kNTypes; ++t)
+      ffirst[t + 1] = ffirst[t] + (t == 0 ? static_cast<int64_t>(keep0.size()) : P.types[t].n);
+    const int64_t nF = ffirst[kNTypes], nC = P.n_comp, nG = static_cast<int64_t>(P.lgroup.size());
+    const int64_t nsrc = nF + nC + nG;
+    auto visit = [&](int64_t s0, int64_t s1, auto&& on_factor, auto&& on_comp, auto&& on_group) {
+      for (int t = 0; t < kNTypes; ++t)
+        for (int64_t s = std::max(s0, ffirst[t]); s < std::min(s1, ffirst[t + 1]); ++s)
+          on_factor(t, t == 0 ? keep0[s] : static_cast<int>(s - ffirst[t]));
+      for (int64_t s = std::max(s0, nF); s < std::min(s1, nF + nC); ++s) {
+        const int c = static_cast<int>(s - nF);
+        if (P.comp_nb_start[c + 1] == P.comp_nb_start[c] || comp_grouped(c)) continue;
+        on_comp(c);
       }
-      for (int c = 0; c < P.n_comp; ++c) {
-        const int32_t nb0 = P.comp_nb_start[c], m = P.comp_nb_start[c + 1] - nb0;
-        if (m == 0 || P.nb_pose[nb0 + m - 1] < p0 || P.nb_pose[nb0] >= p1 || comp_grouped(c)) continue;
-        for (int a = 0; a < m; ++a)
-          for (int32_t q = P.nbedge_start[nb0 + a]; q < P.nbedge_start[nb0 + a + 1]; ++q)
-            fn(P.nb_pose[nb0 + a], GEntry{P.nbedge_w[q], static_cast<uint32_t>(P.off_v + 3ull * (P.comp_start[c] + P.nbedge_pt[q])), 3, -1});
-      }
-      for (const LoneGroup& G : P.lgroup) {
-        const int32_t* ps = P.lone_pose.data() + G.pose_beg;
-        if (ps[G.m - 1] < p0 || ps[0] >= p1) continue;
-        const uint32_t g0 = G.out + 36u * (G.m * (G.m + 1) / 2);
-        for (int a = 0; a < G.m; ++a) fn(ps[a], GEntry{static_cast<uint32_t>(P.off_I6), g0 + 6u * a, 6, 1});
-      }
+      for (int64_t s = std::max(s0, nF + nC); s < s1; ++s) on_group(P.lgroup[s - nF - nC]);
     };
-    // pair index: dense rows of width (max A - B) + 1 when that is small,
-    // a hash map otherwise. The distinct pairs are the factor pose pairs and
-    // the (a, b) neighbour pairs of every component (each neighbour pose has
-    // at least one edge), so marking does not walk the edge lists.
-    auto each_distinct = [&](auto&& fn) {
-      for (int t = 0; t < kNTypes; ++t) {
-        const TypePlan& tp = P.types[t];
-        const int nk = kNKeys[t];
-        if (kNPoseSlots[t] < 2) continue;
-        for (int i = 0; i < tp.n; ++i)
-          for (int sa = 0; sa < nk; ++sa)
-            if (kSlotKind[t][sa] == 0)
-              for (int sb = 0; sb < nk; ++sb)
-                if (kSlotKind[t][sb] == 0 && tp.idx[i * nk + sa] >= tp.idx[i * nk + sb])
-                  fn(tp.idx[i * nk + sa], tp.idx[i * nk + sb]);
-      }
-      for (int c = 0; c < P.n_comp; ++c) {
-        const int32_t nb0 = P.comp_nb_start[c], m = P.comp_nb_start[c + 1] - nb0;
-        for (int a = 0; a < m; ++a)
-          for (int b = 0; b <= a; ++b) fn(P.nb_pose[nb0 + a], P.nb_pose[nb0 + b]);
-      }
-    };
-    int32_t W = 0;
-    for (int t = 0; t < kNTypes; ++t) {
-      const TypePlan& tp = P.types[t];
-      const int nk = kNKeys[t];
-      if (kNPoseSlots[t] < 2) continue;
-      for (int i = 0; i < tp.n; ++i)
-        for (int sa = 0; sa < nk; ++sa)
-          for (int sb = 0; sb < nk; ++sb)
-            if (kSlotKind[t][sa] == 0 && kSlotKind[t][sb] == 0)
-              W = std::max(W, tp.idx[i * nk + sa] - tp.idx[i * nk + sb]);
-    }
-    for (int c = 0; c < P.n_comp; ++c) {  // nb poses are sorted per component
-      const int32_t nb0 = P.comp_nb_start[c], nb1 = P.comp_nb_start[c + 1];
-      if (nb1 > nb0) W = std::max(W, P.nb_pose[nb1 - 1] - P.nb_pose[nb0]);
-    }
-    const int64_t span = static_cast<int64_t>(W) + 1;
-    const bool dense = static_cast<int64_t>(P.n_pose) * span <= (int64_t{1} << 26);
-    std::vector<int32_t> id_dense;
-    std::unordered_map<uint64_t, int32_t> id_map;
-    auto pkey = [](int32_t A, int32_t B) { return (static_cast<uint64_t>(B) << 32) | static_cast<uint32_t>(A); };
-    if (dense) id_dense.assign(static_cast<size_t>(P.n_pose) * span, -1);
-    auto mark = [&](int32_t A, int32_t B) {
-      if (dense) id_dense[static_cast<size_t>(A) * span + (A - B)] = 0;
-      else id_map.emplace(pkey(A, B), 0);
-    };
-    for (int32_t A = 0; A < P.n_pose; ++A) mark(A, A);
-    each_distinct(mark);
-    P.red_A.clear();
-    P.red_B.clear();
-    if (dense) {
-      for (int32_t B = 0; B < P.n_pose; ++B)
-        for (int32_t A = B; A < P.n_pose && A - B < span; ++A) {
-          int32_t& id = id_dense[static_cast<size_t>(A) * span + (A - B)];
-          if (id < 0) continue;
-          id = static_cast<int32_t>(P.red_A.size());
-          P.red_A.push_back(A);
-          P.red_B.push_back(B);
-        }
-    } else {
-      std::vector<uint64_t> ks;
-      ks.reserve(id_map.size());
-      for (const auto& kv : id_map) ks.push_back(kv.first);
-      std::sort(ks.begin(), ks.end());  // (B, A) order
-      for (uint64_t k : ks) {
-        id_map[k] = static_cast<int32_t>(P.red_A.size());
-        P.red_A.push_back(static_cast<int32_t>(k & 0xffffffffu));
-        P.red_B.push_back(static_cast<int32_t>(k >> 32));
-      }
-    }
-    auto tid = [&](int32_t A, int32_t B) -> int32_t {
-      return dense ? id_dense[static_cast<size_t>(A) * span + (A - B)] : id_map.at(pkey(A, B));
-    };
-    // per worker, the B range of its targets: a component whose neighbour
-    // poses (sorted) miss it emits nothing there and is skipped whole
-    const std::vector<int64_t> rcut = even_cuts(static_cast<int64_t>(P.red_A.size()));
     if (!structure_only) {
-    csr_target_ranges(P.red_A.size(), rcut,
-                      [&](int r, auto&& fn) {
-                        if (rcut[r + 1] <= rcut[r]) return;
-                        const int32_t blo = P.red_B[rcut[r]], bhi = P.red_B[rcut[r + 1] - 1];
-                        auto pf = [&](int32_t A, int32_t B, const GEntry& e) {
-                          if (B >= blo && B <= bhi) fn(tid(A, B), e);
-                        };
-                        emit_factor_pairs(pf);
-                        for (int c = 0; c < P.n_comp; ++c) {
-                          const int32_t nb0 = P.comp_nb_start[c], nb1 = P.comp_nb_start[c + 1];
-                          if (nb1 == nb0 || P.nb_pose[nb1 - 1] < blo || P.nb_pose[nb0] > bhi || comp_grouped(c)) continue;
-                          emit_comp_pairs(c, pf);
-                        }
-                        emit_group_pairs(blo, bhi, pf);
-                      },
-                      P.gRed);
-    const std::vector<int64_t> gcut = even_cuts(P.n_pose);
-    csr_target_ranges(P.n_pose, gcut, [&](int r, auto&& fn) { emit_grad(fn, gcut[r], gcut[r + 1]); }, P.gGred);
+      // J_A^T J_B per factor pair, -W_A Y_B per component pair, the groups'
+      // partial blocks
+      // target ranges: worker r owns the targets of a B range and enumerates
+      // every source, skipping components and groups outside its range;
+      // each worker writes one contiguous part of the list
+      const std::vector<int64_t> rcut = even_cuts(static_cast<int64_t>(P.red_A.size()));
+      csr_target_ranges(P.red_A.size(), rcut,
+                        [&](int r, auto&& fn) {
+                          if (rcut[r + 1] <= rcut[r]) return;
+                          const int32_t blo = P.red_B[rcut[r]], bhi = P.red_B[rcut[r + 1] - 1];
+                          auto pf = [&](int32_t A, int32_t B, const GEntry& e) {
+                            if (B >= blo && B <= bhi) fn(tid(A, B), e);
+                          };
+                          visit(0, nsrc, [&](int t, int i) { factor_pairs(t, i, pf); },
+                                [&](int c) {
+                                  const int32_t nb0 = P.comp_nb_start[c], nb1 = P.comp_nb_start[c + 1];
+                                  if (P.nb_pose[nb1 - 1] < blo || P.nb_pose[nb0] > bhi) return;
+                                  emit_comp_pairs(c, pf);
+                                },
+                                [&](const LoneGroup& G) {
+                                  const int32_t* ps = P.lone_pose.data() + G.pose_beg;
+                                  if (ps[G.m - 1] < blo || ps[0] > bhi) return;
+                                  for (int a = 0; a < G.m; ++a)
+                                    for (int b = 0; b <= a; ++b)
+                                      pf(ps[a], ps[b], GEntry{static_cast<uint32_t>(P.off_I6),
+                                                              G.out + 36u * (a * (a + 1) / 2 + b), 6, 1});
+                                });
+                        },
+                        P.gRed);
+      // gradient gathers per pose: J_A^T b per factor, -W_A v per component,
+      // the groups' partial gradients
+      const std::vector<int64_t> gcut = even_cuts(P.n_pose);
+      csr_target_ranges(P.n_pose, gcut,
+                        [&](int r, auto&& fn) {
+                          const int64_t p0 = gcut[r], p1 = gcut[r + 1];
+                          visit(0, nsrc,
+                                [&](int t, int i) {
+                                  const TypePlan& tp = P.types[t];
+                                  const int nk = kNKeys[t], d = kDim[t];
+                                  for (int sa = 0; sa < nk; ++sa)
+                                    if (kSlotKind[t][sa] == 0)
+                                      fn(tp.idx[i * nk + sa], GEntry{block_off(tp, t, i, sa), b_off(tp, t, i), d, 1});
+                                },
+                                [&](int c) {
+                                  const int32_t nb0 = P.comp_nb_start[c], m = P.comp_nb_start[c + 1] - nb0;
+                                  if (P.nb_pose[nb0 + m - 1] < p0 || P.nb_pose[nb0] >= p1) return;
+                                  for (int a = 0; a < m; ++a)
+                                    for (int32_t q = P.nbedge_start[nb0 + a]; q < P.nbedge_start[nb0 + a + 1]; ++q)
+                                      fn(P.nb_pose[nb0 + a],
+                                         GEntry{P.nbedge_w[q],
+                                                static_cast<uint32_t>(P.off_v + 3ull * (P.comp_start[c] + P.nbedge_pt[q])), 3, -1});
+                                },
+                                [&](const LoneGroup& G) {
+                                  const int32_t* ps = P.lone_pose.data() + G.pose_beg;
+                                  if (ps[G.m - 1] < p0 || ps[0] >= p1) return;
+                                  const uint32_t g0 = G.out + 36u * (G.m * (G.m + 1) / 2);
+                                  for (int a = 0; a < G.m; ++a)
+                                    fn(ps[a], GEntry{static_cast<uint32_t>(P.off_I6), g0 + 6u * a, 6, 1});
+                                });
+                        },
+                        P.gGred);
     }
   }
   plan_mark("reduced system targets", tmark);
 
-  // ---- band layout ----
-  P.n_red = 6 * P.n_pose;
-  P.NT = (P.n_red + kTile - 1) / kTile;
-  std::vector<int32_t> rlow(P.NT);
-  for (int j = 0; j < P.NT; ++j) rlow[j] = j;
-  for (size_t t = 0; t < P.red_A.size(); ++t) {
-    const int r1 = (6 * P.red_A[t] + 5) / kTile;
-    const int c0 = (6 * P.red_B[t]) / kTile, c1 = (6 * P.red_B[t] + 5) / kTile;
-    for (int j = c0; j <= c1; ++j) rlow[j] = std::max(rlow[j], r1);
-  }
-  for (int j = 1; j < P.NT; ++j) rlow[j] = std::max(rlow[j], rlow[j - 1]);
-  P.band_D.resize(P.NT);
-  P.max_D = 0;
-  for (int j = 0; j < P.NT; ++j) {
-    P.band_D[j] = rlow[j] - j;
-    P.max_D = std::max(P.max_D, P.band_D[j]);
-  }
-  plan_mark("band", tmark);
-  if (with_schedule && !build_tile_schedule(P)) {
+  if (sched.joinable()) sched.join();
+  if (with_schedule && !sched_ok) {
     err = "graph too short in time for " + std::to_string(nranks) + " partitions";
     return DYNOHIP_ESTRUCT;
   }
-  plan_mark("tile schedule", tmark);
+  plan_mark("tile schedule (join)", tmark);
   if (with_schedule && !structure_only) compute_red_slots(P);
   plan_mark("reduced target slots", tmark);
   return DYNOHIP_OK;

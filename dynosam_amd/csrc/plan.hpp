@@ -239,7 +239,9 @@ void plan_recycle(Plan& P);
 // tile-level fill and the task DAG with its level schedule. With
 // P.nranks > 1 the top of the dissection is split into rank subtrees; false
 // when the graph is too short for that many.
-bool build_tile_schedule(Plan& P);
+// own_threads: the candidate orderings run on threads of their own instead
+// of the planner pool (the schedule then runs beside the gather builds).
+bool build_tile_schedule(Plan& P, bool own_threads = false);
 
 // Plan::red_slot from the tile structure (after the tile schedule).
 void compute_red_slots(Plan& P);

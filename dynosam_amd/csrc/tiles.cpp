@@ -582,7 +582,7 @@ void filter_tasks(const std::vector<TileTask>& all, const std::vector<int32_t>& 
 
 }  // namespace
 
-bool build_tile_schedule(Plan& P) {
+bool build_tile_schedule(Plan& P, bool own_threads) {
   const int NT = P.NT;
   auto bt0 = std::chrono::steady_clock::now();
   auto bmark = [&](const char* what) {
@@ -629,9 +629,17 @@ bool build_tile_schedule(Plan& P) {
       leaves.push_back(leaf);
     }
     std::vector<Sched> cand(leaves.size());
-    parallel_chunks(static_cast<int64_t>(leaves.size()), 1, [&](int64_t c0, int64_t c1) {
-      for (int64_t c = c0; c < c1; ++c) schedule(NT, adj, maxnb, leaves[c], cand[c], nr);
-    });
+    if (own_threads) {
+      std::vector<std::thread> th;
+      for (size_t c = 1; c < leaves.size(); ++c)
+        th.emplace_back([&, c] { schedule(NT, adj, maxnb, leaves[c], cand[c], nr); });
+      schedule(NT, adj, maxnb, leaves[0], cand[0], nr);
+      for (auto& t : th) t.join();
+    } else {
+      parallel_chunks(static_cast<int64_t>(leaves.size()), 1, [&](int64_t c0, int64_t c1) {
+        for (int64_t c = c0; c < c1; ++c) schedule(NT, adj, maxnb, leaves[c], cand[c], nr);
+      });
+    }
     if (!cand[0].ok) return false;
     size_t bi = 0;
     for (size_t c = 1; c < cand.size(); ++c)
