@@ -1028,6 +1028,47 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
       for (int64_t s = std::max(s0, nF + nC); s < s1; ++s) on_group(P.lgroup[s - nF - nC]);
     };
     if (!structure_only) {
+      std::thread grad([&] {
+        // gradient gathers per pose: J_A^T b per factor, -W_A v per component,
+        // the groups' partial gradients
+        // (on a thread of its own, one range: it runs beside the pair lists)
+        const std::vector<int64_t> gcut{0, P.n_pose};
+        csr_target_ranges(P.n_pose, gcut,
+                          [&](int r, auto&& fn) {
+                            const int64_t p0 = gcut[r], p1 = gcut[r + 1];
+                            visit(0, nsrc,
+                                  [&](int t, int i) {
+                                    const TypePlan& tp = P.types[t];
+                                    const int nk = kNKeys[t], d = kDim[t];
+                                    for (int sa = 0; sa < nk; ++sa)
+                                      if (kSlotKind[t][sa] == 0)
+                                        fn(tp.idx[i * nk + sa], GEntry{block_off(tp, t, i, sa), b_off(tp, t, i), d, 1});
+                                  },
+                                  [&](int c) {
+                                    const int32_t nb0 = P.comp_nb_start[c], m = P.comp_nb_start[c + 1] - nb0;
+                                    if (P.nb_pose[nb0 + m - 1] < p0 || P.nb_pose[nb0] >= p1) return;
+                                    for (int a = 0; a < m; ++a)
+                                      for (int32_t q = P.nbedge_start[nb0 + a]; q < P.nbedge_start[nb0 + a + 1]; ++q)
+                                        fn(P.nb_pose[nb0 + a],
+                                           GEntry{P.nbedge_w[q],
+                                                  static_cast<uint32_t>(P.off_v + 3ull * (P.comp_start[c] + P.nbedge_pt[q])), 3, -1});
+                                  },
+                                  [&](const LoneGroup& G) {
+                                    const int32_t* ps = P.lone_pose.data() + G.pose_beg;
+                                    if (ps[G.m - 1] < p0 || ps[0] >= p1) return;
+                                    const uint32_t g0 = G.out + 36u * (G.m * (G.m + 1) / 2);
+                                    for (int a = 0; a < G.m; ++a)
+                                      fn(ps[a], GEntry{static_cast<uint32_t>(P.off_I6), g0 + 6u * a, 6, 1});
+                                  });
+                          },
+                          P.gGred);
+      });
+      struct JoinGrad {
+        std::thread& t;
+        ~JoinGrad() {
+          if (t.joinable()) t.join();
+        }
+      } grad_join{grad};
       // J_A^T J_B per factor pair, -W_A Y_B per component pair, the groups'
       // partial blocks
       // target ranges: worker r owns the targets of a B range and enumerates
@@ -1057,38 +1098,7 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
                                 });
                         },
                         P.gRed);
-      // gradient gathers per pose: J_A^T b per factor, -W_A v per component,
-      // the groups' partial gradients
-      const std::vector<int64_t> gcut = even_cuts(P.n_pose);
-      csr_target_ranges(P.n_pose, gcut,
-                        [&](int r, auto&& fn) {
-                          const int64_t p0 = gcut[r], p1 = gcut[r + 1];
-                          visit(0, nsrc,
-                                [&](int t, int i) {
-                                  const TypePlan& tp = P.types[t];
-                                  const int nk = kNKeys[t], d = kDim[t];
-                                  for (int sa = 0; sa < nk; ++sa)
-                                    if (kSlotKind[t][sa] == 0)
-                                      fn(tp.idx[i * nk + sa], GEntry{block_off(tp, t, i, sa), b_off(tp, t, i), d, 1});
-                                },
-                                [&](int c) {
-                                  const int32_t nb0 = P.comp_nb_start[c], m = P.comp_nb_start[c + 1] - nb0;
-                                  if (P.nb_pose[nb0 + m - 1] < p0 || P.nb_pose[nb0] >= p1) return;
-                                  for (int a = 0; a < m; ++a)
-                                    for (int32_t q = P.nbedge_start[nb0 + a]; q < P.nbedge_start[nb0 + a + 1]; ++q)
-                                      fn(P.nb_pose[nb0 + a],
-                                         GEntry{P.nbedge_w[q],
-                                                static_cast<uint32_t>(P.off_v + 3ull * (P.comp_start[c] + P.nbedge_pt[q])), 3, -1});
-                                },
-                                [&](const LoneGroup& G) {
-                                  const int32_t* ps = P.lone_pose.data() + G.pose_beg;
-                                  if (ps[G.m - 1] < p0 || ps[0] >= p1) return;
-                                  const uint32_t g0 = G.out + 36u * (G.m * (G.m + 1) / 2);
-                                  for (int a = 0; a < G.m; ++a)
-                                    fn(ps[a], GEntry{static_cast<uint32_t>(P.off_I6), g0 + 6u * a, 6, 1});
-                                });
-                        },
-                        P.gGred);
+      grad.join();
     }
   }
   plan_mark("reduced system targets", tmark);

@@ -24,6 +24,7 @@
 #include "../../include/dynohip.h"
 #include "kernels.hpp"
 #include "plan.hpp"
+#include "plan_pool.hpp"
 
 using namespace dynohip;
 
@@ -205,6 +206,89 @@ class ResPool {
  private:
   std::mutex mu_;
   std::vector<HandleRes> free_;
+};
+
+// A plan's host arrays go to the device through one pinned staging buffer
+// (process-wide, grow-only): packed by the planner's workers, each worker
+// copying whole 1 MB pieces, then one asynchronous DMA per array. From
+// pageable memory the runtime stages every array itself, one copy at a time
+// on the calling thread (C2: ~18 MB of plan arrays, 1.0-1.4 ms).
+class PinnedStage {
+ public:
+  static PinnedStage& get() {
+    static PinnedStage* p = new PinnedStage();
+    return *p;
+  }
+  struct Item {
+    void* dev;
+    const void* host;
+    size_t bytes, off;
+  };
+  // copies every item to the device on `st` and waits for it; false if the
+  // staging buffer could not be allocated or a copy failed to enqueue (the
+  // caller then copies from pageable memory)
+  bool run(const std::vector<Item>& items, size_t total, hipStream_t st) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (total > cap_) {
+      if (buf_) (void)hipHostFree(buf_);
+      buf_ = nullptr;
+      cap_ = 0;
+      const size_t want = total + total / 4;
+      if (hipHostMalloc(reinterpret_cast<void**>(&buf_), want, hipHostMallocPortable) != hipSuccess) {
+        buf_ = nullptr;
+        return false;
+      }
+      cap_ = want;
+    }
+    constexpr size_t kPiece = size_t{1} << 20;
+    std::vector<std::pair<size_t, size_t>> pieces;   // (item, piece start)
+    for (size_t i = 0; i < items.size(); ++i)
+      for (size_t o = 0; o < items[i].bytes; o += kPiece) pieces.push_back({i, o});
+    parallel_chunks(static_cast<int64_t>(pieces.size()), 1, [&](int64_t k0, int64_t k1) {
+      for (int64_t k = k0; k < k1; ++k) {
+        const Item& it = items[pieces[k].first];
+        const size_t o = pieces[k].second, nb = std::min(kPiece, it.bytes - o);
+        std::memcpy(buf_ + it.off + o, static_cast<const char*>(it.host) + o, nb);
+      }
+    });
+    for (const Item& it : items)
+      if (hipMemcpyAsync(it.dev, buf_ + it.off, it.bytes, hipMemcpyHostToDevice, st) != hipSuccess) return false;
+    return hipStreamSynchronize(st) == hipSuccess;   // the buffer is reused by the next upload
+  }
+  void trim() {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (buf_) (void)hipHostFree(buf_);
+    buf_ = nullptr;
+    cap_ = 0;
+  }
+
+ private:
+  std::mutex mu_;
+  char* buf_ = nullptr;
+  size_t cap_ = 0;
+};
+
+// the uploads of one plan, collected (device buffers allocated) and then
+// staged together
+struct Uploads {
+  std::vector<PinnedStage::Item> items;
+  size_t total = 0;
+  template <typename T, class Alloc>
+  hipError_t add(DevBuf<T>& d, const std::vector<T, Alloc>& v) {
+    const hipError_t e = d.alloc(v.size());
+    if (e != hipSuccess || v.empty()) return e;
+    items.push_back({d.p, v.data(), v.size() * sizeof(T), total});
+    total += (v.size() * sizeof(T) + 255) & ~size_t{255};
+    return hipSuccess;
+  }
+  hipError_t run(hipStream_t st) {
+    if (items.empty() || PinnedStage::get().run(items, total, st)) return hipSuccess;
+    for (const auto& it : items) {   // pageable fallback
+      const hipError_t e = hipMemcpyAsync(it.dev, it.host, it.bytes, hipMemcpyHostToDevice, st);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
 };
 
 struct GraphCopy {
@@ -390,15 +474,16 @@ int set_err(dynohip_solver* s, int code, const char* fmt, ...) {
     if (e_ != hipSuccess) return set_err(s, DYNOHIP_EHIP, "%s: %s", #expr, hipGetErrorString(e_)); \
   } while (0)
 
-int upload_gather(dynohip_solver* s, const GatherList& g, GatherBufs& b) {
-  HIPCHK(s, b.start.upload(g.start, s->stream));
-  HIPCHK(s, b.ent.upload(g.ent, s->stream));
+int upload_gather(dynohip_solver* s, const GatherList& g, GatherBufs& b, Uploads& up) {
+  HIPCHK(s, up.add(b.start, g.start));
+  HIPCHK(s, up.add(b.ent, g.ent));
   return 0;
 }
 
 int upload_plan(dynohip_solver* s) {
   Plan& P = s->plan;
   hipStream_t st = s->stream;
+  Uploads up;
   HIPCHK(s, s->pose.alloc(12ull * P.n_pose));
   HIPCHK(s, s->pt.alloc(3ull * P.n_pt));
   HIPCHK(s, s->pose_c.alloc(12ull * P.n_pose));
@@ -407,10 +492,10 @@ int upload_plan(dynohip_solver* s) {
   int slots = 1;
   for (int t = 0; t < kNTypes; ++t) {
     TypePlan& tp = P.types[t];
-    HIPCHK(s, s->tb[t].idx.upload(tp.idx, st));
-    HIPCHK(s, s->tb[t].meas.upload(tp.meas, st));
-    HIPCHK(s, s->tb[t].isig.upload(tp.isig, st));
-    HIPCHK(s, s->tb[t].hk.upload(tp.hk, st));
+    HIPCHK(s, up.add(s->tb[t].idx, tp.idx));
+    HIPCHK(s, up.add(s->tb[t].meas, tp.meas));
+    HIPCHK(s, up.add(s->tb[t].isig, tp.isig));
+    HIPCHK(s, up.add(s->tb[t].hk, tp.hk));
     TypeDev& d = s->td[t];
     d.n = tp.n;
     d.base = tp.base;
@@ -428,38 +513,39 @@ int upload_plan(dynohip_solver* s) {
   HIPCHK(s, hipMemsetAsync(s->sumctr.p, 0, sizeof(unsigned), st));
   s->failp = reinterpret_cast<int*>(s->result.p + 5);
   HIPCHK(s, hipMemsetAsync(s->result.p, 0, 8 * sizeof(double), st));
-  if (upload_gather(s, P.gD, s->gD) || upload_gather(s, P.gE, s->gE) || upload_gather(s, P.gGp, s->gGp) ||
-      upload_gather(s, P.gW, s->gW) || upload_gather(s, P.gRed, s->gRed) || upload_gather(s, P.gGred, s->gGred))
+  if (upload_gather(s, P.gD, s->gD, up) || upload_gather(s, P.gE, s->gE, up) || upload_gather(s, P.gGp, s->gGp, up) ||
+      upload_gather(s, P.gW, s->gW, up) || upload_gather(s, P.gRed, s->gRed, up) ||
+      upload_gather(s, P.gGred, s->gGred, up))
     return DYNOHIP_EHIP;
-  HIPCHK(s, s->redA.upload(P.red_A, st));
-  HIPCHK(s, s->redB.upload(P.red_B, st));
-  HIPCHK(s, s->redslot.upload(P.red_slot, st));
-  HIPCHK(s, s->comp_start.upload(P.comp_start, st));
-  HIPCHK(s, s->comp_nb_start.upload(P.comp_nb_start, st));
-  HIPCHK(s, s->nb_comp.upload(P.nb_comp, st));
-  HIPCHK(s, s->comp_y_base.upload(P.comp_y_base, st));
-  HIPCHK(s, s->nbedge_start.upload(P.nbedge_start, st));
-  HIPCHK(s, s->nbedge_pt.upload(P.nbedge_pt, st));
-  HIPCHK(s, s->nbedge_w.upload(P.nbedge_w, st));
-  HIPCHK(s, s->pt_edge_start.upload(P.pt_edge_start, st));
-  HIPCHK(s, s->edge_pose.upload(P.edge_pose, st));
-  HIPCHK(s, s->edge_pt.upload(P.edge_pt, st));
+  HIPCHK(s, up.add(s->redA, P.red_A));
+  HIPCHK(s, up.add(s->redB, P.red_B));
+  HIPCHK(s, up.add(s->redslot, P.red_slot));
+  HIPCHK(s, up.add(s->comp_start, P.comp_start));
+  HIPCHK(s, up.add(s->comp_nb_start, P.comp_nb_start));
+  HIPCHK(s, up.add(s->nb_comp, P.nb_comp));
+  HIPCHK(s, up.add(s->comp_y_base, P.comp_y_base));
+  HIPCHK(s, up.add(s->nbedge_start, P.nbedge_start));
+  HIPCHK(s, up.add(s->nbedge_pt, P.nbedge_pt));
+  HIPCHK(s, up.add(s->nbedge_w, P.nbedge_w));
+  HIPCHK(s, up.add(s->pt_edge_start, P.pt_edge_start));
+  HIPCHK(s, up.add(s->edge_pose, P.edge_pose));
+  HIPCHK(s, up.add(s->edge_pt, P.edge_pt));
   HIPCHK(s, s->slots.alloc(static_cast<size_t>(P.n_slots) * kTile * kTile));
-  HIPCHK(s, s->tile_pos.upload(P.tile_pos, st));
-  HIPCHK(s, s->row_start.upload(P.row_start, st));
-  HIPCHK(s, s->row_col.upload(P.row_col, st));
-  HIPCHK(s, s->row_slot.upload(P.row_slot, st));
-  HIPCHK(s, s->bent.upload(P.bent, st));
-  HIPCHK(s, s->ftask.upload(P.ftask, st));
-  HIPCHK(s, s->pairs.upload(P.pairs, st));
+  HIPCHK(s, up.add(s->tile_pos, P.tile_pos));
+  HIPCHK(s, up.add(s->row_start, P.row_start));
+  HIPCHK(s, up.add(s->row_col, P.row_col));
+  HIPCHK(s, up.add(s->row_slot, P.row_slot));
+  HIPCHK(s, up.add(s->bent, P.bent));
+  HIPCHK(s, up.add(s->ftask, P.ftask));
+  HIPCHK(s, up.add(s->pairs, P.pairs));
   HIPCHK(s, s->contrib.alloc(static_cast<size_t>(P.n_slots) * kTile));
-  HIPCHK(s, s->bpart.upload(P.bpart, st));
+  HIPCHK(s, up.add(s->bpart, P.bpart));
   HIPCHK(s, s->bpartials.alloc(static_cast<size_t>(P.n_partials) * kTile + 1));
   HIPCHK(s, s->arrive.alloc(static_cast<size_t>(P.NT) + 1));
   HIPCHK(s, hipMemsetAsync(s->arrive.p, 0, (static_cast<size_t>(P.NT) + 1) * sizeof(int), st));
-  HIPCHK(s, s->fdep_start.upload(P.fdep_start, st));
-  HIPCHK(s, s->fdep.upload(P.fdep, st));
-  HIPCHK(s, s->fqueue.upload(P.fqueue, st));
+  HIPCHK(s, up.add(s->fdep_start, P.fdep_start));
+  HIPCHK(s, up.add(s->fdep, P.fdep));
+  HIPCHK(s, up.add(s->fqueue, P.fqueue));
   HIPCHK(s, s->fsync.alloc((static_cast<size_t>(P.n_slots) + 4 + 3) / 4 * 4));
   HIPCHK(s, hipMemsetAsync(s->fsync.p, 0, s->fsync.n * sizeof(unsigned), st));
   HIPCHK(s, s->done.alloc(static_cast<size_t>(P.NT) + 1));
@@ -502,7 +588,7 @@ int upload_plan(dynohip_solver* s) {
   c.off_v = P.off_v;
   c.off_L = P.off_L;
   c.off_M = P.off_M;
-  HIPCHK(s, s->lone_blk.upload(P.lone_blk, st));
+  HIPCHK(s, up.add(s->lone_blk, P.lone_blk));
   LoneSchurDev& ld = s->ld;
   ld.n_group = static_cast<int>(P.lgroup.size());
   ld.blk = s->lone_blk.p;
@@ -533,6 +619,7 @@ int upload_plan(dynohip_solver* s) {
   s->sd.forder = s->fqueue.p;
   s->sd.fqueue = s->fsync.p;
   s->sd.wcnt = s->fsync.p + 4;
+  HIPCHK(s, up.run(st));
   // debug: DYNOHIP_POISON_MASK fills the selected device buffers with NaN
   // bytes after a re-plan (bit 0 arena, 1 partials, 2 slots, 3 gred, 4 xy,
   // 5 dpt, (6 unused), 7 linv, 8 contrib, 9 bpartials, 10 pose_c/pt_c), so a read
@@ -1072,6 +1159,7 @@ void dynohip_destroy(dynohip_solver* s) {
 
 int dynohip_pool_trim(void) {
   HostCache::get().trim();
+  PinnedStage::get().trim();
   const size_t n = DevPool::get().trim();
   return static_cast<int>(std::min<size_t>(n >> 20, 0x7fffffff));
 }
