@@ -228,7 +228,7 @@ void plan_recycle(Plan& P) {
 }
 
 int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t* kind, size_t n, Plan& P,
-               std::string& err, int nranks, int rank, bool with_schedule, bool structure_only) {
+               std::string& err, int nranks, int rank, bool with_schedule, bool structure_only, PlanHook* hook) {
   double tmark = plan_now();
   plan_recycle(P);
   P.nranks = nranks;
@@ -438,6 +438,7 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
     });
   }
 
+  if (hook) hook->types_ready(P);
   plan_mark("before point-pose edges", tmark);
   // ---- point-pose edges ----
   {

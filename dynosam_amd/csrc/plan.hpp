@@ -253,8 +253,17 @@ void compute_red_slots(Plan& P);
 // the point chains, the reduced system's pose-pair blocks and (with
 // with_schedule) the tile schedule only, which is all the partitioned plan
 // needs of the global graph.
+// Called by build_plan as parts of the plan become final (the caller may
+// start uploading them while the planner goes on).
+struct PlanHook {
+  virtual ~PlanHook() = default;
+  // P.types (indices, measurements, 1/sigma, Huber k) are final
+  virtual void types_ready(const Plan& P) = 0;
+};
+
 int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t* kind, size_t n, Plan& plan,
-               std::string& err, int nranks = 1, int rank = 0, bool with_schedule = true, bool structure_only = false);
+               std::string& err, int nranks = 1, int rank = 0, bool with_schedule = true, bool structure_only = false,
+               PlanHook* hook = nullptr);
 
 // Partitioned full-batch solve: what one rank holds (partition.cpp).
 struct Partition {

@@ -179,6 +179,8 @@ struct HandleRes {
   hipEvent_t ev_main = nullptr, ev_side = nullptr, ev_res = nullptr;
   hipEvent_t ev[9] = {};
   double* hres = nullptr;
+  char* stage[2] = {nullptr, nullptr};   // pinned upload staging: early (factor records), rest
+  size_t stage_cap[2] = {0, 0};
 };
 
 class ResPool {
@@ -208,70 +210,17 @@ class ResPool {
   std::vector<HandleRes> free_;
 };
 
-// A plan's host arrays go to the device through one pinned staging buffer
-// (process-wide, grow-only): packed by the planner's workers, each worker
-// copying whole 1 MB pieces, then one asynchronous DMA per array. From
-// pageable memory the runtime stages every array itself, one copy at a time
-// on the calling thread (C2: ~18 MB of plan arrays, 1.0-1.4 ms).
-class PinnedStage {
- public:
-  static PinnedStage& get() {
-    static PinnedStage* p = new PinnedStage();
-    return *p;
-  }
+// A plan's host arrays go to the device through pinned staging buffers of
+// the handle (recycled with its streams): packed into the buffer, each
+// array then one asynchronous DMA. From pageable memory the runtime stages
+// every array itself, one copy at a time on the calling thread.
+struct Uploads {
   struct Item {
     void* dev;
     const void* host;
     size_t bytes, off;
   };
-  // copies every item to the device on `st` and waits for it; false if the
-  // staging buffer could not be allocated or a copy failed to enqueue (the
-  // caller then copies from pageable memory)
-  bool run(const std::vector<Item>& items, size_t total, hipStream_t st) {
-    std::lock_guard<std::mutex> lk(mu_);
-    if (total > cap_) {
-      if (buf_) (void)hipHostFree(buf_);
-      buf_ = nullptr;
-      cap_ = 0;
-      const size_t want = total + total / 4;
-      if (hipHostMalloc(reinterpret_cast<void**>(&buf_), want, hipHostMallocPortable) != hipSuccess) {
-        buf_ = nullptr;
-        return false;
-      }
-      cap_ = want;
-    }
-    constexpr size_t kPiece = size_t{1} << 20;
-    std::vector<std::pair<size_t, size_t>> pieces;   // (item, piece start)
-    for (size_t i = 0; i < items.size(); ++i)
-      for (size_t o = 0; o < items[i].bytes; o += kPiece) pieces.push_back({i, o});
-    parallel_chunks(static_cast<int64_t>(pieces.size()), 1, [&](int64_t k0, int64_t k1) {
-      for (int64_t k = k0; k < k1; ++k) {
-        const Item& it = items[pieces[k].first];
-        const size_t o = pieces[k].second, nb = std::min(kPiece, it.bytes - o);
-        std::memcpy(buf_ + it.off + o, static_cast<const char*>(it.host) + o, nb);
-      }
-    });
-    for (const Item& it : items)
-      if (hipMemcpyAsync(it.dev, buf_ + it.off, it.bytes, hipMemcpyHostToDevice, st) != hipSuccess) return false;
-    return hipStreamSynchronize(st) == hipSuccess;   // the buffer is reused by the next upload
-  }
-  void trim() {
-    std::lock_guard<std::mutex> lk(mu_);
-    if (buf_) (void)hipHostFree(buf_);
-    buf_ = nullptr;
-    cap_ = 0;
-  }
-
- private:
-  std::mutex mu_;
-  char* buf_ = nullptr;
-  size_t cap_ = 0;
-};
-
-// the uploads of one plan, collected (device buffers allocated) and then
-// staged together
-struct Uploads {
-  std::vector<PinnedStage::Item> items;
+  std::vector<Item> items;
   size_t total = 0;
   template <typename T, class Alloc>
   hipError_t add(DevBuf<T>& d, const std::vector<T, Alloc>& v) {
@@ -281,12 +230,50 @@ struct Uploads {
     total += (v.size() * sizeof(T) + 255) & ~size_t{255};
     return hipSuccess;
   }
-  hipError_t run(hipStream_t st) {
-    if (items.empty() || PinnedStage::get().run(items, total, st)) return hipSuccess;
-    for (const auto& it : items) {   // pageable fallback
-      const hipError_t e = hipMemcpyAsync(it.dev, it.host, it.bytes, hipMemcpyHostToDevice, st);
+  // packs into `buf` (grown to fit; pinned) on the planner's workers or on
+  // this thread, and enqueues the copies on `st` without waiting: the
+  // caller synchronises before the buffer is reused
+  hipError_t run(char*& buf, size_t& cap, hipStream_t st, bool parallel) {
+    if (items.empty()) return hipSuccess;
+    if (total > cap) {
+      if (buf) (void)hipHostFree(buf);
+      buf = nullptr;
+      cap = 0;
+      const size_t want = total + total / 4;
+      if (hipHostMalloc(reinterpret_cast<void**>(&buf), want, hipHostMallocPortable) != hipSuccess) {
+        buf = nullptr;
+        for (const auto& it : items) {   // pageable fallback
+          const hipError_t e = hipMemcpyAsync(it.dev, it.host, it.bytes, hipMemcpyHostToDevice, st);
+          if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+      }
+      cap = want;
+    }
+    static const bool timing = std::getenv("DYNOHIP_PLAN_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    constexpr size_t kPiece = size_t{1} << 20;
+    std::vector<std::pair<size_t, size_t>> pieces;   // (item, piece start)
+    for (size_t i = 0; i < items.size(); ++i)
+      for (size_t o = 0; o < items[i].bytes; o += kPiece) pieces.push_back({i, o});
+    auto pack = [&](int64_t k0, int64_t k1) {
+      for (int64_t k = k0; k < k1; ++k) {
+        const Item& it = items[pieces[k].first];
+        const size_t o = pieces[k].second, nb = std::min(kPiece, it.bytes - o);
+        std::memcpy(buf + it.off + o, static_cast<const char*>(it.host) + o, nb);
+      }
+    };
+    if (parallel) parallel_chunks(static_cast<int64_t>(pieces.size()), 1, pack);
+    else pack(0, static_cast<int64_t>(pieces.size()));
+    const auto t1 = std::chrono::steady_clock::now();
+    for (const Item& it : items) {
+      const hipError_t e = hipMemcpyAsync(it.dev, buf + it.off, it.bytes, hipMemcpyHostToDevice, st);
       if (e != hipSuccess) return e;
     }
+    if (timing)
+      std::fprintf(stderr, "[upload] %zu arrays, %.2f MB: pack %.2f ms, enqueue %.2f ms\n", items.size(),
+                   total / 1048576.0, std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                   std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count());
     return hipSuccess;
   }
 };
@@ -427,6 +414,8 @@ struct dynohip_solver {
   // recorded before the speculative linearisation is enqueued: the host
   // decides while the GPU linearises
   double* hres = nullptr;
+  char* stage[2] = {nullptr, nullptr};   // HandleRes::stage
+  size_t stage_cap[2] = {0, 0};
   hipEvent_t ev_res = nullptr;
   int iterations = 0, inner = 0, converged = 0;
   std::vector<dynohip_trace_entry> trace;
@@ -480,7 +469,8 @@ int upload_gather(dynohip_solver* s, const GatherList& g, GatherBufs& b, Uploads
   return 0;
 }
 
-int upload_plan(dynohip_solver* s) {
+// types_done: the factor records were uploaded during planning (EarlyUpload)
+int upload_plan(dynohip_solver* s, bool types_done = false) {
   Plan& P = s->plan;
   hipStream_t st = s->stream;
   Uploads up;
@@ -492,10 +482,12 @@ int upload_plan(dynohip_solver* s) {
   int slots = 1;
   for (int t = 0; t < kNTypes; ++t) {
     TypePlan& tp = P.types[t];
-    HIPCHK(s, up.add(s->tb[t].idx, tp.idx));
-    HIPCHK(s, up.add(s->tb[t].meas, tp.meas));
-    HIPCHK(s, up.add(s->tb[t].isig, tp.isig));
-    HIPCHK(s, up.add(s->tb[t].hk, tp.hk));
+    if (!types_done) {
+      HIPCHK(s, up.add(s->tb[t].idx, tp.idx));
+      HIPCHK(s, up.add(s->tb[t].meas, tp.meas));
+      HIPCHK(s, up.add(s->tb[t].isig, tp.isig));
+      HIPCHK(s, up.add(s->tb[t].hk, tp.hk));
+    }
     TypeDev& d = s->td[t];
     d.n = tp.n;
     d.base = tp.base;
@@ -619,7 +611,7 @@ int upload_plan(dynohip_solver* s) {
   s->sd.forder = s->fqueue.p;
   s->sd.fqueue = s->fsync.p;
   s->sd.wcnt = s->fsync.p + 4;
-  HIPCHK(s, up.run(st));
+  HIPCHK(s, up.run(s->stage[1], s->stage_cap[1], st, true));
   // debug: DYNOHIP_POISON_MASK fills the selected device buffers with NaN
   // bytes after a re-plan (bit 0 arena, 1 partials, 2 slots, 3 gred, 4 xy,
   // 5 dpt, (6 unused), 7 linv, 8 contrib, 9 bpartials, 10 pose_c/pt_c), so a read
@@ -1119,6 +1111,10 @@ int dynohip_create(int device_id, dynohip_solver** out) {
   s->ev_res = r.ev_res;
   for (int k = 0; k < 9; ++k) s->ev[k] = r.ev[k];
   s->hres = r.hres;
+  for (int k = 0; k < 2; ++k) {
+    s->stage[k] = r.stage[k];
+    s->stage_cap[k] = r.stage_cap[k];
+  }
   // the dataflow factorisation keeps one 158 KB-LDS workgroup per CU
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_id) == hipSuccess && cus > 0)
@@ -1147,6 +1143,10 @@ void dynohip_destroy(dynohip_solver* s) {
   r.ev_res = s->ev_res;
   for (int k = 0; k < 9; ++k) r.ev[k] = s->ev[k];
   r.hres = s->hres;
+  for (int k = 0; k < 2; ++k) {
+    r.stage[k] = s->stage[k];
+    r.stage_cap[k] = s->stage_cap[k];
+  }
   if (r.stream) ResPool::get().give(r);
   HostCache::get().give(s->plan, s->graph);
   const auto t1 = std::chrono::steady_clock::now();
@@ -1159,7 +1159,6 @@ void dynohip_destroy(dynohip_solver* s) {
 
 int dynohip_pool_trim(void) {
   HostCache::get().trim();
-  PinnedStage::get().trim();
   const size_t n = DevPool::get().trim();
   return static_cast<int>(std::min<size_t>(n >> 20, 0x7fffffff));
 }
@@ -1193,6 +1192,36 @@ int dynohip_set_graph(dynohip_solver* s, const dynohip_graph_view* g) {
   return DYNOHIP_OK;
 }
 
+// The factor records (indices, measurements, 1/sigma, Huber k: ~40% of a
+// plan's bytes) are final once build_plan has laid out the factor types:
+// they are staged and copied on a thread of their own while the planner
+// builds the rest (same stream; upload_plan's synchronisation covers them).
+struct EarlyUpload : PlanHook {
+  explicit EarlyUpload(dynohip_solver* h) : s(h) {}
+  ~EarlyUpload() override { join(); }
+  void types_ready(const Plan& P) override {
+    th = std::thread([this, &P] {
+      (void)hipSetDevice(s->device);
+      Uploads up;
+      for (int t = 0; t < kNTypes && err == hipSuccess; ++t) {
+        const TypePlan& tp = P.types[t];
+        if ((err = up.add(s->tb[t].idx, tp.idx)) != hipSuccess || (err = up.add(s->tb[t].meas, tp.meas)) != hipSuccess ||
+            (err = up.add(s->tb[t].isig, tp.isig)) != hipSuccess || (err = up.add(s->tb[t].hk, tp.hk)) != hipSuccess)
+          break;
+      }
+      if (err == hipSuccess) err = up.run(s->stage[0], s->stage_cap[0], s->stream, false);
+      done = err == hipSuccess;
+    });
+  }
+  void join() {
+    if (th.joinable()) th.join();
+  }
+  dynohip_solver* s;
+  std::thread th;
+  hipError_t err = hipSuccess;
+  bool done = false;
+};
+
 int dynohip_set_values(dynohip_solver* s, const uint64_t* keys, const uint8_t* kind, const double* data, size_t n) {
   if (!s || (n && (!keys || !kind || !data))) return DYNOHIP_EINVAL;
   if (!s->has_graph) return set_err(s, DYNOHIP_ESTATE, "set_graph first");
@@ -1203,16 +1232,23 @@ int dynohip_set_values(dynohip_solver* s, const uint64_t* keys, const uint8_t* k
     const auto tb0 = std::chrono::steady_clock::now();
     s->has_plan = false;
     dynohip_graph_view g = s->graph.view();
+    EarlyUpload early(s);
     int rc = s->nranks > 1 ? build_partitioned_plan(g, keys, kind, n, s->nranks, s->rank, s->plan, s->part,
                                                     s->local_graph, s->err)
-                           : build_plan(g, keys, kind, n, s->plan, s->err);
-    if (rc) return rc;
+                           : build_plan(g, keys, kind, n, s->plan, s->err, 1, 0, true, false, &early);
+    early.join();
+    if (rc) {
+      if (early.done) (void)hipStreamSynchronize(s->stream);   // its staging buffer is reused next time
+      return rc;
+    }
+    if (early.err != hipSuccess) return set_err(s, DYNOHIP_EHIP, "HIP error %d (%s) in the factor record upload",
+                                                 static_cast<int>(early.err), hipGetErrorString(early.err));
     static const bool timing = std::getenv("DYNOHIP_PLAN_TIMING") != nullptr;
     const auto t0 = std::chrono::steady_clock::now();
     if (timing)
       std::fprintf(stderr, "[plan] build_plan (set_values)     %8.2f ms\n",
                    std::chrono::duration<double, std::milli>(t0 - tb0).count());
-    rc = upload_plan(s);
+    rc = upload_plan(s, early.done);
     if (rc) return rc;
     if (timing) {
       (void)hipStreamSynchronize(s->stream);
