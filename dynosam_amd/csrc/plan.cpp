@@ -12,6 +12,7 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <future>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
@@ -246,7 +247,7 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
   const dynohip_factor_block* blocks[kNTypes] = {&g.pose_to_point, &g.landmark_motion_ternary, &g.between,
                                                  &g.prior, &g.landmark_motion_pose, &g.landmark_pose_smoothing};
   // user index per factor slot
-  std::vector<int32_t> fuser[kNTypes];
+  std::vector<int32_t, default_init_allocator<int32_t>> fuser[kNTypes];   // (every entry written below)
   for (int t = 0; t < kNTypes; ++t) {
     const auto* b = blocks[t];
     if (b->n == 0) continue;
@@ -628,6 +629,11 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
   // a hash map otherwise. The distinct pairs are the factor pose pairs and
   // the (a, b) neighbour pairs of every component (each neighbour pose has
   // at least one edge), so marking does not walk the edge lists.
+  std::vector<int32_t> id_dense;
+  std::unordered_map<uint64_t, int32_t> id_map;
+  auto pkey = [](int32_t A, int32_t B) { return (static_cast<uint64_t>(B) << 32) | static_cast<uint32_t>(A); };
+  int64_t span = 1;
+  bool dense = true;
   auto each_distinct = [&](auto&& fn) {
     for (int t = 0; t < kNTypes; ++t) {
       const TypePlan& tp = P.types[t];
@@ -646,78 +652,78 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
         for (int b = 0; b <= a; ++b) fn(P.nb_pose[nb0 + a], P.nb_pose[nb0 + b]);
     }
   };
-  int32_t W = 0;
-  for (int t = 0; t < kNTypes; ++t) {
-    const TypePlan& tp = P.types[t];
-    const int nk = kNKeys[t];
-    if (kNPoseSlots[t] < 2) continue;
-    for (int i = 0; i < tp.n; ++i)
-      for (int sa = 0; sa < nk; ++sa)
-        for (int sb = 0; sb < nk; ++sb)
-          if (kSlotKind[t][sa] == 0 && kSlotKind[t][sb] == 0)
-            W = std::max(W, tp.idx[i * nk + sa] - tp.idx[i * nk + sb]);
-  }
-  for (int c = 0; c < P.n_comp; ++c) {  // nb poses are sorted per component
-    const int32_t nb0 = P.comp_nb_start[c], nb1 = P.comp_nb_start[c + 1];
-    if (nb1 > nb0) W = std::max(W, P.nb_pose[nb1 - 1] - P.nb_pose[nb0]);
-  }
-  const int64_t span = static_cast<int64_t>(W) + 1;
-  const bool dense = static_cast<int64_t>(P.n_pose) * span <= (int64_t{1} << 26);
-  std::vector<int32_t> id_dense;
-  std::unordered_map<uint64_t, int32_t> id_map;
-  auto pkey = [](int32_t A, int32_t B) { return (static_cast<uint64_t>(B) << 32) | static_cast<uint32_t>(A); };
-  if (dense) id_dense.assign(static_cast<size_t>(P.n_pose) * span, -1);
-  auto mark = [&](int32_t A, int32_t B) {
-    if (dense) id_dense[static_cast<size_t>(A) * span + (A - B)] = 0;
-    else id_map.emplace(pkey(A, B), 0);
-  };
-  for (int32_t A = 0; A < P.n_pose; ++A) mark(A, A);
-  each_distinct(mark);
-  P.red_A.clear();
-  P.red_B.clear();
-  if (dense) {
-    for (int32_t B = 0; B < P.n_pose; ++B)
-      for (int32_t A = B; A < P.n_pose && A - B < span; ++A) {
-        int32_t& id = id_dense[static_cast<size_t>(A) * span + (A - B)];
-        if (id < 0) continue;
-        id = static_cast<int32_t>(P.red_A.size());
-        P.red_A.push_back(A);
-        P.red_B.push_back(B);
-      }
-  } else {
-    std::vector<uint64_t> ks;
-    ks.reserve(id_map.size());
-    for (const auto& kv : id_map) ks.push_back(kv.first);
-    std::sort(ks.begin(), ks.end());  // (B, A) order
-    for (uint64_t k : ks) {
-      id_map[k] = static_cast<int32_t>(P.red_A.size());
-      P.red_A.push_back(static_cast<int32_t>(k & 0xffffffffu));
-      P.red_B.push_back(static_cast<int32_t>(k >> 32));
+  auto structure = [&] {
+    int32_t W = 0;
+    for (int t = 0; t < kNTypes; ++t) {
+      const TypePlan& tp = P.types[t];
+      const int nk = kNKeys[t];
+      if (kNPoseSlots[t] < 2) continue;
+      for (int i = 0; i < tp.n; ++i)
+        for (int sa = 0; sa < nk; ++sa)
+          for (int sb = 0; sb < nk; ++sb)
+            if (kSlotKind[t][sa] == 0 && kSlotKind[t][sb] == 0)
+              W = std::max(W, tp.idx[i * nk + sa] - tp.idx[i * nk + sb]);
     }
-  }
-  auto tid = [&](int32_t A, int32_t B) -> int32_t {
-    return dense ? id_dense[static_cast<size_t>(A) * span + (A - B)] : id_map.at(pkey(A, B));
+    for (int c = 0; c < P.n_comp; ++c) {  // nb poses are sorted per component
+      const int32_t nb0 = P.comp_nb_start[c], nb1 = P.comp_nb_start[c + 1];
+      if (nb1 > nb0) W = std::max(W, P.nb_pose[nb1 - 1] - P.nb_pose[nb0]);
+    }
+    span = static_cast<int64_t>(W) + 1;
+    dense = static_cast<int64_t>(P.n_pose) * span <= (int64_t{1} << 26);
+    if (dense) id_dense.assign(static_cast<size_t>(P.n_pose) * span, -1);
+    auto mark = [&](int32_t A, int32_t B) {
+      if (dense) id_dense[static_cast<size_t>(A) * span + (A - B)] = 0;
+      else id_map.emplace(pkey(A, B), 0);
+    };
+    for (int32_t A = 0; A < P.n_pose; ++A) mark(A, A);
+    each_distinct(mark);
+    P.red_A.clear();
+    P.red_B.clear();
+    if (dense) {
+      for (int32_t B = 0; B < P.n_pose; ++B)
+        for (int32_t A = B; A < P.n_pose && A - B < span; ++A) {
+          int32_t& id = id_dense[static_cast<size_t>(A) * span + (A - B)];
+          if (id < 0) continue;
+          id = static_cast<int32_t>(P.red_A.size());
+          P.red_A.push_back(A);
+          P.red_B.push_back(B);
+        }
+    } else {
+      std::vector<uint64_t> ks;
+      ks.reserve(id_map.size());
+      for (const auto& kv : id_map) ks.push_back(kv.first);
+      std::sort(ks.begin(), ks.end());  // (B, A) order
+      for (uint64_t k : ks) {
+        id_map[k] = static_cast<int32_t>(P.red_A.size());
+        P.red_A.push_back(static_cast<int32_t>(k & 0xffffffffu));
+        P.red_B.push_back(static_cast<int32_t>(k >> 32));
+      }
+    }
+    // ---- band layout ----
+    P.n_red = 6 * P.n_pose;
+    P.NT = (P.n_red + kTile - 1) / kTile;
+    std::vector<int32_t> rlow(P.NT);
+    for (int j = 0; j < P.NT; ++j) rlow[j] = j;
+    for (size_t t = 0; t < P.red_A.size(); ++t) {
+      const int r1 = (6 * P.red_A[t] + 5) / kTile;
+      const int c0 = (6 * P.red_B[t]) / kTile, c1 = (6 * P.red_B[t] + 5) / kTile;
+      for (int j = c0; j <= c1; ++j) rlow[j] = std::max(rlow[j], r1);
+    }
+    for (int j = 1; j < P.NT; ++j) rlow[j] = std::max(rlow[j], rlow[j - 1]);
+    P.band_D.resize(P.NT);
+    P.max_D = 0;
+    for (int j = 0; j < P.NT; ++j) {
+      P.band_D[j] = rlow[j] - j;
+      P.max_D = std::max(P.max_D, P.band_D[j]);
+    }
   };
-  // ---- band layout ----
-  P.n_red = 6 * P.n_pose;
-  P.NT = (P.n_red + kTile - 1) / kTile;
-  std::vector<int32_t> rlow(P.NT);
-  for (int j = 0; j < P.NT; ++j) rlow[j] = j;
-  for (size_t t = 0; t < P.red_A.size(); ++t) {
-    const int r1 = (6 * P.red_A[t] + 5) / kTile;
-    const int c0 = (6 * P.red_B[t]) / kTile, c1 = (6 * P.red_B[t] + 5) / kTile;
-    for (int j = c0; j <= c1; ++j) rlow[j] = std::max(rlow[j], r1);
-  }
-  for (int j = 1; j < P.NT; ++j) rlow[j] = std::max(rlow[j], rlow[j - 1]);
-  P.band_D.resize(P.NT);
-  P.max_D = 0;
-  for (int j = 0; j < P.NT; ++j) {
-    P.band_D[j] = rlow[j] - j;
-    P.max_D = std::max(P.max_D, P.band_D[j]);
-  }
-  // The tile schedule depends on the pose-pair structure alone: it is built
-  // on a thread of its own while this one builds the gather lists (the
-  // schedule writes only its own Plan fields; joined before the target slots)
+  // The pair structure, the band and then the tile schedule depend on the
+  // factors' pose slots and the components' neighbour poses alone: they are
+  // built on a thread of its own while this one builds the point-side lists
+  // (the thread writes only its own Plan fields; the pair lists below wait
+  // for the pair index, the target slots for the whole thread)
+  std::promise<void> pairs_ready;
+  std::future<void> pairs_done = pairs_ready.get_future();
   bool sched_ok = true;
   std::thread sched;
   struct Joiner {
@@ -726,8 +732,15 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
       if (t.joinable()) t.join();
     }
   } sched_join{sched};
-  if (with_schedule) sched = std::thread([&P, &sched_ok] { sched_ok = build_tile_schedule(P, true); });
-  plan_mark("reduced system structure, band", tmark);
+  sched = std::thread([&] {
+    structure();
+    pairs_ready.set_value();
+    if (with_schedule) sched_ok = build_tile_schedule(P, true);
+  });
+  auto tid = [&](int32_t A, int32_t B) -> int32_t {
+    return dense ? id_dense[static_cast<size_t>(A) * span + (A - B)] : id_map.at(pkey(A, B));
+  };
+  plan_mark("reduced system structure (started)", tmark);
 
   plan_mark("before point-side gathers", tmark);
   std::vector<uint8_t> lone_grouped(P.n_pt, 0);   // per point: in a lone-point group
@@ -941,7 +954,8 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
   }
 
 
-  plan_mark("before reduced system targets", tmark);
+  pairs_done.wait();
+  plan_mark("before reduced system targets (pair index wait)", tmark);
   // ---- reduced system targets ----
   // Pose-pair blocks (A >= B) of the reduced system: every diagonal (for the
   // damping), the pose pairs of every factor and the neighbour-pose pairs of
