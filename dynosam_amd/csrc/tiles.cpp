@@ -181,20 +181,30 @@ void schedule(int NT, const std::vector<std::vector<int32_t>>& adj, const std::v
     int32_t R, a, b;  // ready level, operand slots (A B^T)
     int32_t own;      // owner of the source column
   };
-  // every slot's contributions in generation (column) order, as a linked
-  // list over one pool (no per-slot allocation), and the largest ready level
-  struct CNode {
-    Contrib c;
-    int32_t next;
+  // every slot's contributions in generation (column) order, in one pool
+  // laid out by slot (counted first: a column adds one contribution to each
+  // slot (s[x], s[y]), x >= y >= 1, of its structure), and the largest ready
+  // level. The slot of (s[x], s[y]) is found by walking column s[y]'s
+  // structure, which holds every s[x] (fill-path theorem), in step with x.
+  auto each_pair_slot = [&](const std::vector<int32_t>& s, auto&& fn) {   // fn(x, y, slot)
+    for (size_t y = 1; y < s.size(); ++y) {
+      const auto& sy = S.st[s[y]];
+      const int32_t base = S.slot_base[s[y]];
+      size_t pos = 0;
+      for (size_t x = y; x < s.size(); ++x) {
+        while (sy[pos] < s[x]) ++pos;
+        fn(x, y, base + static_cast<int32_t>(pos));
+      }
+    }
   };
-  std::vector<CNode> cpool;
-  std::vector<int32_t> chead(ns, -1), ctail(ns, -1), cmaxR(ns, 0);
+  std::vector<int64_t> cstart(static_cast<size_t>(ns) + 1, 0);
+  for (int cp = 0; cp < NT; ++cp) each_pair_slot(S.st[cp], [&](size_t, size_t, int32_t sl) { cstart[sl + 1]++; });
+  for (int32_t sl = 0; sl < ns; ++sl) cstart[sl + 1] += cstart[sl];
+  std::vector<Contrib> cpool(cstart[ns]);
+  std::vector<int64_t> cfill(cstart.begin(), cstart.end() - 1);
+  std::vector<int32_t> cmaxR(ns, 0);
   auto add_contrib = [&](int32_t sl, const Contrib& c) {
-    const int32_t id = static_cast<int32_t>(cpool.size());
-    cpool.push_back({c, -1});
-    if (ctail[sl] < 0) chead[sl] = id;
-    else cpool[ctail[sl]].next = id;
-    ctail[sl] = id;
+    cpool[cfill[sl]++] = c;
     cmaxR[sl] = std::max(cmaxR[sl], c.R);
   };
   std::vector<int32_t> lvlP(ns, 0);
@@ -208,6 +218,10 @@ void schedule(int NT, const std::vector<std::vector<int32_t>>& adj, const std::v
   };
   std::vector<LT> tasks;
   std::vector<int32_t> ppool;   // 2 ints per pair
+  // every contribution becomes one pair (of an update or of the panel that
+  // absorbs it); a slot has one panel and at most one update per ready level
+  ppool.reserve(2 * cpool.size());
+  tasks.reserve(2 * static_cast<size_t>(ns));
   const double T3 = static_cast<double>(kTile) * kTile * kTile;
   double flops = 0.0;
   std::vector<Contrib> all, cs, mine;
@@ -221,8 +235,7 @@ void schedule(int NT, const std::vector<std::vector<int32_t>>& adj, const std::v
   // panel, so that the tile leaves phase 0 as that rank's partial Schur
   // complement.
   auto plan_tile = [&](int32_t sl, int32_t P, int32_t* aoff, int32_t* an, int32_t town) {
-    all.clear();
-    for (int32_t id = chead[sl]; id >= 0; id = cpool[id].next) all.push_back(cpool[id].c);
+    all.assign(cpool.begin() + cstart[sl], cpool.begin() + cfill[sl]);
     std::sort(all.begin(), all.end(), [](const Contrib& x, const Contrib& y) { return x.R < y.R; });
     auto emit_updates = [&](const std::vector<Contrib>& v, size_t& q, int32_t limitR, int32_t own) {
       while (q < v.size() && v[q].R <= limitR) {
@@ -285,14 +298,13 @@ void schedule(int NT, const std::vector<std::vector<int32_t>>& adj, const std::v
       lvlP[sl] = t.lvl;
       tasks.push_back(t);
     }
-    for (size_t x = 1; x < s.size(); ++x) {
-      const int32_t sa = S.slot_base[cp] + static_cast<int32_t>(x);
-      for (size_t y = 1; y <= x; ++y) {
-        const int32_t sb = S.slot_base[cp] + static_cast<int32_t>(y);
-        add_contrib(S.slot(s[x], s[y]), {std::max(lvlP[sa], lvlP[sb]), sa, sb, cown});
-        flops += 2.0 * T3;
-      }
-    }
+    // (a slot receives at most one contribution per column, so the order of
+    // the pairs within a column does not change any slot's list)
+    each_pair_slot(s, [&](size_t x, size_t y, int32_t sl) {
+      const int32_t sa = S.slot_base[cp] + static_cast<int32_t>(x), sb = S.slot_base[cp] + static_cast<int32_t>(y);
+      add_contrib(sl, {std::max(lvlP[sa], lvlP[sb]), sa, sb, cown});
+      flops += 2.0 * T3;
+    });
   }
   S.flops = flops;
   tmark("contributions/tasks");
