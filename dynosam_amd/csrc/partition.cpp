@@ -18,11 +18,16 @@
 // partial Schur complement, which the ranks sum (one all-reduce), and every
 // rank factors the small separator system redundantly (solver.cpp).
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "plan.hpp"
+#include "plan_pool.hpp"
 
 namespace dynohip {
 
@@ -62,38 +67,68 @@ int build_partitioned_plan(const dynohip_graph_view& g, const uint64_t* keys, co
   // the global graph's structure (point chains, reduced system, the
   // partitioned tile schedule) without its gather lists: this rank's own
   // plan below builds those for its share only
+  static const bool timing = std::getenv("DYNOHIP_PLAN_TIMING") != nullptr;
+  auto t0 = std::chrono::steady_clock::now();
+  auto mark = [&](const char* what) {
+    const auto t = std::chrono::steady_clock::now();
+    if (timing) std::fprintf(stderr, "[part] %-40s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(t - t0).count());
+    t0 = t;
+  };
+  // The global structure first; its tile schedule then runs on a thread of
+  // its own while this rank's share and local plan are built (the owners
+  // they need follow from the pose-pair structure alone)
   Plan G;
-  int rc = build_plan(g, keys, kind, n, G, err, nranks, rank, true, true);
+  int rc = build_plan(g, keys, kind, n, G, err, nranks, rank, false, true);
   if (rc) return rc;
+  std::vector<int32_t> towner;
+  if (!partition_tile_owners(G, nranks, towner)) {
+    err = "graph too short in time for " + std::to_string(nranks) + " partitions";
+    return DYNOHIP_ESTRUCT;
+  }
+  bool sched_ok = true;
+  std::thread sched([&G, &sched_ok] { sched_ok = build_tile_schedule(G, true); });
+  struct Joiner {
+    std::thread& t;
+    ~Joiner() {
+      if (t.joinable()) t.join();
+    }
+  } sched_join{sched};
+  mark("global structure, owners");
   part = Partition();
   part.nranks = nranks;
   part.rank = rank;
   auto pose_owner = [&](int32_t p) {
     int32_t o = -1;
-    for (int t = (6 * p) / kTile; t <= (6 * p + 5) / kTile; ++t) o = merge_owner(o, G.tile_owner[t]);
+    for (int t = (6 * p) / kTile; t <= (6 * p + 5) / kTile; ++t) o = merge_owner(o, towner[t]);
     return o;
   };
   std::vector<int32_t> comp_of(G.n_pt);
-  for (int c = 0; c < G.n_comp; ++c)
-    for (int32_t i = G.comp_start[c]; i < G.comp_start[c + 1]; ++i) comp_of[i] = c;
-  // pass 1: landmark chains take the union of their factors' pose owners
+  parallel_for(G.n_comp, [&](int64_t c0, int64_t c1) {
+    for (int64_t c = c0; c < c1; ++c)
+      for (int32_t i = G.comp_start[c]; i < G.comp_start[c + 1]; ++i) comp_of[i] = static_cast<int32_t>(c);
+  });
+  // pass 1: every factor's pose owner (on the workers), then landmark chains
+  // take the union of their factors' pose owners
   std::vector<int32_t> comp_own(G.n_comp, -1);
   std::vector<int32_t> fown[kNTypes];
   for (int t = 0; t < kNTypes; ++t) {
     const TypePlan& tp = G.types[t];
     const int nk = kNKeys[t];
-    fown[t].assign(tp.n, -1);
-    for (int i = 0; i < tp.n; ++i) {
-      int32_t o = -1;
-      for (int sl = 0; sl < nk; ++sl)
-        if (kSlotKind[t][sl] == 0) o = merge_owner(o, pose_owner(tp.idx[i * nk + sl]));
-      fown[t][i] = o;
+    fown[t].resize(tp.n);
+    parallel_for(tp.n, [&](int64_t i0, int64_t i1) {
+      for (int64_t i = i0; i < i1; ++i) {
+        int32_t o = -1;
+        for (int sl = 0; sl < nk; ++sl)
+          if (kSlotKind[t][sl] == 0) o = merge_owner(o, pose_owner(tp.idx[i * nk + sl]));
+        fown[t][i] = o;
+      }
+    });
+    for (int i = 0; i < tp.n; ++i)
       for (int sl = 0; sl < nk; ++sl)
         if (kSlotKind[t][sl] == 1) {
           const int c = comp_of[tp.idx[i * nk + sl]];
-          comp_own[c] = merge_owner(comp_own[c], o);
+          comp_own[c] = merge_owner(comp_own[c], fown[t][i]);
         }
-    }
   }
   for (int c = 0; c < G.n_comp; ++c) {
     if (comp_own[c] == -2) {
@@ -102,35 +137,57 @@ int build_partitioned_plan(const dynohip_graph_view& g, const uint64_t* keys, co
     }
     if (comp_own[c] < 0) comp_own[c] = 0;  // separator-only chains: rank 0
   }
-  // pass 2: factor owners, the local graph in the global factor order
+  // pass 2: factor owners, the local graph in the global factor order (an
+  // ordered filter on the workers: owners and counts per chunk, then each
+  // chunk's factors copied to their place)
   const dynohip_factor_block* gb[kNTypes] = {&g.pose_to_point, &g.landmark_motion_ternary, &g.between,
                                              &g.prior, &g.landmark_motion_pose, &g.landmark_pose_smoothing};
   lg = GraphStore();
   for (int t = 0; t < kNTypes; ++t) {
     const TypePlan& tp = G.types[t];
-    const int nk = kNKeys[t];
-    for (int i = 0; i < tp.n; ++i) {
-      int32_t o = fown[t][i];
-      for (int sl = 0; sl < nk; ++sl)
-        if (kSlotKind[t][sl] == 1) o = merge_owner(o, comp_own[comp_of[tp.idx[i * nk + sl]]]);
-      if (o == -2) {
+    const int nk = kNKeys[t], md = kMeasDim[t], dd = kDim[t];
+    const int64_t nt = tp.n;
+    const int nw = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(PlanPool::get().workers(), nt / 8192 + 1)));
+    std::vector<int64_t> cnt(static_cast<size_t>(nw) + 1, 0);
+    std::vector<uint8_t> bad(static_cast<size_t>(nw), 0);
+    PlanPool::get().run(nw, [&](int w) {
+      int64_t c = 0;
+      for (int64_t i = nt * w / nw; i < nt * (w + 1) / nw; ++i) {
+        int32_t o = fown[t][i];
+        for (int sl = 0; sl < nk; ++sl)
+          if (kSlotKind[t][sl] == 1) o = merge_owner(o, comp_own[comp_of[tp.idx[i * nk + sl]]]);
+        if (o == -2) bad[w] = 1;
+        if (o < 0) o = 0;
+        fown[t][i] = o;
+        c += o == rank;
+      }
+      cnt[w + 1] = c;
+    });
+    for (int w = 0; w < nw; ++w)
+      if (bad[w]) {
         err = "internal: a factor spans two partitions";
         return DYNOHIP_ESTRUCT;
       }
-      if (o < 0) o = 0;
-      part.factors_total++;
-      if (o != rank) continue;
-      part.factors_local++;
-      lg.n[t]++;
-      lg.keys[t].insert(lg.keys[t].end(), gb[t]->keys + static_cast<size_t>(i) * nk,
-                        gb[t]->keys + static_cast<size_t>(i + 1) * nk);
-      if (kMeasDim[t])
-        lg.meas[t].insert(lg.meas[t].end(), gb[t]->measured + static_cast<size_t>(i) * kMeasDim[t],
-                          gb[t]->measured + static_cast<size_t>(i + 1) * kMeasDim[t]);
-      lg.sig[t].insert(lg.sig[t].end(), gb[t]->sigmas + static_cast<size_t>(i) * kDim[t],
-                       gb[t]->sigmas + static_cast<size_t>(i + 1) * kDim[t]);
-      lg.hub[t].push_back(gb[t]->huber_k ? gb[t]->huber_k[i] : 0.0);
-    }
+    for (int w = 0; w < nw; ++w) cnt[w + 1] += cnt[w];
+    const int64_t nl = cnt[nw];
+    part.factors_total += nt;
+    part.factors_local += nl;
+    lg.n[t] = nl;
+    lg.keys[t].resize(nl * nk);
+    lg.meas[t].resize(nl * md);
+    lg.sig[t].resize(nl * dd);
+    lg.hub[t].resize(nl);
+    PlanPool::get().run(nw, [&](int w) {
+      int64_t o = cnt[w];
+      for (int64_t i = nt * w / nw; i < nt * (w + 1) / nw; ++i) {
+        if (fown[t][i] != rank) continue;
+        std::memcpy(lg.keys[t].data() + o * nk, gb[t]->keys + i * nk, nk * sizeof(uint64_t));
+        if (md) std::memcpy(lg.meas[t].data() + o * md, gb[t]->measured + i * md, md * sizeof(double));
+        std::memcpy(lg.sig[t].data() + o * dd, gb[t]->sigmas + i * dd, dd * sizeof(double));
+        lg.hub[t][o] = gb[t]->huber_k ? gb[t]->huber_k[i] : 0.0;
+        ++o;
+      }
+    });
   }
   // values: every pose, this rank's landmarks
   part.value_owner.assign(n, -1);
@@ -146,9 +203,21 @@ int build_partitioned_plan(const dynohip_graph_view& g, const uint64_t* keys, co
       part.global_of.push_back(static_cast<int32_t>(v));
     }
   }
+  mark("owners, local graph and values");
   const dynohip_graph_view lv = lg.view();
   rc = build_plan(lv, part.keys.data(), part.kind.data(), part.keys.size(), L, err, nranks, rank, false);
   if (rc) return rc;
+  mark("local plan");
+  sched.join();
+  if (!sched_ok) {
+    err = "graph too short in time for " + std::to_string(nranks) + " partitions";
+    return DYNOHIP_ESTRUCT;
+  }
+  if (G.tile_owner != towner) {
+    err = "internal: tile owners differ from the schedule's";
+    return DYNOHIP_ESTRUCT;
+  }
+  mark("global schedule (join)");
   if (L.n_pose != G.n_pose || L.NT != G.NT || L.pose_key != G.pose_key) {
     err = "internal: local pose numbering differs from the global one";
     return DYNOHIP_ESTRUCT;
@@ -189,6 +258,7 @@ int build_partitioned_plan(const dynohip_graph_view& g, const uint64_t* keys, co
   compute_red_slots(L);
   // damping: interior rows by their owner, separator rows by rank 0 (the
   // ranks' diagonals are summed in the exchange)
+  mark("schedule into the local plan");
   part.damp_row.assign(static_cast<size_t>(L.n_red), 0);
   for (int q = 0; q < L.n_red; ++q) {
     const int32_t o = L.tile_owner[q / kTile];

@@ -141,12 +141,6 @@ void csr_target_ranges(size_t ntargets, const std::vector<int64_t>& tcut, Emit&&
                  std::chrono::duration<double, std::milli>(T3 - T2).count());
 }
 
-// body(b, e) over [0, n) in contiguous ranges on the planner's workers
-template <typename Body>
-void parallel_for(int64_t n, Body&& body) {
-  const int nw = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(PlanPool::get().workers(), n / 8192 + 1)));
-  PlanPool::get().run(nw, [&](int r) { body(n * r / nw, n * (r + 1) / nw); });
-}
 
 // even cut of [0, n) targets into the planner's workers, one per 1024
 // targets at most (a sliding window's few hundred targets take one: each

@@ -243,6 +243,12 @@ void plan_recycle(Plan& P);
 // of the planner pool (the schedule then runs beside the gather builds).
 bool build_tile_schedule(Plan& P, bool own_threads = false);
 
+// The tile owners of the partitioned schedule (per natural tile: rank, -1 =
+// top separator) from the pose-pair structure alone: the top splits of the
+// dissection do not depend on the leaf size, so this equals the schedule's
+// tile_owner. False when the graph is too short in time for nranks.
+bool partition_tile_owners(const Plan& P, int nranks, std::vector<int32_t>& owner);
+
 // Plan::red_slot from the tile structure (after the tile schedule).
 void compute_red_slots(Plan& P);
 

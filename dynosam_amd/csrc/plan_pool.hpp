@@ -111,6 +111,13 @@ class PlanPool {
   std::atomic<uint64_t> gen_{0};
 };
 
+// body(b, e) over [0, n) in contiguous ranges on the planner's workers
+template <typename Body>
+void parallel_for(int64_t n, Body&& body) {
+  const int nw = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(PlanPool::get().workers(), n / 8192 + 1)));
+  PlanPool::get().run(nw, [&](int r) { body(n * r / nw, n * (r + 1) / nw); });
+}
+
 // body(b, e) over chunks of [0, n) handed out one at a time (work of uneven
 // size per item, e.g. chains sorted longest first)
 template <typename Body>

@@ -592,7 +592,50 @@ void filter_tasks(const std::vector<TileTask>& all, const std::vector<int32_t>& 
   }
 }
 
+// largest tile each tile shares a reduced block with (at least itself)
+std::vector<int32_t> tile_maxnb(const Plan& P) {
+  std::vector<int32_t> maxnb(P.NT);
+  for (int t = 0; t < P.NT; ++t) maxnb[t] = t;
+  for (size_t q = 0; q < P.red_A.size(); ++q) {
+    const int r1 = (6 * P.red_A[q] + 5) / kTile;
+    const int c0 = (6 * P.red_B[q]) / kTile;
+    // the pair's tiles span rows r0..r1 and columns c0..c1; the smallest
+    // tile of any cross pair is >= c0 and the largest <= r1
+    maxnb[c0] = std::max(maxnb[c0], r1);
+    const int c1 = (6 * P.red_B[q] + 5) / kTile, r0 = (6 * P.red_A[q]) / kTile;
+    for (int a = r0; a <= r1; ++a)
+      for (int b = c0; b <= c1; ++b)
+        if (a != b) maxnb[std::min(a, b)] = std::max(maxnb[std::min(a, b)], std::max(a, b));
+  }
+  return maxnb;
+}
+
+// the tile owners of nd_order_part's top splits (in natural tile order)
+bool owners_part(int lo, int hi, const std::vector<int32_t>& maxnb, int nr, int r0, std::vector<int32_t>& owner) {
+  if (nr == 1) {
+    for (int t = lo; t < hi; ++t) owner[t] = r0;
+    return true;
+  }
+  const int n = hi - lo;
+  if (n < 3) return false;
+  const int m = lo + n / 2;
+  int reach = m - 1;
+  for (int t = lo; t < m; ++t) reach = std::max(reach, std::min(maxnb[t], hi - 1));
+  const int s_end = reach + 1;
+  if (hi - s_end < 1 || s_end <= m) return false;
+  const int nl = nr / 2;
+  if (!owners_part(lo, m, maxnb, nl, r0, owner)) return false;
+  if (!owners_part(s_end, hi, maxnb, nr - nl, r0 + nl, owner)) return false;
+  for (int t = m; t < s_end; ++t) owner[t] = -1;
+  return true;
+}
+
 }  // namespace
+
+bool partition_tile_owners(const Plan& P, int nranks, std::vector<int32_t>& owner) {
+  owner.assign(P.NT, 0);
+  return owners_part(0, P.NT, tile_maxnb(P), std::max(1, nranks), 0, owner);
+}
 
 bool build_tile_schedule(Plan& P, bool own_threads) {
   const int NT = P.NT;
