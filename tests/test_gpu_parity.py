@@ -456,6 +456,39 @@ def test_bit_reproducible(gpu_available):
     assert np.array_equal(a, s2.values_data())
 
 
+def test_replan_on_reused_handles(gpu_available):
+    """A handle re-planned for other graphs (its plan arrays recycled, the
+    factor records uploaded while planning, the pinned staging buffers
+    reused), and a fresh handle that takes over a destroyed one's host
+    arrays (HostCache), give the values of a first solve on a new handle,
+    bit for bit."""
+    graphs = [synth.generate(n, seed=sd)[:2] for n, sd in (("C1", 42), ("T2", 43), ("C1", 44))]
+    ref = []
+    for g, v in graphs:
+        h = Solver(0)
+        h.set_graph(g)
+        h.set_values(v)
+        h.optimize()
+        ref.append(h.values_data())
+        h.close()
+    s = Solver(0)
+    for k in (0, 1, 2, 1, 0):   # larger, smaller, larger again
+        g, v = graphs[k]
+        s.set_graph(g)
+        s.set_values(v)
+        s.optimize()
+        assert np.array_equal(s.values_data(), ref[k]), k
+    s.close()
+    for k in (2, 0):
+        g, v = graphs[k]
+        h = Solver(0)   # takes the closed handle's plan arrays and graph copy
+        h.set_graph(g)
+        h.set_values(v)
+        h.optimize()
+        assert np.array_equal(h.values_data(), ref[k]), k
+        h.close()
+
+
 def test_full_size_c2_properties(gpu_available):
     g, v, _, s = make("C2")
     sg = s.optimize()
