@@ -1929,6 +1929,22 @@ __global__ __launch_bounds__(64) void k_sep_rhs(const int32_t* __restrict__ tile
   r[static_cast<int64_t>(tile[q]) * kTile + l] -= acc;
 }
 
+// one workgroup per chunk: 16-byte copies, then the tail bytes
+__global__ __launch_bounds__(256) void k_scatter_chunks(const char* __restrict__ data,
+                                                        const CopyChunk* __restrict__ chunks) {
+  const CopyChunk c = chunks[blockIdx.x];
+  char* dst = reinterpret_cast<char*>(c.dst);
+  const char* src = data + c.src_off;
+  const uint32_t n16 = c.bytes / 16;
+  for (uint32_t i = threadIdx.x; i < n16; i += blockDim.x)
+    reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+  for (uint32_t i = 16 * n16 + threadIdx.x; i < c.bytes; i += blockDim.x) dst[i] = src[i];
+}
+
+void launch_scatter_chunks(const char* data, const CopyChunk* chunks, int n_chunks, hipStream_t s) {
+  if (n_chunks > 0) k_scatter_chunks<<<n_chunks, 256, 0, s>>>(data, chunks);
+}
+
 void launch_sep_rhs(int n_sep_tiles, const int32_t* tile, const int32_t* start, const int32_t* slot, double* r,
                     double* contrib, hipStream_t s) {
   if (n_sep_tiles > 0) k_sep_rhs<<<n_sep_tiles, 64, 0, s>>>(tile, start, slot, r, contrib);

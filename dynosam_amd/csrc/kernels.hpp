@@ -142,6 +142,16 @@ void launch_gather_reduced(const GatherDev& band, const int32_t* tA, const int32
                            const uint8_t* damp = nullptr);
 // partitioned: r[rows of separator tile] -= sum of this rank's contributions
 // L(s,c) y_c (c interior), which are then zeroed; CSR over separator tiles
+// Plan upload: one host-to-device copy of a staged block, then this kernel
+// places its pieces (chunks of <= 64 KB, 16-byte aligned) into their device
+// arrays.
+struct CopyChunk {
+  uint64_t dst;      // device address
+  uint32_t src_off;  // from the staged data's start
+  uint32_t bytes;
+};
+void launch_scatter_chunks(const char* data, const CopyChunk* chunks, int n_chunks, hipStream_t s);
+
 void launch_sep_rhs(int n_sep_tiles, const int32_t* tile, const int32_t* start, const int32_t* slot, double* r,
                     double* contrib, hipStream_t s);
 
