@@ -19,6 +19,8 @@
 #include <map>
 #include <memory>
 #include <set>
+#include <unordered_map>
+#include <unordered_set>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -110,7 +112,9 @@ struct ObjectNode {
 
 struct Map {
   std::map<uint64_t, FrameNode> frames;
-  std::map<int64_t, LandmarkNode> landmarks;
+  // by tracklet id; hashed (looked up per measurement and per factor), so a
+  // caller that needs tracklet order sorts the ids itself
+  std::unordered_map<int64_t, LandmarkNode> landmarks;
   std::map<int32_t, ObjectNode> objects;
 
   const FrameNode* frame(uint64_t f) const {
@@ -189,13 +193,17 @@ struct Map {
       for (const auto& kv : landmarks.at(t).measurements) out.insert(kv.first);
     return out;
   }
-  // ObjectNode::getLandmarksSeenAtFrame (MapNodes-inl.hpp:252-262)
+  // ObjectNode::getLandmarksSeenAtFrame (MapNodes-inl.hpp:252-262): the
+  // object's tracklets seen at f, ascending. Walked from the frame's dynamic
+  // tracklets (the same set: a dynamic measurement at f puts its tracklet in
+  // both, and a tracklet never changes object) instead of every tracklet the
+  // object ever had, which grows with the stream.
   std::vector<int64_t> object_landmarks_at(int32_t obj, uint64_t f) const {
     std::vector<int64_t> out;
-    const ObjectNode* on = object(obj);
-    if (!on) return out;
-    for (int64_t t : on->dynamic_landmarks)
-      if (landmarks.at(t).seen_at(f)) out.push_back(t);
+    const FrameNode* fn = frame(f);
+    if (!fn || !object(obj)) return out;
+    for (int64_t t : fn->dynamic_landmarks)
+      if (landmarks.at(t).object_id == obj) out.push_back(t);
     return out;
   }
   bool initial_sensor_pose(uint64_t f, P3* X) const {
@@ -246,8 +254,14 @@ void values_insert(Values& vals, uint64_t key, const Value& v) {
 void values_insert(Values& vals, const Values& other) {
   for (const auto& kv : other) values_insert(vals, kv.first, kv.second);
 }
+// both maps ascend, so each key is tried next to the previous one first (O(1)
+// when the keys are adjacent in vals, as in a window's own theta)
 void values_insert_or_assign(Values& vals, const Values& other) {
-  for (const auto& kv : other) vals[kv.first] = kv.second;
+  auto hint = vals.begin();
+  for (const auto& kv : other) {
+    hint = vals.insert_or_assign(hint, kv.first, kv.second);
+    ++hint;
+  }
 }
 
 enum FactorType { kPoseToPoint = 0, kTernary = 1, kBetween = 2, kPrior = 3, kMotionPose = 4, kPoseSmoothing = 5 };
@@ -269,7 +283,12 @@ struct Factor {
 
 struct Graph {
   std::vector<Factor> factors;
+  // a sink for a new_factors list nobody reads (constructGraph returns the
+  // fresh updater's own factors_, which hold the same factors): adds and
+  // appends are dropped instead of copying every factor twice
+  bool discard = false;
   void add(uint8_t type, std::initializer_list<uint64_t> keys, const double* meas, const Noise& n) {
+    if (discard) return;
     Factor f;
     std::memset(&f, 0, sizeof(f));
     f.type = type;
@@ -279,7 +298,33 @@ struct Graph {
     f.noise = n;
     factors.push_back(f);
   }
-  void append(const Graph& o) { factors.insert(factors.end(), o.factors.begin(), o.factors.end()); }
+  void append(const Graph& o) {
+    if (!discard) factors.insert(factors.end(), o.factors.begin(), o.factors.end());
+  }
+};
+
+// Where the factors of one update go. The reference collects them in a local
+// graph appended to factors_ and to the caller's new_factors at the end; when
+// new_factors is a discard sink they go straight into factors_ (one copy
+// fewer). An exception leaves factors_ as it was, as in the reference.
+struct FactorSink {
+  Graph& factors;
+  Graph& new_factors;
+  Graph local;
+  size_t mark;
+  bool done = false;
+  FactorSink(Graph& f, Graph& nf) : factors(f), new_factors(nf), mark(f.factors.size()) {}
+  Graph& out() { return new_factors.discard ? factors : local; }
+  void commit() {
+    if (!new_factors.discard) {
+      factors.append(local);
+      new_factors.append(local);
+    }
+    done = true;
+  }
+  ~FactorSink() {
+    if (!done) factors.factors.resize(mark);
+  }
 };
 
 // SoA export of a factor list (dynohip_graph_view)
@@ -350,8 +395,9 @@ struct Formulation {
   NoiseModels noise;
   Values theta;
   Graph factors;
-  std::set<uint64_t> is_other_values_in_map;       // Formulation.hpp:448
-  std::set<int64_t> is_dynamic_tracklet_in_map;    // WorldPoseEstimator.hpp:79
+  // membership only (never iterated), hashed
+  std::unordered_set<uint64_t> is_other_values_in_map;       // Formulation.hpp:448
+  std::unordered_set<int64_t> is_dynamic_tracklet_in_map;    // WorldPoseEstimator.hpp:79
   // WorldMotionAccessor::object_pose_cache_ (object -> frame -> pose)
   std::map<int32_t, std::map<uint64_t, P3>> object_pose_cache;
   std::string err;
@@ -516,7 +562,8 @@ struct Formulation {
 
   // Formulation::updateStaticObservations (Formulation-impl.hpp:203-305)
   void update_static(uint64_t k, Values& new_values, Graph& new_factors, bool do_backtrack) {
-    Graph internal;
+    FactorSink sink(factors, new_factors);
+    Graph& internal = sink.out();
     const FrameNode* fk = map->frame(k);
     DB_CHECK(fk != nullptr, DYNOHIP_ESTATE, "updateStaticObservations: frame not in map");
     P3 T_world_camera_frontend;
@@ -542,8 +589,7 @@ struct Formulation {
       }
     }
     values_insert_or_assign(theta, new_values);
-    factors.append(internal);
-    new_factors.append(internal);
+    sink.commit();
   }
 
   struct PointContext {
@@ -662,7 +708,8 @@ struct Formulation {
   // Formulation::updateDynamicObservations (Formulation-impl.hpp:307-584)
   void update_dynamic(uint64_t k, Values& new_values, Graph& new_factors, bool do_backtrack) {
     constexpr size_t kMinNumberPoints = 3u;
-    Graph internal;
+    FactorSink sink(factors, new_factors);
+    Graph& internal = sink.out();
     UpdateResult result;
     const uint64_t k_1 = k - 1u;
     const FrameNode* fk = map->frame(k);
@@ -743,8 +790,7 @@ struct Formulation {
         ++idx;
       }
     }
-    factors.append(internal);
-    new_factors.append(internal);
+    sink.commit();
   }
 
   // ---- WorldMotionAccessor::postUpdateCallback (WorldMotionEstimator.cc:68-152)
@@ -950,6 +996,7 @@ std::unique_ptr<Formulation> construct_graph(Map* map, const dynob_params& p, ui
   auto u = std::make_unique<Formulation>(map, p);
   Values new_values;
   Graph new_factors;
+  new_factors.discard = true;   // u->factors is the window's graph
   for (uint64_t f = from; f <= to; ++f) {
     P3 T;
     DB_CHECK(map->initial_sensor_pose(f, &T), DYNOHIP_ESTATE, "no frontend pose for frame " + std::to_string(f));
@@ -1319,6 +1366,7 @@ int dynob_get_static_landmarks(dynob_formulation* f, uint64_t frame_id, int64_t*
     if (frame_id == UINT64_MAX) {  // getFullStaticMap (Accessor-impl.hpp:194-214)
       for (const auto& kv : f->f->map->landmarks)
         if (kv.second.is_static()) ids.push_back(kv.first);
+      std::sort(ids.begin(), ids.end());   // the reference's map is ordered by tracklet id
     } else {  // getStaticLandmarkEstimates (Accessor-impl.hpp:166-192)
       const FrameNode* fn = f->f->map->frame(frame_id);
       DB_CHECK(fn != nullptr, DYNOHIP_ESTATE, "getStaticLandmarkEstimates: frame not in map");
@@ -1608,6 +1656,7 @@ int dynob_module_spin(dynob_module* m, const dynob_input_packet* in, dynob_spin_
     const P3 T_k = fn.X_world;
     Values nv;
     Graph nf;
+    nf.discard = true;   // the spin's new factors are only kept in the updater's factors_
     if (!m->bootstrapped) {
       // boostrapSpinImpl (RGBDBackendModule.cc:129-152)
       uint64_t s, e;
