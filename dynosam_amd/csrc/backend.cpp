@@ -715,6 +715,33 @@ struct Formulation {
     const FrameNode* fk = map->frame(k);
     DB_CHECK(fk != nullptr, DYNOHIP_ESTATE, "updateDynamicObservations: frame not in map");
     DB_CHECK(map->frame(k_1) != nullptr, DYNOHIP_ESTATE, "updateDynamicObservations: frame k-1 not in map");
+    // The camera poses at k-1 and k read for every point: the loop inserts
+    // only points and motions into theta, so each is looked up once, on
+    // first use (a failing lookup is not kept and fails at the same point).
+    struct PoseMemo {
+      bool have = false;
+      P3 X;
+    };
+    PoseMemo iol_memo[2], sp_memo[2];
+    auto iol_pose = [&](uint64_t f) -> P3 {
+      if (f != k_1 && f != k) return initial_or_linearized_sensor_pose(f);
+      PoseMemo& m = iol_memo[f == k];
+      if (!m.have) {
+        m.X = initial_or_linearized_sensor_pose(f);
+        m.have = true;
+      }
+      return m.X;
+    };
+    auto sensor_pose_memo = [&](uint64_t f, P3* X) -> bool {
+      if (f != k_1 && f != k) return sensor_pose(f, X);
+      PoseMemo& m = sp_memo[f == k];
+      if (!m.have) {
+        if (!sensor_pose(f, &m.X)) return false;
+        m.have = true;
+      }
+      *X = m.X;
+      return true;
+    };
     for (int32_t obj : fk->objects_seen) {
       if (!map->object_motion_expected(k, obj)) continue;
       const std::vector<int64_t> seen_k = map->object_landmarks_at(obj, k);
@@ -741,7 +768,7 @@ struct Formulation {
                      "tracklet " + std::to_string(t) + " is not seen in consecutive frames");
             if (it->first > k) break;
             P3 X_k_1;
-            DB_CHECK(sensor_pose(prev->first, &X_k_1), DYNOHIP_ESTATE,
+            DB_CHECK(sensor_pose_memo(prev->first, &X_k_1), DYNOHIP_ESTATE,
                      "Failed cam pose query at frame " + std::to_string(prev->first));
             PointContext c;
             c.tracklet = t;
@@ -751,7 +778,7 @@ struct Formulation {
             // the reference reads the sensor pose at k-1 here as well
             // (Formulation-impl.hpp:470-471), and initialises the point at k
             // with it; kept for parity
-            c.X_k_measured = initial_or_linearized_sensor_pose(prev->first);
+            c.X_k_measured = iol_pose(prev->first);
             c.X_k_1_measured = X_k_1;
             c.is_starting_motion_frame = (it == start_it);
             Values local;
@@ -765,8 +792,8 @@ struct Formulation {
           c.object = obj;
           c.frame_k_1 = k_1;
           c.frame_k = k;
-          c.X_k_1_measured = initial_or_linearized_sensor_pose(k_1);
-          c.X_k_measured = initial_or_linearized_sensor_pose(k);
+          c.X_k_1_measured = iol_pose(k_1);
+          c.X_k_measured = iol_pose(k);
           c.is_starting_motion_frame = false;
           Values local;
           dynamic_point_update(c, result, local, internal);
