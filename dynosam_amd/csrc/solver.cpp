@@ -416,6 +416,9 @@ struct dynohip_solver {
   // LM state
   dynohip_lm_params prm{};
   double lambda = 1e-5, error = 0.0;
+  // `error` was computed by lm_reset at the current values and nothing has
+  // moved them since (set_values then optimize: one initial error, not two)
+  bool error_fresh = false;
   // the arena holds the linearisation at the current values (left there by
   // the speculative linearisation of an accepted step); next_oldlin is its
   // linear error at delta = 0
@@ -920,6 +923,7 @@ void compute_base_stats(dynohip_solver* s) {
 // LevenbergMarquardtOptimizer::iterate()
 int lm_iterate(dynohip_solver* s) {
   hipStream_t st = s->stream;
+  s->error_fresh = false;
   // Speculation: right after each try, the linearisation at the candidate
   // values is enqueued too (before the host has seen whether the step is
   // accepted), so the GPU is not idle while the host decides. Accepted: the
@@ -1202,6 +1206,7 @@ int dynohip_set_graph(dynohip_solver* s, const dynohip_graph_view* g) {
   s->lin_valid = false;
   s->has_plan = false;
   s->has_values = false;
+  s->error_fresh = false;
   return DYNOHIP_OK;
 }
 
@@ -1239,6 +1244,7 @@ int dynohip_set_values(dynohip_solver* s, const uint64_t* keys, const uint8_t* k
   if (!s || (n && (!keys || !kind || !data))) return DYNOHIP_EINVAL;
   if (!s->has_graph) return set_err(s, DYNOHIP_ESTATE, "set_graph first");
   (void)hipSetDevice(s->device);
+  s->error_fresh = false;
   const bool same = s->has_plan && s->value_keys.size() == n &&
                     std::equal(s->value_keys.begin(), s->value_keys.end(), keys);
   if (!same) {
@@ -1365,7 +1371,10 @@ int dynohip_lm_reset(dynohip_solver* s, const dynohip_lm_params* p) {
   s->n_lin = 0;
   s->n_solves = 0;
   for (double& v : s->phase_ms) v = 0.0;
-  return compute_error(s, s->pose.p, s->pt.p, &s->error);
+  if (s->error_fresh) return DYNOHIP_OK;
+  rc = compute_error(s, s->pose.p, s->pt.p, &s->error);
+  s->error_fresh = rc == 0;
+  return rc;
 }
 
 int dynohip_iterate(dynohip_solver* s, dynohip_lm_summary* out) {
@@ -1520,6 +1529,7 @@ int dynohip_values_restore(dynohip_solver* s) {
     return set_err(s, DYNOHIP_ESTATE, "no snapshot of the current graph's values");
   (void)hipSetDevice(s->device);
   s->lin_valid = false;
+  s->error_fresh = false;
   if (P.n_pose) HIPCHK(s, hipMemcpyAsync(s->pose.p, s->pose_snap.p, 12ull * P.n_pose * sizeof(double), hipMemcpyDeviceToDevice, s->stream));
   if (P.n_pt) HIPCHK(s, hipMemcpyAsync(s->pt.p, s->pt_snap.p, 3ull * P.n_pt * sizeof(double), hipMemcpyDeviceToDevice, s->stream));
   HIPCHK(s, hipStreamSynchronize(s->stream));
@@ -1564,6 +1574,7 @@ int dynohip_set_partition(dynohip_solver* s, int nranks, int rank, dynohip_allre
   s->has_plan = false;
   s->has_values = false;
   s->lin_valid = false;
+  s->error_fresh = false;
   return DYNOHIP_OK;
 }
 
