@@ -1039,10 +1039,16 @@ std::unique_ptr<Formulation> construct_graph(Map* map, const dynob_params& p, ui
   return u;
 }
 
-int solve(dynob_module* m, const Formulation& problem, dynob_spin_result* r) {
+// the problem handed to the solver (gtsam's getGraph() / getTheta() copies,
+// taken before the reference starts its optimise timer)
+void export_problem(dynob_module* m, const Formulation& problem) {
   m->last_graph.build(problem.factors);
   m->last_values.build(problem.theta);
   m->last_optimised = m->last_values.data;
+}
+
+// LM on the exported problem (export_problem first), then updateTheta
+int solve(dynob_module* m, dynob_spin_result* r) {
   if (!m->mp.optimize) return DYNOHIP_OK;
   if (!m->solver) {
     const int rc = dynohip_create(m->mp.device_id, &m->solver);
@@ -1710,8 +1716,10 @@ int dynob_module_spin(dynob_module* m, const dynob_input_packet* in, dynob_spin_
       if (dynohip_full_batch_trigger(m->mp.full_batch_frame, k)) {
         // RGBDBackendModule.cc:211-231
         m->stats.add(name + ".full_batch_opt_num_vars_all", static_cast<double>(up.theta.size()));
+        // getTheta() / getGraph() precede the timer (RGBDBackendModule.cc:209-216)
+        export_problem(m, up);
         TimingStatsCollector timer(m->stats, name + ".full_batch_opt");
-        const int rc = solve(m, up, r);
+        const int rc = solve(m, r);
         DB_CHECK(rc == DYNOHIP_OK, rc, m->err);
         if (r->optimized) {
           m->stats.add(name + ".inner_iterations", r->inner_iterations);
@@ -1733,9 +1741,12 @@ int dynob_module_spin(dynob_module* m, const dynob_input_packet* in, dynob_spin_
         r->ms_construct += now_ms() - tc;
         r->window_start = s;
         r->window_end = e;
+        // the window's graph and values exist before the optimise timer
+        // starts (RGBDBackendModule.cc:358-368)
+        export_problem(m, *window);
         TimingStatsCollector timer(m->stats, name + ".sliding_window_optimise");
         m->stats.add(name + ".sliding_window_optimise_num_vars_all", static_cast<double>(window->theta.size()));
-        const int rc = solve(m, *window, r);
+        const int rc = solve(m, r);
         DB_CHECK(rc == DYNOHIP_OK, rc, m->err);
       }
     }
