@@ -1024,6 +1024,13 @@ std::unique_ptr<Formulation> construct_graph(Map* map, const dynob_params& p, ui
   Values new_values;
   Graph new_factors;
   new_factors.discard = true;   // u->factors is the window's graph
+  // room for the window's factors up front (a PoseToPoint per static
+  // measurement, at most three factors per dynamic one), so the list is not
+  // regrown and copied as the frames are added
+  size_t est = 0;
+  for (uint64_t f = from; f <= to; ++f)
+    if (const FrameNode* fn = map->frame(f)) est += fn->static_landmarks.size() + 3 * fn->dynamic_landmarks.size() + 4;
+  u->factors.factors.reserve(est);
   for (uint64_t f = from; f <= to; ++f) {
     P3 T;
     DB_CHECK(map->initial_sensor_pose(f, &T), DYNOHIP_ESTATE, "no frontend pose for frame " + std::to_string(f));
