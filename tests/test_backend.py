@@ -286,6 +286,36 @@ def test_tracklet_gap_is_an_error():
             of.update_dynamic(k)
 
 
+def test_module_spin_error_leaves_factors_unchanged():
+    """The module's spin writes the update's factors straight into the
+    formulation's factors_ (its new_factors list is never read); a spin that
+    fails inside updateDynamicObservations must leave factors_ as the
+    reference does (the local graph is only appended on success)."""
+    I = np.concatenate([np.eye(3).reshape(9), np.zeros(3)])
+    # tracklet 3 (processed last at frame 4) misses frame 3, so the failing
+    # update has already written the factors of tracklets 0-2
+    frames = {0: [0, 1, 2, 3], 1: [0, 1, 2, 3], 2: [0, 1, 2, 3], 3: [0, 1, 2], 4: [0, 1, 2, 3]}
+    m = backend.RGBDBackendModule(full_batch_frame=100, optimize=False, post_update=False)
+    types_before = None
+    for k, trks in frames.items():
+        st = make_measurements([50], [0], [k], np.array([[0.0, 0.0, 9.0]]))
+        dy = make_measurements(trks, [1] * len(trks), [k] * len(trks), np.array([[t, 0.0, 5.0] for t in trks]))
+        pk = backend.RGBDInstanceOutputPacket(frame_id=k, T_world_camera=I, static_measurements=st,
+                                              dynamic_measurements=dy)
+        if k < 4:
+            m.spinOnce(pk)
+            types_before = m.formulation.factorTypes()
+        else:
+            with pytest.raises(BackendError):
+                m.spinOnce(pk)   # tracklet 3 seen at 4, in the map, but no point at 3
+    types_after = m.formulation.factorTypes()
+    # the odometry and static factors of frame 4 were committed before the
+    # failing dynamic update; nothing of the dynamic update was
+    assert np.array_equal(types_after[:len(types_before)], types_before)
+    assert set(types_after[len(types_before):].tolist()) <= {2, 0}   # Between, static PoseToPoint
+    assert len(types_after) - len(types_before) == 2
+
+
 def test_output_packet_and_object_pose_propagation():
     packets, gt = stream.generate(STREAMS["basic"])
     m = backend.RGBDBackendModule(full_batch_frame=len(packets), optimize=False)
