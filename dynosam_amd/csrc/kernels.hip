@@ -1934,7 +1934,7 @@ __global__ __launch_bounds__(256) void k_scatter_chunks(const char* __restrict__
                                                         const CopyChunk* __restrict__ chunks) {
   const CopyChunk c = chunks[blockIdx.x];
   char* dst = reinterpret_cast<char*>(c.dst);
-  const char* src = data + c.src_off;
+  const char* src = data + (static_cast<size_t>(c.src_off) << 8);
   const uint32_t n16 = c.bytes / 16;
   for (uint32_t i = threadIdx.x; i < n16; i += blockDim.x)
     reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];

@@ -147,7 +147,7 @@ void launch_gather_reduced(const GatherDev& band, const int32_t* tA, const int32
 // arrays.
 struct CopyChunk {
   uint64_t dst;      // device address
-  uint32_t src_off;  // from the staged data's start
+  uint32_t src_off;  // from the staged data's start, in 256-byte units
   uint32_t bytes;
 };
 void launch_scatter_chunks(const char* data, const CopyChunk* chunks, int n_chunks, hipStream_t s);

@@ -9,6 +9,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <cstdlib>
+#include <exception>
 #include <functional>
 #include <mutex>
 #include <thread>
@@ -22,7 +23,9 @@ namespace dynohip {
 // to back, so an idle worker spins on the section counter for a while before
 // it blocks on the condition variable (waking a blocked thread costs tens of
 // microseconds per section), and the caller spins until its helpers are
-// done. Never destroyed: the threads block until the process exits.
+// done. An exception in a body (any worker's) reaches the caller of run()
+// after every helper has finished. Never destroyed: the threads block until
+// the process exits.
 class PlanPool {
  public:
   static PlanPool& get() {
@@ -57,9 +60,24 @@ class PlanPool {
                  std::memory_order_release);
     }
     if (sleepers_.load(std::memory_order_acquire) > 0) cv_.notify_all();
-    body(0);
+    // the helpers call through fn_, which lives in this frame: wait for them
+    // however body(0) ends, then rethrow the first exception of any worker
+    std::exception_ptr mine;
+    try {
+      body(0);
+    } catch (...) {
+      mine = std::current_exception();
+    }
     while (pending_.load(std::memory_order_acquire) != 0) pause();
     fn_ = nullptr;
+    std::exception_ptr theirs;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      theirs = err_;
+      err_ = nullptr;
+    }
+    if (mine) std::rethrow_exception(mine);
+    if (theirs) std::rethrow_exception(theirs);
   }
 
  private:
@@ -99,7 +117,12 @@ class PlanPool {
       }
       seen = g;
       if (r >= static_cast<int>(g & 255)) continue;
-      (*fn_)(r);
+      try {
+        (*fn_)(r);
+      } catch (...) {   // handed to the caller of run(); the worker lives on
+        std::lock_guard<std::mutex> lk(mu_);
+        if (!err_) err_ = std::current_exception();
+      }
       pending_.fetch_sub(1, std::memory_order_acq_rel);
     }
   }
@@ -107,6 +130,7 @@ class PlanPool {
   std::mutex call_mu_, mu_;
   std::condition_variable cv_;
   std::function<void(int)>* fn_ = nullptr;
+  std::exception_ptr err_;   // first exception of a helper in the current section
   std::atomic<int> pending_{0}, sleepers_{0};
   std::atomic<uint64_t> gen_{0};
 };

@@ -19,6 +19,9 @@
 // them differently moved whole Jacobian rows by ~1e-5.
 #pragma clang fp contract(off)
 
+// sin, tan and acos shared with the CPU oracle (identical rounding)
+#include "trig.h"
+
 namespace dynohip {
 
 #define DH_HD __host__ __device__ __forceinline__
@@ -109,8 +112,8 @@ DH_HD void rot_expmap(const double* w, double* R) {
 #pragma unroll
   for (int i = 0; i < 9; ++i) K[i] = W[i] / theta;
   mat3_mul(K, K, KK);
-  const double s = sin(theta);
-  const double s2 = sin(theta / 2.0);
+  const double s = dht_sin(theta);
+  const double s2 = dht_sin(theta / 2.0);
   const double omc = 2.0 * s2 * s2;
 #pragma unroll
   for (int i = 0; i < 9; ++i) R[i] = s * K[i] + omc * KK[i];
@@ -149,8 +152,8 @@ DH_HD void rot_logmap(const double* R, double* w) {
   double magnitude;
   const double tr_3 = tr - 3.0;
   if (tr_3 < -1e-6) {
-    const double theta = acos((tr - 1.0) / 2.0);
-    magnitude = theta / (2.0 * sin(theta));
+    const double theta = dht_acos((tr - 1.0) / 2.0);
+    magnitude = theta / (2.0 * dht_sin(theta));
   } else {
     magnitude = 0.5 - tr_3 / 12.0 + tr_3 * tr_3 / 60.0;
   }
@@ -197,7 +200,7 @@ DH_HD void pose_logmap(const P3& T, double* xi) {
   }
   const double wn[3] = {w[0] / th, w[1] / th, w[2] / th};
   const double W[9] = {0.0, -wn[2], wn[1], wn[2], 0.0, -wn[0], -wn[1], wn[0], 0.0};
-  const double Tan = tan(0.5 * th);
+  const double Tan = dht_tan(0.5 * th);
   double WT[3], WWT[3];
   mat3_vec(W, T.t, WT);
   mat3_vec(W, WT, WWT);

@@ -36,8 +36,10 @@ namespace {
 // C2 handle), and the next allocation of a similar size takes one back: the
 // reference constructs a fresh LevenbergMarquardtOptimizer per call
 // (RGBDBackendModule.cc:207,364), and a fresh handle per call then costs no
-// device allocation at all after the first. Held bytes are capped
-// (DYNOHIP_POOL_MAX_MB, default 16384); dynohip_pool_trim() frees them.
+// device allocation at all after the first. Held bytes are capped at
+// DYNOHIP_POOL_MAX_MB (default 16384) and a quarter of the device's memory;
+// dynohip_pool_trim() frees them, and an allocation that fails for lack of
+// memory frees its device's cached blocks and tries again.
 class DevPool {
  public:
   static DevPool& get() {
@@ -66,9 +68,12 @@ class DevPool {
   }
   void give(int dev, void* p, size_t bytes) {
     if (!p) return;
+    size_t total = 0;   // the cache keeps at most a quarter of the device's memory
+    if (hipDeviceTotalMem(&total, dev) != hipSuccess) total = 0;
+    const size_t limit = total ? std::min(max_bytes_, total / 4) : max_bytes_;
     {
       std::lock_guard<std::mutex> lk(mu_);
-      if (held_ + bytes <= max_bytes_) {
+      if (held_ + bytes <= limit) {
         free_.push_back({p, bytes, dev});
         held_ += bytes;
         return;
@@ -76,12 +81,25 @@ class DevPool {
     }
     (void)hipFree(p);
   }
-  size_t trim() {
+  // frees the cached blocks of `dev` (all devices for dev < 0)
+  size_t trim(int dev = -1) {
     std::vector<Blk> all;
     {
       std::lock_guard<std::mutex> lk(mu_);
-      all.swap(free_);
-      held_ = 0;
+      if (dev < 0) {
+        all.swap(free_);
+        held_ = 0;
+      } else {
+        for (size_t i = 0; i < free_.size();)
+          if (free_[i].dev == dev) {
+            all.push_back(free_[i]);
+            held_ -= free_[i].bytes;
+            free_[i] = free_.back();
+            free_.pop_back();
+          } else {
+            ++i;
+          }
+      }
     }
     size_t n = 0;
     int cur = 0;
@@ -134,6 +152,12 @@ struct DevBuf {
     std::swap(cap, o.cap);
     std::swap(dev, o.dev);
   }
+  // The block goes to the pool, where another handle (another thread, another
+  // stream) may take it at once: it is released only while the owning
+  // handle's stream is idle. Every path that can grow a buffer runs after a
+  // stream synchronisation (dynohip_set_values before re-planning,
+  // dynohip_values_snapshot, dynohip_destroy), and no buffer is grown twice
+  // between two synchronisations.
   void release() {
     if (p) DevPool::get().give(dev, p, cap * sizeof(T));
     p = nullptr;
@@ -154,7 +178,18 @@ struct DevBuf {
       cap = got / sizeof(T);
       return hipSuccess;
     }
-    const hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), c * sizeof(T));
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), c * sizeof(T));
+    if (e == hipErrorOutOfMemory) {
+      // blocks too small for this request may sit in the cache: give this
+      // device's back and try once more (without the headroom)
+      (void)hipGetLastError();
+      DevPool::get().trim(dev);
+      e = hipMalloc(reinterpret_cast<void**>(&p), count * sizeof(T));
+      if (e == hipSuccess) {
+        n = cap = count;
+        return hipSuccess;
+      }
+    }
     if (e != hipSuccess) {
       p = nullptr;
       return e;
@@ -241,10 +276,13 @@ struct Uploads {
     std::vector<CopyChunk> ch;
     for (const Item& it : items)
       for (size_t o = 0; o < it.bytes; o += kChunk)
-        ch.push_back({reinterpret_cast<uint64_t>(static_cast<char*>(it.dev) + o), static_cast<uint32_t>(it.off + o),
+        ch.push_back({reinterpret_cast<uint64_t>(static_cast<char*>(it.dev) + o), static_cast<uint32_t>((it.off + o) >> 8),
                       static_cast<uint32_t>(std::min(kChunk, it.bytes - o))});
     const size_t tb = (ch.size() * sizeof(CopyChunk) + 255) & ~size_t{255};
     const size_t all = tb + total;
+    // chunk offsets are 256-byte units in 32 bits (items start 256-aligned,
+    // chunks 64 KiB into them): staged plans up to 1 TiB
+    if (total >= (size_t{1} << 40)) return hipErrorInvalidValue;
     if (all > cap) {
       if (buf) (void)hipHostFree(buf);
       buf = nullptr;
@@ -1220,14 +1258,18 @@ struct EarlyUpload : PlanHook {
   void types_ready(const Plan& P) override {
     th = std::thread([this, &P] {
       (void)hipSetDevice(s->device);
-      Uploads up;
-      for (int t = 0; t < kNTypes && err == hipSuccess; ++t) {
-        const TypePlan& tp = P.types[t];
-        if ((err = up.add(s->tb[t].idx, tp.idx)) != hipSuccess || (err = up.add(s->tb[t].meas, tp.meas)) != hipSuccess ||
-            (err = up.add(s->tb[t].isig, tp.isig)) != hipSuccess || (err = up.add(s->tb[t].hk, tp.hk)) != hipSuccess)
-          break;
+      try {
+        Uploads up;
+        for (int t = 0; t < kNTypes && err == hipSuccess; ++t) {
+          const TypePlan& tp = P.types[t];
+          if ((err = up.add(s->tb[t].idx, tp.idx)) != hipSuccess || (err = up.add(s->tb[t].meas, tp.meas)) != hipSuccess ||
+              (err = up.add(s->tb[t].isig, tp.isig)) != hipSuccess || (err = up.add(s->tb[t].hk, tp.hk)) != hipSuccess)
+            break;
+        }
+        if (err == hipSuccess) err = up.run(s->stage[0], s->stage_cap[0], s->dstage[0], s->stream, false);
+      } catch (const std::exception&) {   // host allocation
+        err = hipErrorOutOfMemory;
       }
-      if (err == hipSuccess) err = up.run(s->stage[0], s->stage_cap[0], s->dstage[0], s->stream, false);
       done = err == hipSuccess;
     });
   }
@@ -1249,12 +1291,23 @@ int dynohip_set_values(dynohip_solver* s, const uint64_t* keys, const uint8_t* k
                     std::equal(s->value_keys.begin(), s->value_keys.end(), keys);
   if (!same) {
     const auto tb0 = std::chrono::steady_clock::now();
+    // re-planning may grow device buffers, whose old blocks then go to the
+    // process-wide pool: nothing of this handle may still run on them (the
+    // speculative linearisation of the last try does)
+    HIPCHK(s, hipStreamSynchronize(s->stream));
     s->has_plan = false;
     dynohip_graph_view g = s->graph.view();
     EarlyUpload early(s);
-    int rc = s->nranks > 1 ? build_partitioned_plan(g, keys, kind, n, s->nranks, s->rank, s->plan, s->part,
-                                                    s->local_graph, s->err)
-                           : build_plan(g, keys, kind, n, s->plan, s->err, 1, 0, true, false, &early);
+    int rc;
+    try {   // nothing thrown crosses the C-ABI (host allocation failures, a planner worker's exception)
+      rc = s->nranks > 1 ? build_partitioned_plan(g, keys, kind, n, s->nranks, s->rank, s->plan, s->part,
+                                                  s->local_graph, s->err)
+                         : build_plan(g, keys, kind, n, s->plan, s->err, 1, 0, true, false, &early);
+    } catch (const std::exception& ex) {
+      early.join();
+      if (early.done) (void)hipStreamSynchronize(s->stream);
+      return set_err(s, DYNOHIP_EINVAL, "planner: %s", ex.what());
+    }
     early.join();
     if (rc) {
       if (early.done) (void)hipStreamSynchronize(s->stream);   // its staging buffer is reused next time
@@ -1509,7 +1562,9 @@ int dynohip_values_snapshot(dynohip_solver* s) {
   if (rc) return rc;
   (void)hipSetDevice(s->device);
   const Plan& P = s->plan;
-  // sized for the current plan (a re-planned handle may hold a larger graph)
+  // sized for the current plan (a re-planned handle may hold a larger graph);
+  // a grown buffer's old block goes to the pool with the stream idle
+  HIPCHK(s, hipStreamSynchronize(s->stream));
   if (P.n_pose) HIPCHK(s, s->pose_snap.alloc(12ull * P.n_pose));
   if (P.n_pt) HIPCHK(s, s->pt_snap.alloc(3ull * P.n_pt));
   if (P.n_pose) HIPCHK(s, hipMemcpyAsync(s->pose_snap.p, s->pose.p, 12ull * P.n_pose * sizeof(double), hipMemcpyDeviceToDevice, s->stream));

@@ -41,12 +41,13 @@ class TorchAllReduce:
     that read the result, with no host synchronisation; with gloo the stream
     is synchronised and the buffer staged through host memory."""
 
-    def __init__(self, device, group=None):
+    def __init__(self, device, group=None, op=None):
         import torch
         import torch.distributed as dist
 
         self.torch, self.dist = torch, dist
         self.group = group
+        self.op = dist.ReduceOp.SUM if op is None else op   # tests: a PREMUL_SUM makes the ordering visible
         self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
         self.backend = dist.get_backend(group)
         self.on_gpu = self.backend == "nccl"
@@ -65,7 +66,7 @@ class TorchAllReduce:
                 ext = torch.cuda.ExternalStream(int(stream or 0), device=self.device)
                 if self.on_gpu:
                     with torch.cuda.stream(ext):   # stream-ordered, returns before completion
-                        dist.all_reduce(t, group=self.group)
+                        dist.all_reduce(t, op=self.op, group=self.group)
                 else:
                     ext.synchronize()
                     h = t.cpu()

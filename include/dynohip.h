@@ -41,7 +41,13 @@ extern "C" {
       its trailing `ternary_inactive` pointer (dynorefine.h is covered by
       this version: a consumer built against an older header must not call
       dynorefine_upload).
-   3: dynohip_solve_delta. */
+   3: dynohip_solve_delta; dynohip_allreduce_fn gained its fifth argument
+      `stream`, and its ordering contract changed: for on_device = 1 the
+      buffer may still be unwritten when the callback is called (the
+      solver no longer synchronises its stream first), so the reduction
+      must be enqueued on that stream, or the callback must synchronise it
+      before reading. A v2 callback that stages through host memory without
+      that synchronisation reads stale separator data. */
 #define DYNOHIP_ABI_VERSION 3
 
 typedef enum {

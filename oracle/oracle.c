@@ -22,6 +22,11 @@
 #include <stdlib.h>
 #include <string.h>
 
+/* the shared transcendental functions (sin, tan, acos) of the pose
+   arithmetic: the same IEEE operations as the kernels (se3.hpp), in place
+   of glibc's, see trig.h */
+#include "../dynosam_amd/csrc/trig.h"
+
 #ifndef M_PI
 #define M_PI 3.14159265358979323846
 #endif
@@ -81,8 +86,8 @@ void oracle_rot_expmap(const double w[3], double R[9]) {
   double K[9], KK[9];
   for (int i = 0; i < 9; ++i) K[i] = W[i] / theta;
   m3_mul(K, K, KK);
-  const double s = sin(theta);
-  const double s2 = sin(theta / 2.0);
+  const double s = dht_sin(theta);
+  const double s2 = dht_sin(theta / 2.0);
   const double omc = 2.0 * s2 * s2;
   for (int i = 0; i < 9; ++i) R[i] = s * K[i] + omc * KK[i];
   R[0] += 1.0; R[4] += 1.0; R[8] += 1.0;
@@ -125,8 +130,8 @@ void oracle_rot_logmap(const double R[9], double w[3]) {
   double magnitude;
   const double tr_3 = tr - 3.0;
   if (tr_3 < -1e-6) {
-    const double theta = acos((tr - 1.0) / 2.0);
-    magnitude = theta / (2.0 * sin(theta));
+    const double theta = dht_acos((tr - 1.0) / 2.0);
+    magnitude = theta / (2.0 * dht_sin(theta));
   } else {
     magnitude = 0.5 - tr_3 / 12.0 + tr_3 * tr_3 / 60.0;
   }
@@ -168,11 +173,17 @@ void oracle_pose_logmap(const double T[12], double xi[6]) {
   double wn[3] = {w[0] / th, w[1] / th, w[2] / th};
   double W[9], WT[3], WWT[3];
   skew(wn, W);
-  const double Tan = tan(0.5 * th);
+  const double Tan = dht_tan(0.5 * th);
   m3_mv(W, t, WT);
   m3_mv(W, WT, WWT);
   const double c = 1 - th / (2. * Tan);
   for (int i = 0; i < 3; ++i) xi[3 + i] = t[i] - (0.5 * th) * WT[i] + c * WWT[i];
+}
+
+/* trig.h evaluated on n arguments: which 0 sin, 1 tan, 2 acos */
+void oracle_trig(int which, const double* x, double* y, size_t n) {
+  for (size_t i = 0; i < n; ++i)
+    y[i] = which == 0 ? dht_sin(x[i]) : which == 1 ? dht_tan(x[i]) : dht_acos(x[i]);
 }
 
 void oracle_pose_compose(const double A[12], const double B[12], double C[12]) {

@@ -87,6 +87,8 @@ void oracle_pose_compose(const double A[12], const double B[12], double C[12]);
 void oracle_pose_inverse(const double A[12], double C[12]);
 void oracle_rot_expmap(const double w[3], double R[9]);
 void oracle_rot_logmap(const double R[9], double w[3]);
+/* the shared sin / tan / acos of trig.h: which 0, 1, 2 */
+void oracle_trig(int which, const double* x, double* y, size_t n);
 
 /* keys */
 uint64_t oracle_cantor_pair(uint64_t k1, uint64_t k2);

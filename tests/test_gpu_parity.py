@@ -21,8 +21,6 @@ from graphs_extra import mixed_lone_graph
 pytestmark = pytest.mark.gpu
 
 PER_ITER_TOL = 1e-6
-DEEP_LAMBDA = 1e-16   # below: deep convergence, see test_per_iteration_parity_conditioned
-DEEP_TOL = 2e-6
 
 
 def cores():
@@ -86,13 +84,18 @@ def test_linearize_and_error_match_oracle(gpu_available, name, kw):
     assert lg.shape == lo.shape
     scale = np.max(np.abs(lo))
     assert np.max(np.abs(lg - lo)) <= 1e-12 * scale * (1e3 if kw.get("formulation") else 1.0)
-    # PoseToPoint and LandmarkMotionTernary (no transcendental functions):
-    # the same expressions rounded the same way (no FMA contraction on
-    # either side), so their whitened, Huber-reweighted rows are
+    # every factor type evaluates the same expressions rounded the same way
+    # (no FMA contraction on either side; sin / tan / acos of the Pose3
+    # Expmap and Logmap from the one shared trig.h): the whitened,
+    # Huber-reweighted rows, the Between / Prior rows included, are
     # bit-identical to the oracle's
     n_pp, n_tern = g.count("pose_to_point"), g.count("landmark_motion_ternary")
     n0 = n_pp * 3 * 10 + n_tern * 3 * 13
+    bad = np.flatnonzero(lg != lo)
+    print(name, kw, f"rows {lg.size} differing {bad.size}", f"first at {bad[0]} of PP+ternary {n0}" if bad.size else "")
     assert np.array_equal(lg[:n0], lo[:n0])
+    if not kw.get("formulation"):
+        assert bad.size == 0
 
 
 @pytest.mark.parametrize("name,kw,iters", [("T1", {}, 7), ("T2", {}, 10), ("C1", {}, 10), ("C2", {}, 15),
@@ -101,15 +104,10 @@ def test_per_iteration_parity_conditioned(gpu_available, name, kw, iters):
     """Conditioned per LM iteration (the oracle is put on the GPU's values
     before each; lambda agrees because the tries do), at the north-star 1e-6
     relative Frobenius; C2 (configs[1]) over all 15 LM iterations of its
-    free run. Deep convergence (lambda < 1e-16, C2 iterations 12-14): the
-    undamped step runs along the least-determined directions, where the
-    ulp-level difference between the GPU's and libm's trigonometry in the
-    Between/Prior Pose3 logmap (1 - theta / (2 tan(theta / 2)) cancels for
-    small rotations, acos near 1) moves the step by a few percent and the
-    values by up to ~1.0e-6; there the bar is DEEP_TOL = 2e-6. Each side's
-    linear solve has a backward error of ~4e-21 against its own
-    linearisation, and the PoseToPoint / ternary rows are bit-identical
-    (DESIGN.md §5)."""
+    free run, deep convergence (lambda down to 1e-19) included. The
+    linearisations are bit-identical (test_linearize_and_error_match_oracle;
+    the Pose3 logmap's sin / tan / acos come from the shared trig.h), so
+    what differs is the linear solve's summation order."""
     g, v, _, s = make(name, **kw)
     o = Oracle(g, v, threads=cores())
     s.reset()
@@ -126,10 +124,10 @@ def test_per_iteration_parity_conditioned(gpu_available, name, kw, iters):
         lam = s.trace()[-1]["lam"]
         vr = rel(s.values_data(), o.values_data())
         print(name, it, f"lambda {lam:.0e} values rel {vr:.2e}")
-        assert vr < (PER_ITER_TOL if lam >= DEEP_LAMBDA else DEEP_TOL), it
+        assert vr < PER_ITER_TOL, it
         # robust=0: sigma 1e-5 Gaussian ternaries weigh value differences by
         # 1e10 (a 1e-10 value difference moves the cost by 1e-5 relative)
-        assert sg.final_error == pytest.approx(so.final_error, rel=3e-5 if kw.get("robust") == 0 else 1e-6)
+        assert sg.final_error == pytest.approx(so.final_error, rel=1e-5 if kw.get("robust") == 0 else 1e-6)
 
 
 @pytest.mark.parametrize("name", ["T2", "C1", "C2"])
@@ -149,7 +147,7 @@ def test_solve_delta_matches_oracle(gpu_available, name):
     assert np.array_equal(s.values_data(), v.data)
 
 
-@pytest.mark.parametrize("name,iters", [("NS", 3), ("C5", 2)])
+@pytest.mark.parametrize("name,iters", [("NS", 17), ("C5", 6)])
 def test_conditioned_vs_oracle_at_scale(gpu_available, name, iters):
     """The north-star graph (NS: 500 frames, 5 objects, 100k landmarks) and
     configs[4] (C5: 2000 frames, 20 objects, 500k landmarks) on ONE handle
@@ -179,6 +177,31 @@ def test_conditioned_vs_oracle_at_scale(gpu_available, name, iters):
         assert vr < PER_ITER_TOL, it
         assert sg.final_error == pytest.approx(so.final_error, rel=1e-6), it
         lam = sg.final_lambda
+
+
+def test_free_running_ns_vs_oracle(gpu_available):
+    """The north-star graph (500 frames, 5 objects, 100k landmarks) solved
+    free-running by both sides, RGBDBackendModule.cc:207-231's whole LM:
+    the same iterations and inner iterations, the same accept / lambda
+    sequence, errors and final values within 1e-6."""
+    g, v, _, s = make("NS")
+    sg = s.optimize()
+    o = Oracle(g, v, threads=cores())
+    so = o.optimize()
+    tg, to = s.trace(), o.trace()
+    vr = rel(s.values_data(), o.values_data())
+    print("NS free run", (sg.iterations, sg.inner_iterations), (so.iterations, so.inner_iterations),
+          f"values rel {vr:.2e}", f"error {sg.final_error:.12e} {so.final_error:.12e}")
+    for a, b in zip(tg, to):
+        print(f"  lam {a['lam']:.0e} {b['lam']:.0e} accepted {a['accepted']} {b['accepted']}"
+              f" new {a['new_error']:.12e} {b['new_error']:.12e}")
+    assert (sg.iterations, sg.inner_iterations) == (so.iterations, so.inner_iterations)
+    assert [(e["accepted"], e["lam"]) for e in tg] == [(e["accepted"], e["lam"]) for e in to]
+    for a, b in zip(tg, to):
+        if a["accepted"]:
+            assert a["new_error"] == pytest.approx(b["new_error"], rel=1e-6)
+    assert sg.final_error == pytest.approx(so.final_error, rel=1e-6)
+    assert vr < PER_ITER_TOL
 
 
 @pytest.mark.parametrize("name,kw", [("T1", {}), ("T2", {}), ("C1", {}), ("T2", {"noise_code_defaults": 1})])
@@ -487,6 +510,49 @@ def test_replan_on_reused_handles(gpu_available):
         h.optimize()
         assert np.array_equal(h.values_data(), ref[k]), k
         h.close()
+
+
+def test_replan_two_threads_two_handles(gpu_available):
+    """Two handles on two threads (two streams) re-plan back and forth
+    between graphs of different sizes while the other solves: blocks that a
+    growing buffer gives back to the process-wide device pool are taken by
+    the other handle at once. A block is released only with its handle's
+    stream idle (dynohip_set_values synchronises before re-planning), so
+    every solve equals a lone solve bit for bit."""
+    import threading
+    graphs = [synth.generate(n, seed=sd)[:2] for n, sd in (("T2", 51), ("C1", 52), ("T2", 53), ("C1", 54))]
+    ref = []
+    for g, v in graphs:
+        h = Solver(0)
+        h.set_graph(g)
+        h.set_values(v)
+        h.optimize()
+        ref.append(h.values_data())
+        h.close()
+    from dynosam_amd import _native
+    _native.load("libdynohip.so").dynohip_pool_trim()
+    errors = []
+
+    def worker(order):
+        try:
+            s = Solver(0)
+            for k in order:
+                g, v = graphs[k]
+                s.set_graph(g)
+                s.set_values(v)
+                s.optimize()
+                if not np.array_equal(s.values_data(), ref[k]):
+                    errors.append((order, k))
+            s.close()
+        except Exception as e:   # noqa: BLE001 - reported below
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(o,)) for o in ([0, 1, 2, 3, 0, 1], [3, 2, 1, 0, 3, 2])]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors
 
 
 def test_full_size_c2_properties(gpu_available):

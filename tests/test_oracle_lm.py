@@ -94,10 +94,16 @@ def test_golden_regression(name):
     g, v, _ = synth.generate(name)
     o = Oracle(g, v)
     s = o.optimize()
+    # the fixtures were written while the oracle's Pose3 Expmap / Logmap
+    # called glibc's sin / tan / acos, as GTSAM does; it now calls the
+    # shared trig.h (within 0.7 / 1.8 / 1 ulp of mpmath, tests/test_trig.py).
+    # That ulp-level change moves the converged T1 / T2 solutions by
+    # 3.4e-9 / 5.3e-10 relative (final error 7.4e-9 / 9.1e-10): the size of
+    # the difference between the glibc-based GTSAM and this restatement.
     assert s.iterations == gold["iterations"] and s.inner_iterations == gold["inner_iterations"]
-    assert s.final_error == pytest.approx(gold["final_error"], rel=1e-9)
+    assert s.final_error == pytest.approx(gold["final_error"], rel=5e-8)
     ref = np.array(gold["final_values"])
-    assert np.linalg.norm(o.values_data() - ref) / np.linalg.norm(ref) < 1e-9
+    assert np.linalg.norm(o.values_data() - ref) / np.linalg.norm(ref) < 5e-8
 
 
 def test_indefinite_system_fails_step():

@@ -296,6 +296,33 @@ def test_allreduce_callback_gloo(tmp_path):
         assert row[9] == 1 and row[10] == 8
 
 
+@pytest.mark.gpu
+def test_rccl_device_branch_stream_ordered():
+    """TorchAllReduce's RCCL branch (backend "nccl", world size 1, set up in a
+    fresh process before any GPU call; tools/rccl_stream_check.py): the
+    device buffer is passed while the kernel writing it is still running on
+    the stream, as the partitioned solver passes its separator system; the
+    reduction (a pre-multiplied sum, factor 2, so that the order shows in
+    the values) is enqueued behind that kernel and ahead of the stream's next
+    one, and the callback returns before the stream has finished."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "rccl_stream_check.py")], cwd=root,
+                       capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    print(res)
+    assert res["backend"] == "nccl" and res["world_size"] == 1
+    assert res["rc"] == 0 and res["calls"] == 1 and res["doubles"] == 1 << 20
+    assert res["returned_before_done"]
+    assert res["exact"], res["max_err"]
+    assert res["host_rc"] == 0 and res["host_ok"]
+
+
 def _run_partition_check(tmp_path, config, nranks, extra=(), timeout=240):
     import json
     import os
