@@ -449,7 +449,7 @@ def main():
     # Phase A: Jacobian assembly = linearisation + point-side
     # blocks, priced against B_A (the algorithmic bytes), per linearisation
     lin_ms = st["ms_linearize"] / nlin
-    lin_kernels = [k for k in pmc if k.startswith("k_linearize") or k == "k_gather_point"]
+    lin_kernels = [k for k in pmc if k.startswith("k_linearize") or k in ("k_gather_point", "k_lone_lin")]
     lin_traffic = sum(pk(k, "traffic_bytes_per_launch") or 0.0 for k in lin_kernels) if lin_kernels else None
     phase_a = {"bound": "hbm", "achieved": st["lin_bytes"] / (lin_ms * 1e-3) / 1e9 if lin_ms > 0 else 0.0,
                "peak": HBM_PEAK_GBS, "unit": "GB/s", "ms_per_launch": lin_ms,

@@ -287,15 +287,21 @@ __device__ __forceinline__ void factor_vars(const TypeDev& tp, int i, const doub
 // reweight by sqrt(w(||b||)) (RGBDBackendModule.cc:97-113). Returns the
 // factor's linear error at delta = 0, 0.5 ||b||^2, summed exactly as
 // linerr_one sums it (0 - b is exact), so the fused value is bit-identical.
+// The whitened, reweighted Jacobian Jw (d x cols, row-major, the factor's
+// column order) and right-hand side bw of factor i, and its linear error at
+// delta = 0. k_linearize stores them as the factor's record; k_lone_lin
+// (the fused static landmarks) consumes them in registers. Both get the same
+// bits.
 template <int T>
-__device__ __forceinline__ double linearize_one(const TypeDev& tp, int i, const double* __restrict__ pose,
-                                                const double* __restrict__ pt, double* __restrict__ arena) {
-  constexpr int d = kDim[T], cols = kCols[T], nk = kNKeys[T];
+__device__ __forceinline__ double eval_whitened(const TypeDev& tp, int i, const double* __restrict__ pose,
+                                                const double* __restrict__ pt, double (&Jw)[kDim[T] * kCols[T]],
+                                                double (&bw)[kDim[T]]) {
+  constexpr int d = kDim[T], cols = kCols[T];
   const double* v[4];
   factor_vars<T>(tp, i, pose, pt, v);
   const double* meas = kMeasDim[T] ? tp.meas + static_cast<int64_t>(i) * kMeasDim[T] : nullptr;
-  double r[6], J[d * cols];
-  evaluate<T>(v, meas, r, J);
+  double r[6];
+  evaluate<T>(v, meas, r, Jw);
   double isig[6], b[6], n2 = 0.0;
 #pragma unroll
   for (int k = 0; k < d; ++k) {
@@ -310,6 +316,33 @@ __device__ __forceinline__ double linearize_one(const TypeDev& tp, int i, const 
     const double w = e <= hk ? 1.0 : hk / e;
     sw = sqrt(w);
   }
+#pragma unroll
+  for (int k = 0; k < d; ++k) {
+    const double sc = isig[k];
+#pragma unroll
+    for (int c = 0; c < cols; ++c) {
+      double a = Jw[k * cols + c] * sc;
+      if (hk > 0.0) a *= sw;
+      Jw[k * cols + c] = a;
+    }
+  }
+  double e = 0.0;
+#pragma unroll
+  for (int k = 0; k < d; ++k) {
+    const double bk = hk > 0.0 ? b[k] * sw : b[k];
+    bw[k] = bk;
+    const double rk = 0.0 - bk;
+    e += rk * rk;
+  }
+  return e * 0.5;
+}
+
+template <int T>
+__device__ __forceinline__ double linearize_one(const TypeDev& tp, int i, const double* __restrict__ pose,
+                                                const double* __restrict__ pt, double* __restrict__ arena) {
+  constexpr int d = kDim[T], cols = kCols[T], nk = kNKeys[T];
+  double J[d * cols], b[d];
+  const double e = eval_whitened<T>(tp, i, pose, pt, J, b);
   double* rec = arena + tp.base + static_cast<uint64_t>(tp.stride) * i;
 #pragma unroll
   for (int s = 0; s < nk; ++s) {
@@ -317,25 +350,13 @@ __device__ __forceinline__ double linearize_one(const TypeDev& tp, int i, const 
     const int c0 = kColStart[T][s];
     double* blk = rec + d * c0;
 #pragma unroll
-    for (int k = 0; k < d; ++k) {
-      const double sc = isig[k];
+    for (int k = 0; k < d; ++k)
 #pragma unroll
-      for (int c = 0; c < ds; ++c) {
-        double a = J[k * cols + c0 + c] * sc;
-        if (hk > 0.0) a *= sw;
-        blk[k * ds + c] = a;
-      }
-    }
+      for (int c = 0; c < ds; ++c) blk[k * ds + c] = J[k * cols + c0 + c];
   }
-  double e = 0.0;
 #pragma unroll
-  for (int k = 0; k < d; ++k) {
-    const double bk = hk > 0.0 ? b[k] * sw : b[k];
-    rec[d * cols + k] = bk;
-    const double rk = 0.0 - bk;
-    e += rk * rk;
-  }
-  return e * 0.5;
+  for (int k = 0; k < d; ++k) rec[d * cols + k] = b[k];
+  return e;
 }
 
 // NoiseModelFactor::error: Gaussian 0.5 d^2, Robust Huber rho(sqrt(d^2))
@@ -453,7 +474,8 @@ __device__ __forceinline__ double group_apply(const GroupDev& g, int b, F&& f) {
     if constexpr (((M >> T) & 1u) != 0u) {
       if (b < g.bstart[T + 1]) {
         const int i = (b - g.bstart[T]) * kBlock + static_cast<int>(threadIdx.x);
-        return i < g.t[T].n ? f(std::integral_constant<int, T>{}, i) : 0.0;
+        if (i >= g.t[T].n) return 0.0;
+        return f(std::integral_constant<int, T>{}, g.t[T].list ? g.t[T].list[i] : i);
       }
     }
     return group_apply<M, T + 1>(g, b, f);
@@ -736,6 +758,121 @@ __device__ __forceinline__ void lone_point_block(const PointGatherDev& pg, int g
     double* G = pg.dst[2] + 3ll * pt;
 #pragma unroll
     for (int k = 0; k < 3; ++k) G[k] = gs[k];
+  }
+}
+
+// ---- fused static landmarks: k_lone_lin ------------------------------------
+// The grouped static landmarks' PoseToPoint factors (the bulk of every graph:
+// 385k of the 430k PoseToPoint factors at NS) are linearised where their
+// blocks are formed, with no J | b record in HBM. A workgroup per group block,
+// a lane per (point, neighbour a) as lone_point_block: the lane evaluates its
+// factor (eval_whitened, the records' bits), writes W_a = J_p^T J_x and sums
+// D and g_p over the point's lanes by the same shuffles; it stages J_x | b in
+// LDS, from which a thread per (a, entry) sums the block's J_a^T J_a and
+// J_a^T b over the points in point order (the order, and so the bits, of
+// k_lone_schur's former sums over the records) into the group's H area. The
+// lane's 0.5 ||b||^2 goes to the block's partial of the linear error at
+// delta = 0 (summed with k_linearize's partials).
+// H area (plan.hpp): after the per-try partial blocks at `out`, [a] 6x6 full
+// (symmetric) J_a^T J_a, then [a] J_a^T b.
+__host__ __device__ constexpr uint32_t lone_h_off(int m) { return 36u * static_cast<uint32_t>(m * (m + 1) / 2) + 6u * m; }
+constexpr int kRec0 = kDim[0] * kCols[0] + kDim[0];   // PoseToPoint record stride (plan.cpp)
+constexpr int kLoneJ = 21;                            // staged per (point, a): J_x (3x6) | b (3)
+
+__global__ __launch_bounds__(kBlock) void k_lone_lin(LoneLinDev d, const double* __restrict__ pose,
+                                                     const double* __restrict__ pt, double* __restrict__ arena,
+                                                     double* __restrict__ partials) {
+  __shared__ int32_t hdr[kLoneBlk];
+  __shared__ double sJ[kLoneSub * kLoneMaxNb * kLoneJ];
+  const int tid = threadIdx.x;
+  for (int q = tid; q < kLoneBlk; q += kBlock) hdr[q] = d.blk[static_cast<int64_t>(blockIdx.x) * kLoneBlk + q];
+  __syncthreads();
+  const int m = hdr[0], npt = hdr[1];
+  const int lane = tid & 63, per = 64 / m, uu = lane / m, a = lane - uu * m;
+  const int u = (tid >> 6) * per + uu;
+  const bool valid = uu < per && u < npt;
+  double Dp[9], gp[3], e = 0.0;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) Dp[k] = 0.0;
+  gp[0] = gp[1] = gp[2] = 0.0;
+  if (valid) {
+    const uint32_t rec = static_cast<uint32_t>(hdr[4 + 2 * kLoneSub + m * u + a]);
+    const int f = static_cast<int>((rec - d.t0.base) / kRec0);
+    double J[kDim[0] * kCols[0]], bb[3];
+    e = eval_whitened<0>(d.t0, f, pose, pt, J, bb);
+    // the record's blocks: J_x (3x6) and J_p (3x3), row-major
+    double Jx[18], Jp[9];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+#pragma unroll
+      for (int c = 0; c < 6; ++c) Jx[6 * k + c] = J[kCols[0] * k + c];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) Jp[3 * k + c] = J[kCols[0] * k + 6 + c];
+    }
+    double* W = arena + d.off_W + 18ll * (hdr[4 + kLoneSub + u] + a);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+#pragma unroll
+      for (int c = 0; c < 6; ++c) W[6 * k + c] = Jp[k] * Jx[c] + Jp[3 + k] * Jx[6 + c] + Jp[6 + k] * Jx[12 + c];
+#pragma unroll
+      for (int l = 0; l < 3; ++l) Dp[3 * k + l] = Jp[k] * Jp[l] + Jp[3 + k] * Jp[3 + l] + Jp[6 + k] * Jp[6 + l];
+      gp[k] = Jp[k] * bb[0] + Jp[3 + k] * bb[1] + Jp[6 + k] * bb[2];
+    }
+    double* sj = sJ + kLoneJ * (m * u + a);
+#pragma unroll
+    for (int k = 0; k < 18; ++k) sj[k] = Jx[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) sj[18 + k] = bb[k];
+  }
+  // lane a == 0 of each point sums its m lanes (lone_point_block's order)
+  double Ds[9], gs[3];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) Ds[k] = 0.0;
+  gs[0] = gs[1] = gs[2] = 0.0;
+  for (int j = 0; j < m; ++j) {
+    const int src = min(lane + j, 63);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) Ds[k] += __shfl(Dp[k], src);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) gs[k] += __shfl(gp[k], src);
+  }
+  if (valid && a == 0) {
+    const int p = hdr[4 + u];
+    double* D = arena + d.off_D + 9ll * p;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) D[k] = Ds[k];
+    double* G = arena + d.off_gp + 3ll * p;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) G[k] = gs[k];
+  }
+  const double es = block_sum(e);   // (its barrier also publishes sJ)
+  if (tid == 0) partials[d.pslot + blockIdx.x] = es;
+  __syncthreads();
+  // the block's J_a^T J_a (lower entries, written to both halves) and J_a^T b
+  double* H = arena + static_cast<uint32_t>(hdr[2]) + lone_h_off(m);
+  for (int t = tid; t < 27 * m; t += kBlock) {
+    const int aa = t / 27, q = t - 27 * aa;
+    double acc = 0.0;
+    if (q < 21) {
+      int r = 0;
+      while ((r + 1) * (r + 2) / 2 <= q) ++r;
+      const int c = q - r * (r + 1) / 2;
+      for (int p = 0; p < npt; ++p) {
+        const double* sj = sJ + kLoneJ * (m * p + aa);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) acc += sj[6 * k + r] * sj[6 * k + c];
+      }
+      H[36 * aa + 6 * r + c] = acc;
+      H[36 * aa + 6 * c + r] = acc;
+    } else {
+      const int r = q - 21;
+      for (int p = 0; p < npt; ++p) {
+        const double* sj = sJ + kLoneJ * (m * p + aa);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) acc += sj[6 * k + r] * sj[18 + k];
+      }
+      H[36 * m + 6 * aa + r] = acc;
+    }
   }
 }
 
@@ -1329,6 +1466,7 @@ __global__ __launch_bounds__(kBlock) void k_chain_solve_y(ChainDev cd, double* _
 constexpr int kLoneStage = (kLoneSub * 18 * kLoneMaxNb + kBlock - 1) / kBlock;   // W (and J) loads per thread
 static_assert(kLoneSub * 3 * kLoneMaxNb <= 2 * kBlock && 9 * kLoneSub <= kBlock, "lone staging of b, L");
 __host__ __device__ constexpr int lone_point_doubles(int m) { return 39 * m + 12; }  // Z, J, b, z, L
+__host__ __device__ constexpr int lone_point_doubles_fused(int m) { return 18 * m + 12; }  // Z, z, L
 constexpr int kLoneNT = (6 * kLoneMaxNb + 15) / 16;                 // 16-column tiles of Z, at most
 constexpr int kLoneWT = (kLoneNT * (kLoneNT + 1) / 2 + 3) / 4;      // lower tiles per wave, at most
 static_assert(6 * kLoneMaxNb <= 64, "one lane per J_a^T J_a / gradient row");
@@ -1361,12 +1499,16 @@ __global__ __launch_bounds__(kBlock) void k_lone_schur(LoneSchurDev d, double* _
   const int32_t* spt = hdr + 4;
   const int32_t* se0 = hdr + 4 + kLoneSub;
   const int32_t* srec = hdr + 4 + 2 * kLoneSub;
-  double* sZ = lds;                       // [point][a][k][c]: W, then Z in place
-  double* sJ = sZ + kLoneSub * m18;       // [point][a][k][c]
-  double* sB = sJ + kLoneSub * m18;       // [point][a][k]
-  double* sz = sB + kLoneSub * 3 * m;     // [point][k]: g_p, then z in place
-  double* sL = sz + 3 * kLoneSub;         // [point][9]
+  const bool fused = d.fused != 0;
+  double* sZ = lds;                                  // [point][a][k][c]: W, then Z in place
+  double* sJ = sZ + kLoneSub * m18;                  // [point][a][k][c] (records; not fused)
+  double* sB = sJ + kLoneSub * m18;                  // [point][a][k]    (records; not fused)
+  double* sz = fused ? sJ : sB + kLoneSub * 3 * m;   // [point][k]: g_p, then z in place
+  double* sL = sz + 3 * kLoneSub;                    // [point][9]
+  __shared__ double sJJ[36 * kLoneMaxNb];            // J_a^T J_a (fused: the H area's)
+  __shared__ double sJb[6 * kLoneMaxNb];             // fused: J_a^T b
   const int nW = npt * m18, nB = npt * 3 * m;
+  const uint32_t hsrc = static_cast<uint32_t>(hdr[2]) + 36u * np + 6u * m;   // the H area (k_lone_lin)
   {
     double rw[kLoneStage], rj[kLoneStage], rb[2], rl = 0.0, rg = 0.0;
 #pragma unroll
@@ -1376,13 +1518,22 @@ __global__ __launch_bounds__(kBlock) void k_lone_schur(LoneSchurDev d, double* _
       if (q < nW) {
         const int p = q / m18, pa = q / 18;
         rw[u] = arena[d.off_W + 18ll * se0[p] + (q - p * m18)];
-        rj[u] = arena[static_cast<uint32_t>(srec[pa]) + (q - 18 * pa)];
+        if (!fused) rj[u] = arena[static_cast<uint32_t>(srec[pa]) + (q - 18 * pa)];
       }
     }
+    if (fused) {
+      // the H area, 42 m doubles, in place of the J | b records
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int q = tid + kBlock * u, pa = q / 3;
-      rb[u] = q < nB ? arena[static_cast<uint32_t>(srec[pa]) + 27 + (q - 3 * pa)] : 0.0;
+      for (int u = 0; u < 2; ++u) {
+        const int q = tid + kBlock * u;
+        rb[u] = q < 42 * m ? arena[hsrc + q] : 0.0;
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int q = tid + kBlock * u, pa = q / 3;
+        rb[u] = q < nB ? arena[static_cast<uint32_t>(srec[pa]) + 27 + (q - 3 * pa)] : 0.0;
+      }
     }
     if (tid < 9 * npt) rl = arena[d.off_L + 9ll * spt[tid / 9] + tid % 9];
     if (tid < 3 * npt) rg = arena[d.off_gp + 3ll * spt[tid / 3] + tid % 3];
@@ -1391,12 +1542,21 @@ __global__ __launch_bounds__(kBlock) void k_lone_schur(LoneSchurDev d, double* _
       const int q = tid + kBlock * u;
       if (q < nW) {
         sZ[q] = rw[u];
-        sJ[q] = rj[u];
+        if (!fused) sJ[q] = rj[u];
       }
     }
+    if (fused) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
-      if (tid + kBlock * u < nB) sB[tid + kBlock * u] = rb[u];
+      for (int u = 0; u < 2; ++u) {
+        const int q = tid + kBlock * u;
+        if (q < 36 * m) sJJ[q] = rb[u];
+        else if (q < 42 * m) sJb[q - 36 * m] = rb[u];
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        if (tid + kBlock * u < nB) sB[tid + kBlock * u] = rb[u];
+    }
     if (tid < 9 * npt) sL[tid] = rl;
     if (tid < 3 * npt) sz[tid] = rg;
   }
@@ -1424,7 +1584,6 @@ __global__ __launch_bounds__(kBlock) void k_lone_schur(LoneSchurDev d, double* _
   // waves. Beside them on VALU: wave 3 lane (a, r) sums row r of
   // J_a^T J_a, wave 2 lane (a, r) row r of gradient a (these two waves hold
   // fewer tiles). The J_a^T J_a rows meet the tiles through LDS.
-  __shared__ double sJJ[36 * kLoneMaxNb];
   const int wave = tid >> 6, lane = tid & 63, li = lane & 15, lk = lane >> 4;
   const int n6 = 6 * m, nt = (n6 + 15) / 16, nl = nt * (nt + 1) / 2, K = 3 * npt, ks = (K + 3) >> 2;
   v4d acc[kLoneWT];
@@ -1466,7 +1625,18 @@ __global__ __launch_bounds__(kBlock) void k_lone_schur(LoneSchurDev d, double* _
   const uint32_t out = static_cast<uint32_t>(hdr[2]);
   if (wave >= 2 && lane < n6) {
     const int a = lane / 6, r = lane - 6 * a;
-    if (wave == 3) {
+    if (fused) {
+      // J_a^T J_a is in sJJ already; gradient row r of a: J_a^T b - Z_a^T z
+      if (wave == 2) {
+        double zz = 0.0;
+        for (int p = 0; p < npt; ++p) {
+          const double* Zp = sZ + p * m18 + 18 * a + r;
+#pragma unroll
+          for (int k = 0; k < 3; ++k) zz += Zp[6 * k] * sz[3 * p + k];
+        }
+        arena[out + 36 * np + lane] = sJb[lane] - zz;
+      }
+    } else if (wave == 3) {
       double jj[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
       for (int p = 0; p < npt; ++p) {
         const double* Jp = sJ + p * m18 + 18 * a;
@@ -1811,10 +1981,10 @@ GroupPlan plan_groups(const TypeDev* td) {
 // the types of a group must be contiguous in type order for pbase to hold
 static_assert(kGroups[0] == 0xFu, "group 0 must cover types 0..3 contiguously");
 
-SumDev sum_for(const GroupPlan& gp, int g, double* partials, unsigned* counter, double* out) {
+SumDev sum_for(const GroupPlan& gp, int g, double* partials, unsigned* counter, double* out, int n_pre = 0) {
   SumDev sd;
   sd.partials = partials;
-  sd.total = gp.total;
+  sd.total = gp.total + n_pre;
   if (g == gp.last && out) {
     sd.counter = counter;
     sd.out = out;
@@ -1824,9 +1994,11 @@ SumDev sum_for(const GroupPlan& gp, int g, double* partials, unsigned* counter, 
 
 // no factors: the sum is 0
 void launch_empty_sum(double* partials, double* out, int* fail_src, int* fail_dst, hipStream_t s,
-                      const double* extra_in = nullptr, int extra_n = 0, double* extra_out = nullptr) {
+                      const double* extra_in = nullptr, int extra_n = 0, double* extra_out = nullptr,
+                      int total = 0) {
   SumDev sd;
   sd.partials = partials;
+  sd.total = total;
   sd.out = out;
   sd.fail_src = fail_src;
   sd.fail_dst = fail_dst;
@@ -1838,16 +2010,25 @@ void launch_empty_sum(double* partials, double* out, int* fail_src, int* fail_ds
 }  // namespace
 
 int error_blocks(const TypeDev* td) { return plan_groups(td).total; }
+int linearize_blocks(const TypeDev* td) { return plan_groups(td).total; }
 
 void launch_linearize(const TypeDev* td, const double* pose, const double* pt, double* arena, double* partials,
-                      unsigned* counter, double* out, hipStream_t s) {
+                      unsigned* counter, double* out, hipStream_t s, int n_pre) {
   const GroupPlan gp = plan_groups(td);
   for (int g = 0; g < kNGroups; ++g) {
     if (gp.blocks[g] == 0) continue;
     DH_GROUP_DISPATCH(g, k_linearize, gp.blocks[g], gp.dev[g], pose, pt, arena,
-                      sum_for(gp, g, partials, counter, out));
+                      sum_for(gp, g, partials, counter, out, n_pre));
   }
-  if (gp.last < 0 && out) launch_empty_sum(partials, out, nullptr, nullptr, s);
+  if (gp.last < 0 && out) launch_empty_sum(partials, out, nullptr, nullptr, s, nullptr, 0, nullptr, n_pre);
+}
+
+int launch_lone_lin(const LoneLinDev& d, const double* pose, const double* pt, double* arena, double* partials,
+                    hipStream_t s) {
+  if (d.n_group <= 0) return 0;
+  if (!d.blk || !d.t0.idx || !pose || !pt || !arena || !partials) return -1;   // never launched on a null table
+  k_lone_lin<<<d.n_group, kBlock, 0, s>>>(d, pose, pt, arena, partials);
+  return 0;
 }
 
 void launch_error(const TypeDev* td, const double* pose, const double* pt, double* partials, unsigned* counter,
@@ -1979,7 +2160,9 @@ extern "C" int dynohip_debug_lone_clock(unsigned long long* out) { return debug_
 
 void launch_lone_schur(const LoneSchurDev& d, double* arena, hipStream_t s) {
   if (d.n_group > 0)
-    k_lone_schur<<<d.n_group, kBlock, sizeof(double) * kLoneSub * lone_point_doubles(d.max_m), s>>>(d, arena);
+    k_lone_schur<<<d.n_group, kBlock,
+                   sizeof(double) * kLoneSub * (d.fused ? lone_point_doubles_fused(d.max_m) : lone_point_doubles(d.max_m)),
+                   s>>>(d, arena);
 }
 
 int backsub_blocks(const ChainDev& c, int n_lone, int n_pose) {

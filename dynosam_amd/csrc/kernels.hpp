@@ -18,6 +18,9 @@ struct TypeDev {
   const double* meas = nullptr;
   const double* isig = nullptr;
   const double* hk = nullptr;
+  // k_linearize only: the factors to linearise are list[0, n) (factor ids),
+  // null = factors 0 .. n-1 (the fused static landmarks leave theirs out)
+  const int32_t* list = nullptr;
 };
 
 struct GatherDev {
@@ -81,6 +84,21 @@ struct LoneSchurDev {
   int max_m = 0;                          // largest m (sizes the staging LDS)
   const int32_t* blk = nullptr;           // kLoneBlk ints per group
   uint64_t off_W = 0, off_L = 0, off_gp = 0, off_I6 = 0;
+  // fused: J_a^T J_a and J_a^T b come from the group's H area (k_lone_lin,
+  // plan.hpp lone_h_off), not from the PoseToPoint records
+  int fused = 0;
+};
+
+// fused static-landmark linearisation (k_lone_lin), a workgroup per lone
+// group block: evaluates the block's PoseToPoint factors and writes W (per
+// edge), D and g_p (per point), the block's per-pose sums J_a^T J_a, J_a^T b
+// (its H area) and its share of the linear error at delta = 0
+struct LoneLinDev {
+  int n_group = 0;
+  const int32_t* blk = nullptr;
+  TypeDev t0;                             // PoseToPoint factor data (record offset -> factor id via base, stride)
+  uint64_t off_W = 0, off_D = 0, off_gp = 0;
+  int pslot = 0;                          // partial slot of block 0 (linear error at delta = 0)
 };
 
 // reduced system in 64x64 tiles; tile (row tile i, column tile j) with
@@ -121,8 +139,16 @@ struct TileSchedDev {
 // all partials into *out (counter: a zeroed device word, left zeroed);
 // launch_linearize's sum is the linear error at delta = 0.
 int error_blocks(const TypeDev* td);
+// n_pre: partial slots [linearize_blocks(td), + n_pre) were written by an
+// earlier launch (k_lone_lin) and join the sum
+int linearize_blocks(const TypeDev* td);
 void launch_linearize(const TypeDev* td, const double* pose, const double* pt, double* arena, double* partials,
-                      unsigned* counter, double* out, hipStream_t s);
+                      unsigned* counter, double* out, hipStream_t s, int n_pre = 0);
+// fused static-landmark linearisation: W, D, g_p of the grouped lone points,
+// the groups' H areas, and partials[pslot + g] (before launch_linearize)
+// (-1 without launching when a table pointer is null)
+int launch_lone_lin(const LoneLinDev& d, const double* pose, const double* pt, double* arena, double* partials,
+                    hipStream_t s);
 // fail_src (optional): accumulated failure bits, moved to *fail_dst and cleared
 // extra_* (optional): the finishing block also sums extra_in[0, extra_n) in
 // order into *extra_out (the back-substitution's cost-change partials)

@@ -211,7 +211,7 @@ void plan_recycle(Plan& P) {
     k((f.*m).ent, (P.*m).ent);
   }
   k(f.red_A, P.red_A); k(f.red_B, P.red_B); k(f.red_slot, P.red_slot);
-  k(f.lgroup, P.lgroup); k(f.lone_pose, P.lone_pose); k(f.lone_blk, P.lone_blk);
+  k(f.lgroup, P.lgroup); k(f.lone_pose, P.lone_pose); k(f.lone_blk, P.lone_blk); k(f.lin_list0, P.lin_list0);
   k(f.band_D, P.band_D); k(f.tile_pos, P.tile_pos); k(f.row_start, P.row_start); k(f.row_col, P.row_col);
   k(f.row_slot, P.row_slot); k(f.ftask, P.ftask); k(f.pairs, P.pairs); k(f.flevel, P.flevel);
   k(f.fpanels, P.fpanels); k(f.fdep_start, P.fdep_start); k(f.fdep, P.fdep); k(f.fqueue, P.fqueue);
@@ -897,7 +897,10 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
           G.npt = k1 - k0;
           G.pose_beg = static_cast<int32_t>(P.lone_pose.size());
           G.out = static_cast<uint32_t>(arena);
-          arena += 36ull * (m * (m + 1) / 2) + 6ull * m;
+          // the per-try partial blocks and gradients (k_lone_schur), then the
+          // H area of the fused linearisation (k_lone_lin: 6x6 J_a^T J_a and
+          // J_a^T b per neighbour)
+          arena += 36ull * (m * (m + 1) / 2) + 6ull * m + 42ull * m;
           P.lone_max_m = std::max(P.lone_max_m, m);
           for (int32_t a = 0; a < m; ++a) P.lone_pose.push_back(P.edge_pose[e0 + a]);
           const size_t bo = P.lone_blk.size();
@@ -961,7 +964,8 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
     // the PoseToPoint factors outside the lone groups, in factor order (the
     // enumerations below run once per worker and pass: they skip the grouped
     // ones without visiting them)
-    std::vector<int32_t> keep0;
+    std::vector<int32_t>& keep0 = P.lin_list0;
+    keep0.clear();
     {
       // (an ordered filter on the workers: count per chunk, then fill)
       const int64_t n0 = P.types[0].n;

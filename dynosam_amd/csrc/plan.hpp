@@ -64,6 +64,9 @@ struct GEntry {
 // partial) entries. On the device a group is one block of kLoneBlk ints:
 // [m, npt, out, 0, point[kLoneSub], first edge[kLoneSub],
 //  PoseToPoint record offset (J_pose at +0, b at +27)[kLoneSub][m]].
+// The group's arena area at `out` holds those per-try partials (36 m(m+1)/2
+// + 6 m doubles), then its H area (42 m: the 6x6 J_a^T J_a per neighbour,
+// then the J_a^T b), written once per linearisation by k_lone_lin.
 constexpr int kLoneMaxNb = 10;
 constexpr int kLoneSub = 16;
 constexpr int kLoneBlk = 200;
@@ -181,6 +184,10 @@ struct Plan {
   std::vector<int32_t, default_init_allocator<int32_t>> lone_blk;   // kLoneBlk per group (device form)
   int lone_max_m = 0;
   bool lone_all_grouped = false;        // every lone point is in a group (no lone Y is read)
+  // the PoseToPoint factors outside the lone groups, in factor order: the
+  // ones k_linearize still records when the groups linearise their own
+  // factors (k_lone_lin, the fused static landmarks)
+  std::vector<int32_t> lin_list0;
   uint64_t off_I6 = 0;                  // 6x6 identity (the A operand of the partial entries)
   // arena
   uint64_t off_D = 0, off_E = 0, off_gp = 0, off_W = 0, off_Y = 0, off_v = 0, off_L = 0, off_M = 0;

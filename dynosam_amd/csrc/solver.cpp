@@ -420,6 +420,12 @@ struct dynohip_solver {
   DevBuf<double> pose, pt, pose_c, pt_c, arena;
   TypeBufs tb[kNTypes];
   TypeDev td[kNTypes];
+  // fused static landmarks (k_lone_lin): k_linearize's view of the types
+  // (PoseToPoint restricted to Plan::lin_list0) and the group kernel's
+  TypeDev td_lin[kNTypes];
+  DevBuf<int32_t> lin_list0;
+  LoneLinDev lld;
+  bool fused_env = true;   // DYNOHIP_FUSED_LONE=0 keeps the record path
   GatherBufs gD, gE, gGp, gW, gRed, gGred;
   DevBuf<int32_t> redA, redB;
   DevBuf<uint32_t> redslot;
@@ -551,7 +557,18 @@ int upload_plan(dynohip_solver* s, bool types_done = false) {
     d.isig = s->tb[t].isig.p;
     d.hk = s->tb[t].hk.p;
   }
-  slots = std::max(1, error_blocks(s->td));
+  HIPCHK(s, up.add(s->lin_list0, P.lin_list0));
+  for (int t = 0; t < kNTypes; ++t) s->td_lin[t] = s->td[t];
+  s->td_lin[0].n = static_cast<int>(P.lin_list0.size());
+  s->td_lin[0].list = s->lin_list0.p;
+  LoneLinDev& ll = s->lld;
+  ll.n_group = static_cast<int>(P.lgroup.size());
+  ll.t0 = s->td[0];
+  ll.off_W = P.off_W;
+  ll.off_D = P.off_D;
+  ll.off_gp = P.off_gp;
+  ll.pslot = linearize_blocks(s->td_lin);
+  slots = std::max(1, std::max(error_blocks(s->td), ll.pslot + ll.n_group));
   s->partial_slots = slots;
   HIPCHK(s, s->partials.alloc(2ull * slots));
   HIPCHK(s, s->result.alloc(8));
@@ -643,6 +660,7 @@ int upload_plan(dynohip_solver* s, bool types_done = false) {
   ld.off_L = P.off_L;
   ld.off_gp = P.off_gp;
   ld.off_I6 = P.off_I6;
+  s->lld.blk = s->lone_blk.p;
   HIPCHK(s, s->lcpart.alloc(static_cast<size_t>(backsub_blocks(
                                 c, P.lone_all_grouped ? static_cast<int>(P.lgroup.size()) : 0, P.n_pose)) + 1));
   TileDev& b = s->bd;
@@ -781,22 +799,39 @@ int compute_error(dynohip_solver* s, const double* pose, const double* pt, doubl
   return comm_sum(s, err_out, 1, 0);
 }
 
-// linearisation + point-side blocks (once per outer iteration); lin0, when
-// given, receives the linear error at delta = 0 (0.5 ||b||^2)
-void enqueue_linearize(dynohip_solver* s, const double* pose, const double* pt, double* lin0 = nullptr) {
-  Plan& P = s->plan;
-  double* A = s->arena.p;
-  launch_linearize(s->td, pose, pt, A, s->partials.p, s->sumctr.p, lin0, s->stream);
-  const GatherDev g[4] = {s->gD.dev(P.gD.ntargets()), s->gE.dev(P.gE.ntargets()), s->gGp.dev(P.gGp.ntargets()),
-                          s->gW.dev(P.gW.ntargets())};
-  double* const dst[4] = {A + P.off_D, A + P.off_E, A + P.off_gp, A + P.off_W};
-  launch_gather_point(g, dst, A, s->stream, P.lone_all_grouped ? static_cast<int>(P.lgroup.size()) : 0,
-                      s->lone_blk.p);
-}
-
 // result[0] of a try holds the linearised cost change (x2) rather than the
 // new linear error
 bool lin_change_mode(const dynohip_solver* s) { return s->nranks == 1 && !s->linerr_direct; }
+
+// The static landmarks are linearised inside their group blocks (k_lone_lin),
+// with no Jacobian record: every lone point grouped, and nothing reading the
+// records afterwards (the direct linear error and the partitioned handles do)
+bool fused_lone(const dynohip_solver* s) {
+  return s->fused_env && s->plan.lone_all_grouped && !s->plan.lgroup.empty() && lin_change_mode(s);
+}
+
+// linearisation + point-side blocks (once per outer iteration); lin0, when
+// given, receives the linear error at delta = 0 (0.5 ||b||^2).
+// all_records: every factor's J | b record (the dynohip_linearize test hook)
+int enqueue_linearize(dynohip_solver* s, const double* pose, const double* pt, double* lin0 = nullptr,
+                      bool all_records = false) {
+  Plan& P = s->plan;
+  double* A = s->arena.p;
+  const GatherDev g[4] = {s->gD.dev(P.gD.ntargets()), s->gE.dev(P.gE.ntargets()), s->gGp.dev(P.gGp.ntargets()),
+                          s->gW.dev(P.gW.ntargets())};
+  double* const dst[4] = {A + P.off_D, A + P.off_E, A + P.off_gp, A + P.off_W};
+  if (fused_lone(s) && !all_records) {
+    if (launch_lone_lin(s->lld, pose, pt, A, s->partials.p, s->stream))
+      return set_err(s, DYNOHIP_EHIP, "internal: fused static-landmark linearisation without its tables");
+    launch_linearize(s->td_lin, pose, pt, A, s->partials.p, s->sumctr.p, lin0, s->stream, s->lld.n_group);
+    launch_gather_point(g, dst, A, s->stream);
+    return 0;
+  }
+  launch_linearize(s->td, pose, pt, A, s->partials.p, s->sumctr.p, lin0, s->stream);
+  launch_gather_point(g, dst, A, s->stream, P.lone_all_grouped ? static_cast<int>(P.lgroup.size()) : 0,
+                      s->lone_blk.p);
+  return 0;
+}
 
 // damped solve + linearised error + retract + error for one lambda.
 // result[0] = new linear error (or 2x the cost change, lin_change_mode),
@@ -817,6 +852,7 @@ int enqueue_try(dynohip_solver* s, double lambda) {
   z.n[2] = static_cast<int64_t>(s->fsync.n) / 2;
   launch_chain_factor(s->cd, A, lambda, s->failp, z, st);
   launch_chain_solve_y(s->cd, A, st);
+  s->ld.fused = fused_lone(s) ? 1 : 0;
   launch_lone_schur(s->ld, A, st);
   if (timed) (void)hipEventRecord(s->ev[3], st);
   launch_gather_reduced(s->gRed.dev(P.gRed.ntargets()), s->redA.p, s->redB.p, s->redslot.p,
@@ -914,7 +950,14 @@ void compute_base_stats(dynohip_solver* s) {
     // the point-side gathers
     double per = 4.0 * kNKeys[t] + 8.0 * kMeasDim[t] + 8.0 * kDim[t] + 8.0 + 2.0 * 8.0 * tp.stride;
     for (int sl = 0; sl < kNKeys[t]; ++sl) per += kSlotKind[t][sl] == 0 ? 96.0 : 24.0;
-    impl += per * tp.n;
+    if (t == 0 && fused_lone(s)) {
+      // the grouped static landmarks' factors (k_lone_lin) read their inputs
+      // and write no record
+      const double nrec = static_cast<double>(P.lin_list0.size());
+      impl += per * nrec + (per - 2.0 * 8.0 * tp.stride) * (tp.n - nrec);
+    } else {
+      impl += per * tp.n;
+    }
     for (int i = 0; i < tp.n; ++i)
       for (int a = 0; a < kNKeys[t]; ++a)
         for (int b = a + 1; b < kNKeys[t]; ++b)
@@ -929,8 +972,11 @@ void compute_base_stats(dynohip_solver* s) {
   const double wr = 8.0 * (9.0 * P.n_pt + 18.0 * P.n_edge + 9.0 * P.gE.ntargets() + 27.0 * P.n_pose + 36.0 * n_pp);
   st.lin_bytes = rd + wr;
   st.lin_bytes_read = rd;
-  // point-side block outputs (D, E, g_p, W) written by the gathers
+  // point-side block outputs (D, E, g_p, W) written by the gathers; the
+  // fused groups' H areas (42 doubles per group and neighbour)
   impl += 8.0 * (9.0 * P.n_pt + 9.0 * P.gE.ntargets() + 3.0 * P.n_pt + 18.0 * P.n_edge);
+  if (fused_lone(s))
+    for (const LoneGroup& G : P.lgroup) impl += 8.0 * 42.0 * G.m;
   st.lin_bytes_impl = impl;
   double asmb = 0.0;
   for (const GEntry& e : P.gRed.ent) asmb += 16.0 + 8.0 * e.k * 12.0;
@@ -976,7 +1022,7 @@ int lm_iterate(dynohip_solver* s) {
     oldlin_slot = 3;
   } else {
     if (s->timing) (void)hipEventRecord(s->ev[0], st);
-    enqueue_linearize(s, s->pose.p, s->pt.p, s->result.p + 2);
+    if (int rc = enqueue_linearize(s, s->pose.p, s->pt.p, s->result.p + 2)) return rc;
     if (s->timing) (void)hipEventRecord(s->ev[1], st);
   }
   s->lin_valid = false;
@@ -991,7 +1037,7 @@ int lm_iterate(dynohip_solver* s) {
     te.old_linear_error = oldLin;
     if (relinearize) {
       // a rejected speculative step left the candidate's linearisation
-      enqueue_linearize(s, s->pose.p, s->pt.p);
+      if (int rc = enqueue_linearize(s, s->pose.p, s->pt.p)) return rc;
       s->n_lin++;
       relinearize = false;
     }
@@ -1002,7 +1048,7 @@ int lm_iterate(dynohip_solver* s) {
     if (speculate) {
       // result[3] is read with the next try's results (stream order keeps
       // this launch's value until then)
-      enqueue_linearize(s, s->pose_c.p, s->pt_c.p, s->result.p + 3);
+      if (int rc = enqueue_linearize(s, s->pose_c.p, s->pt_c.p, s->result.p + 3)) return rc;
     }
     HIPCHK(s, hipEventSynchronize(s->ev_res));
     double res[5];
@@ -1159,6 +1205,7 @@ int dynohip_create(int device_id, dynohip_solver** out) {
   HostCache::get().take(s->plan, s->graph);   // stale contents: has_graph / has_plan are false
   s->device = device_id;
   if (const char* e = std::getenv("DYNOHIP_LINERR_DIRECT")) s->linerr_direct = std::atoi(e) != 0;
+  if (const char* e = std::getenv("DYNOHIP_FUSED_LONE")) s->fused_env = std::atoi(e) != 0;
   s->stream = r.stream;
   s->side = r.side;
   s->ev_main = r.ev_main;
@@ -1493,7 +1540,7 @@ int dynohip_linearize(dynohip_solver* s, double* out, size_t n_doubles) {
   if (n_doubles < dynohip_linearize_size(s)) return set_err(s, DYNOHIP_EINVAL, "output buffer too small");
   (void)hipSetDevice(s->device);
   s->lin_valid = false;
-  enqueue_linearize(s, s->pose.p, s->pt.p);
+  if (int rc2 = enqueue_linearize(s, s->pose.p, s->pt.p, nullptr, true)) return rc2;
   const Plan& P = s->plan;
   std::vector<double> rec;
   size_t o = 0;
@@ -1532,7 +1579,8 @@ int dynohip_solve_delta(dynohip_solver* s, double lambda, double* delta_out, siz
   const Plan& P = s->plan;
   // the same launches as one tryLambda of lm_iterate, at the current values
   s->lin_valid = false;
-  enqueue_linearize(s, s->pose.p, s->pt.p, s->result.p + 2);
+  rc = enqueue_linearize(s, s->pose.p, s->pt.p, s->result.p + 2);
+  if (rc) return rc;
   rc = enqueue_try(s, lambda);
   if (rc) return rc;
   const size_t nrp = static_cast<size_t>(P.NT) * kTile;

@@ -275,6 +275,43 @@ def test_cliques_fixture_matches_golden(gpu_available):
         assert rel(out[off[i]:off[i + 1]], ref) < PER_ITER_TOL
 
 
+@pytest.mark.parametrize("name", ["T2", "C1", "C2", "mixed"])
+def test_fused_static_landmarks_match_records(gpu_available, name, monkeypatch):
+    """The static landmarks linearised inside their group blocks (k_lone_lin:
+    no PoseToPoint records; W, D, g_p and the groups' J_a^T J_a, J_a^T b
+    formed in registers and LDS) against the record path
+    (DYNOHIP_FUSED_LONE=0: k_linearize writes every record, the point gathers
+    and k_lone_schur re-read them). Same factor bits, same pair-block sums;
+    only the groups' gradients are summed in another order (J_a^T b, then
+    - Z_a^T z, instead of one interleaved sum), so the LM runs agree in every
+    decision and the iterates to rounding."""
+    if name == "mixed":
+        g, v = mixed_lone_graph()[:2]   # not all lone points grouped: the record path either way
+    else:
+        g, v, _ = synth.generate(name)
+    runs = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("DYNOHIP_FUSED_LONE", fused)
+        s = Solver(0)
+        s.set_graph(g)
+        s.set_values(v)
+        out = []
+        for _ in range(4):
+            sm = s.iterate()
+            out.append((sm.iterations, sm.inner_iterations, s.values_data()))
+        runs.append((out, s.trace()))
+        s.close()
+    (oa, ta), (ob, tb) = runs
+    assert [(e["lam"], e["accepted"]) for e in ta] == [(e["lam"], e["accepted"]) for e in tb]
+    for a, b in zip(ta, tb):
+        # 0.5 ||b||^2 at delta = 0: the same per-factor terms, summed by block
+        assert a["old_linear_error"] == pytest.approx(b["old_linear_error"], rel=1e-13)
+    for (ia, na, va), (ib, nb, vb) in zip(oa, ob):
+        assert (ia, na) == (ib, nb)
+        print(name, ia, f"values rel {rel(va, vb):.2e}")
+        assert rel(va, vb) < 1e-10
+
+
 @pytest.mark.parametrize("name", ["C1", "C2"])
 def test_execution_paths_agree(gpu_available, name):
     """The level-launched factorisation (with and without the concurrent

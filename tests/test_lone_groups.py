@@ -90,7 +90,9 @@ def test_group_blocks_match_the_graph(plan):
     # partial areas: disjoint, in group order, m(m+1)/2 6x6 blocks + m gradients each
     for g in range(ngroups - 1):
         m = int(blk[g, 0])
-        assert outs[g + 1] == outs[g] + 36 * (m * (m + 1) // 2) + 6 * m
+        # per-try partial blocks and gradients, then the fused linearisation's
+        # H area (42 m: J_a^T J_a and J_a^T b per neighbour)
+        assert outs[g + 1] == outs[g] + 36 * (m * (m + 1) // 2) + 6 * m + 42 * m
 
 
 def test_groups_split_lists_evenly_in_first_pose_order(plan):
