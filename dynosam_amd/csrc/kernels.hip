@@ -418,6 +418,123 @@ __device__ __forceinline__ double linerr_one(const TypeDev& tp, int i, const dou
   return e * 0.5;
 }
 
+// ---- fused static landmarks (k_linearize's group blocks) --------------------
+// The grouped static landmarks' PoseToPoint factors (the bulk of every graph:
+// 385k of the 430k PoseToPoint factors at NS) are linearised where their
+// blocks are formed, with no J | b record in HBM. A workgroup per group block,
+// a lane per (point, neighbour a) as lone_point_block: the lane evaluates its
+// factor (eval_whitened, the records' bits), writes W_a = J_p^T J_x and sums
+// D and g_p over the point's lanes by the same shuffles; it stages J_x | b in
+// LDS, from which a thread per (a, entry) sums the block's J_a^T J_a and
+// J_a^T b over the points in point order (the order, and so the bits, of
+// k_lone_schur's former sums over the records) into the group's H area. The
+// group blocks run as the first workgroups of the PoseToPoint / Ternary /
+// Between / Prior linearisation launch (k_linearize<0xF>), and their lanes'
+// 0.5 ||b||^2 join that launch's partials of the linear error at delta = 0.
+// H area (plan.hpp): after the per-try partial blocks at `out`, [a] 6x6 full
+// (symmetric) J_a^T J_a, then [a] J_a^T b.
+__host__ __device__ constexpr uint32_t lone_h_off(int m) { return 36u * static_cast<uint32_t>(m * (m + 1) / 2) + 6u * m; }
+constexpr int kRec0 = kDim[0] * kCols[0] + kDim[0];   // PoseToPoint record stride (plan.cpp)
+constexpr int kLoneJ = 21;                            // staged per (point, a): J_x (3x6) | b (3)
+
+// Group block gb; returns this thread's share of the block's linear error at
+// delta = 0 (k_linearize's group_finish sums it with the factor blocks').
+// Every thread of the workgroup must call it (it holds barriers).
+__device__ double lone_lin_block(const LoneLinDev& d, int gb, const double* __restrict__ pose,
+                                 const double* __restrict__ pt, double* __restrict__ arena) {
+  __shared__ int32_t hdr[kLoneBlk];
+  __shared__ double sJ[kLoneSub * kLoneMaxNb * kLoneJ];
+  const int tid = threadIdx.x;
+  for (int q = tid; q < kLoneBlk; q += kBlock) hdr[q] = d.blk[static_cast<int64_t>(gb) * kLoneBlk + q];
+  __syncthreads();
+  const int m = hdr[0], npt = hdr[1];
+  const int lane = tid & 63, per = 64 / m, uu = lane / m, a = lane - uu * m;
+  const int u = (tid >> 6) * per + uu;
+  const bool valid = uu < per && u < npt;
+  double Dp[9], gp[3], e = 0.0;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) Dp[k] = 0.0;
+  gp[0] = gp[1] = gp[2] = 0.0;
+  if (valid) {
+    const uint32_t rec = static_cast<uint32_t>(hdr[4 + 2 * kLoneSub + m * u + a]);
+    const int f = static_cast<int>((rec - d.t0.base) / kRec0);
+    double J[kDim[0] * kCols[0]], bb[3];
+    e = eval_whitened<0>(d.t0, f, pose, pt, J, bb);
+    // the record's blocks: J_x (3x6) and J_p (3x3), row-major
+    double Jx[18], Jp[9];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+#pragma unroll
+      for (int c = 0; c < 6; ++c) Jx[6 * k + c] = J[kCols[0] * k + c];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) Jp[3 * k + c] = J[kCols[0] * k + 6 + c];
+    }
+    double* W = arena + d.off_W + 18ll * (hdr[4 + kLoneSub + u] + a);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+#pragma unroll
+      for (int c = 0; c < 6; ++c) W[6 * k + c] = Jp[k] * Jx[c] + Jp[3 + k] * Jx[6 + c] + Jp[6 + k] * Jx[12 + c];
+#pragma unroll
+      for (int l = 0; l < 3; ++l) Dp[3 * k + l] = Jp[k] * Jp[l] + Jp[3 + k] * Jp[3 + l] + Jp[6 + k] * Jp[6 + l];
+      gp[k] = Jp[k] * bb[0] + Jp[3 + k] * bb[1] + Jp[6 + k] * bb[2];
+    }
+    double* sj = sJ + kLoneJ * (m * u + a);
+#pragma unroll
+    for (int k = 0; k < 18; ++k) sj[k] = Jx[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) sj[18 + k] = bb[k];
+  }
+  // lane a == 0 of each point sums its m lanes (lone_point_block's order)
+  double Ds[9], gs[3];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) Ds[k] = 0.0;
+  gs[0] = gs[1] = gs[2] = 0.0;
+  for (int j = 0; j < m; ++j) {
+    const int src = min(lane + j, 63);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) Ds[k] += __shfl(Dp[k], src);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) gs[k] += __shfl(gp[k], src);
+  }
+  if (valid && a == 0) {
+    const int p = hdr[4 + u];
+    double* D = arena + d.off_D + 9ll * p;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) D[k] = Ds[k];
+    double* G = arena + d.off_gp + 3ll * p;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) G[k] = gs[k];
+  }
+  __syncthreads();   // sJ
+  // the block's J_a^T J_a (lower entries, written to both halves) and J_a^T b
+  double* H = arena + static_cast<uint32_t>(hdr[2]) + lone_h_off(m);
+  for (int t = tid; t < 27 * m; t += kBlock) {
+    const int aa = t / 27, q = t - 27 * aa;
+    double acc = 0.0;
+    if (q < 21) {
+      int r = 0;
+      while ((r + 1) * (r + 2) / 2 <= q) ++r;
+      const int c = q - r * (r + 1) / 2;
+      for (int p = 0; p < npt; ++p) {
+        const double* sj = sJ + kLoneJ * (m * p + aa);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) acc += sj[6 * k + r] * sj[6 * k + c];
+      }
+      H[36 * aa + 6 * r + c] = acc;
+      H[36 * aa + 6 * c + r] = acc;
+    } else {
+      const int r = q - 21;
+      for (int p = 0; p < npt; ++p) {
+        const double* sj = sJ + kLoneJ * (m * p + aa);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) acc += sj[6 * k + r] * sj[18 + k];
+      }
+      H[36 * m + 6 * aa + r] = acc;
+    }
+  }
+  return e;
+}
+
 // ---- type groups ------------------------------------------------------------
 // One launch covers every factor type of a group (a bit mask over types):
 // block b belongs to the type whose [bstart[T], bstart[T+1]) holds it, so a
@@ -430,6 +547,10 @@ struct GroupDev {
   TypeDev t[kNTypes];
   int bstart[kNTypes + 1];
   int pbase;   // partial slot of this launch's block 0
+  // k_linearize<0xF> only: workgroups [0, n_lone) are the fused static
+  // landmarks' group blocks (lone_lin_block), the factor blocks follow
+  int n_lone;
+  LoneLinDev lone;
 };
 
 // Sum of per-block partials. The last launch of a sum (out != nullptr) folds
@@ -540,7 +661,15 @@ template <unsigned M>
 __global__ __launch_bounds__(kBlock) void k_linearize(GroupDev g, const double* __restrict__ pose,
                                                       const double* __restrict__ pt, double* __restrict__ arena,
                                                       SumDev sd) {
-  const double e = group_apply<M>(g, gridDim.x - 1 - blockIdx.x, [&](auto tc, int i) {
+  double e;
+  if constexpr (M == 0xFu) {
+    if (static_cast<int>(blockIdx.x) < g.n_lone) {
+      e = lone_lin_block(g.lone, blockIdx.x, pose, pt, arena);
+      group_finish(e, g, sd);
+      return;
+    }
+  }
+  e = group_apply<M>(g, gridDim.x - 1 - blockIdx.x, [&](auto tc, int i) {
     return linearize_one<decltype(tc)::value>(g.t[decltype(tc)::value], i, pose, pt, arena);
   });
   group_finish(e, g, sd);
@@ -758,121 +887,6 @@ __device__ __forceinline__ void lone_point_block(const PointGatherDev& pg, int g
     double* G = pg.dst[2] + 3ll * pt;
 #pragma unroll
     for (int k = 0; k < 3; ++k) G[k] = gs[k];
-  }
-}
-
-// ---- fused static landmarks: k_lone_lin ------------------------------------
-// The grouped static landmarks' PoseToPoint factors (the bulk of every graph:
-// 385k of the 430k PoseToPoint factors at NS) are linearised where their
-// blocks are formed, with no J | b record in HBM. A workgroup per group block,
-// a lane per (point, neighbour a) as lone_point_block: the lane evaluates its
-// factor (eval_whitened, the records' bits), writes W_a = J_p^T J_x and sums
-// D and g_p over the point's lanes by the same shuffles; it stages J_x | b in
-// LDS, from which a thread per (a, entry) sums the block's J_a^T J_a and
-// J_a^T b over the points in point order (the order, and so the bits, of
-// k_lone_schur's former sums over the records) into the group's H area. The
-// lane's 0.5 ||b||^2 goes to the block's partial of the linear error at
-// delta = 0 (summed with k_linearize's partials).
-// H area (plan.hpp): after the per-try partial blocks at `out`, [a] 6x6 full
-// (symmetric) J_a^T J_a, then [a] J_a^T b.
-__host__ __device__ constexpr uint32_t lone_h_off(int m) { return 36u * static_cast<uint32_t>(m * (m + 1) / 2) + 6u * m; }
-constexpr int kRec0 = kDim[0] * kCols[0] + kDim[0];   // PoseToPoint record stride (plan.cpp)
-constexpr int kLoneJ = 21;                            // staged per (point, a): J_x (3x6) | b (3)
-
-__global__ __launch_bounds__(kBlock) void k_lone_lin(LoneLinDev d, const double* __restrict__ pose,
-                                                     const double* __restrict__ pt, double* __restrict__ arena,
-                                                     double* __restrict__ partials) {
-  __shared__ int32_t hdr[kLoneBlk];
-  __shared__ double sJ[kLoneSub * kLoneMaxNb * kLoneJ];
-  const int tid = threadIdx.x;
-  for (int q = tid; q < kLoneBlk; q += kBlock) hdr[q] = d.blk[static_cast<int64_t>(blockIdx.x) * kLoneBlk + q];
-  __syncthreads();
-  const int m = hdr[0], npt = hdr[1];
-  const int lane = tid & 63, per = 64 / m, uu = lane / m, a = lane - uu * m;
-  const int u = (tid >> 6) * per + uu;
-  const bool valid = uu < per && u < npt;
-  double Dp[9], gp[3], e = 0.0;
-#pragma unroll
-  for (int k = 0; k < 9; ++k) Dp[k] = 0.0;
-  gp[0] = gp[1] = gp[2] = 0.0;
-  if (valid) {
-    const uint32_t rec = static_cast<uint32_t>(hdr[4 + 2 * kLoneSub + m * u + a]);
-    const int f = static_cast<int>((rec - d.t0.base) / kRec0);
-    double J[kDim[0] * kCols[0]], bb[3];
-    e = eval_whitened<0>(d.t0, f, pose, pt, J, bb);
-    // the record's blocks: J_x (3x6) and J_p (3x3), row-major
-    double Jx[18], Jp[9];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-#pragma unroll
-      for (int c = 0; c < 6; ++c) Jx[6 * k + c] = J[kCols[0] * k + c];
-#pragma unroll
-      for (int c = 0; c < 3; ++c) Jp[3 * k + c] = J[kCols[0] * k + 6 + c];
-    }
-    double* W = arena + d.off_W + 18ll * (hdr[4 + kLoneSub + u] + a);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-#pragma unroll
-      for (int c = 0; c < 6; ++c) W[6 * k + c] = Jp[k] * Jx[c] + Jp[3 + k] * Jx[6 + c] + Jp[6 + k] * Jx[12 + c];
-#pragma unroll
-      for (int l = 0; l < 3; ++l) Dp[3 * k + l] = Jp[k] * Jp[l] + Jp[3 + k] * Jp[3 + l] + Jp[6 + k] * Jp[6 + l];
-      gp[k] = Jp[k] * bb[0] + Jp[3 + k] * bb[1] + Jp[6 + k] * bb[2];
-    }
-    double* sj = sJ + kLoneJ * (m * u + a);
-#pragma unroll
-    for (int k = 0; k < 18; ++k) sj[k] = Jx[k];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) sj[18 + k] = bb[k];
-  }
-  // lane a == 0 of each point sums its m lanes (lone_point_block's order)
-  double Ds[9], gs[3];
-#pragma unroll
-  for (int k = 0; k < 9; ++k) Ds[k] = 0.0;
-  gs[0] = gs[1] = gs[2] = 0.0;
-  for (int j = 0; j < m; ++j) {
-    const int src = min(lane + j, 63);
-#pragma unroll
-    for (int k = 0; k < 9; ++k) Ds[k] += __shfl(Dp[k], src);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) gs[k] += __shfl(gp[k], src);
-  }
-  if (valid && a == 0) {
-    const int p = hdr[4 + u];
-    double* D = arena + d.off_D + 9ll * p;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) D[k] = Ds[k];
-    double* G = arena + d.off_gp + 3ll * p;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) G[k] = gs[k];
-  }
-  const double es = block_sum(e);   // (its barrier also publishes sJ)
-  if (tid == 0) partials[d.pslot + blockIdx.x] = es;
-  __syncthreads();
-  // the block's J_a^T J_a (lower entries, written to both halves) and J_a^T b
-  double* H = arena + static_cast<uint32_t>(hdr[2]) + lone_h_off(m);
-  for (int t = tid; t < 27 * m; t += kBlock) {
-    const int aa = t / 27, q = t - 27 * aa;
-    double acc = 0.0;
-    if (q < 21) {
-      int r = 0;
-      while ((r + 1) * (r + 2) / 2 <= q) ++r;
-      const int c = q - r * (r + 1) / 2;
-      for (int p = 0; p < npt; ++p) {
-        const double* sj = sJ + kLoneJ * (m * p + aa);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) acc += sj[6 * k + r] * sj[6 * k + c];
-      }
-      H[36 * aa + 6 * r + c] = acc;
-      H[36 * aa + 6 * c + r] = acc;
-    } else {
-      const int r = q - 21;
-      for (int p = 0; p < npt; ++p) {
-        const double* sj = sJ + kLoneJ * (m * p + aa);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) acc += sj[6 * k + r] * sj[18 + k];
-      }
-      H[36 * m + 6 * aa + r] = acc;
-    }
   }
 }
 
@@ -1231,6 +1245,14 @@ __global__ __launch_bounds__(kBlock) void k_chain_factor(ChainDev cd, double* __
     double2* p = reinterpret_cast<double2*>(zb.p[k]);
     const int64_t n = zb.n[k] / 2;
     for (int64_t i = i0; i < n; i += stride) p[i] = zero;
+  }
+  const double sv = __builtin_bit_cast(double, kBackSentinel);
+  const double2 sent = {sv, sv};
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    double2* p = reinterpret_cast<double2*>(zb.s[k]);
+    const int64_t n = zb.sn[k] / 2;
+    for (int64_t i = i0; i < n; i += stride) p[i] = sent;
   }
 }
 
@@ -1650,15 +1672,21 @@ __global__ __launch_bounds__(kBlock) void k_lone_schur(LoneSchurDev d, double* _
 #pragma unroll
       for (int c = 0; c < 6; ++c) sJJ[36 * a + 6 * r + c] = jj[c];
     } else {
-      double g = 0.0;
+      // J_a^T b over the points (k_lone_lin's H-area order), then Z_a^T z:
+      // the fused and the record paths give the same bits
+      double gj = 0.0, zz = 0.0;
       for (int p = 0; p < npt; ++p) {
         const double* Jp = sJ + p * m18 + 18 * a + r;
-        const double* Zp = sZ + p * m18 + 18 * a + r;
         const double* Bp = sB + p * 3 * m + 3 * a;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) g += Jp[6 * k] * Bp[k] - Zp[6 * k] * sz[3 * p + k];
+        for (int k = 0; k < 3; ++k) gj += Jp[6 * k] * Bp[k];
       }
-      arena[out + 36 * np + lane] = g;
+      for (int p = 0; p < npt; ++p) {
+        const double* Zp = sZ + p * m18 + 18 * a + r;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) zz += Zp[6 * k] * sz[3 * p + k];
+      }
+      arena[out + 36 * np + lane] = gj - zz;
     }
   }
   __syncthreads();
@@ -1951,14 +1979,20 @@ struct GroupPlan {
   int total = 0, last = -1;
 };
 
-GroupPlan plan_groups(const TypeDev* td) {
+// lone (k_linearize only): the fused static landmarks' group blocks lead
+// group 0's launch and take partial slots [0, n_group); the factor blocks'
+// slots follow
+GroupPlan plan_groups(const TypeDev* td, const LoneLinDev* lone = nullptr) {
   GroupPlan gp;
+  const int nl = lone ? lone->n_group : 0;
   int tstart[kNTypes + 1];
-  tstart[0] = 0;
+  tstart[0] = nl;
   for (int t = 0; t < kNTypes; ++t) tstart[t + 1] = tstart[t] + nblocks(td[t].n);
   gp.total = tstart[kNTypes];
   for (int g = 0; g < kNGroups; ++g) {
     GroupDev& d = gp.dev[g];
+    d.n_lone = g == 0 ? nl : 0;
+    if (g == 0 && lone) d.lone = *lone;
     int lo = -1, b = 0;
     for (int t = 0; t < kNTypes; ++t) {
       d.t[t] = td[t];
@@ -1971,9 +2005,9 @@ GroupPlan plan_groups(const TypeDev* td) {
       }
     }
     d.bstart[kNTypes] = b;
-    d.pbase = lo < 0 ? 0 : lo;
-    gp.blocks[g] = b;
-    if (b > 0) gp.last = g;
+    d.pbase = g == 0 ? 0 : (lo < 0 ? 0 : lo);
+    gp.blocks[g] = b + d.n_lone;
+    if (gp.blocks[g] > 0) gp.last = g;
   }
   return gp;
 }
@@ -1981,10 +2015,10 @@ GroupPlan plan_groups(const TypeDev* td) {
 // the types of a group must be contiguous in type order for pbase to hold
 static_assert(kGroups[0] == 0xFu, "group 0 must cover types 0..3 contiguously");
 
-SumDev sum_for(const GroupPlan& gp, int g, double* partials, unsigned* counter, double* out, int n_pre = 0) {
+SumDev sum_for(const GroupPlan& gp, int g, double* partials, unsigned* counter, double* out) {
   SumDev sd;
   sd.partials = partials;
-  sd.total = gp.total + n_pre;
+  sd.total = gp.total;
   if (g == gp.last && out) {
     sd.counter = counter;
     sd.out = out;
@@ -1994,11 +2028,9 @@ SumDev sum_for(const GroupPlan& gp, int g, double* partials, unsigned* counter, 
 
 // no factors: the sum is 0
 void launch_empty_sum(double* partials, double* out, int* fail_src, int* fail_dst, hipStream_t s,
-                      const double* extra_in = nullptr, int extra_n = 0, double* extra_out = nullptr,
-                      int total = 0) {
+                      const double* extra_in = nullptr, int extra_n = 0, double* extra_out = nullptr) {
   SumDev sd;
   sd.partials = partials;
-  sd.total = total;
   sd.out = out;
   sd.fail_src = fail_src;
   sd.fail_dst = fail_dst;
@@ -2010,24 +2042,20 @@ void launch_empty_sum(double* partials, double* out, int* fail_src, int* fail_ds
 }  // namespace
 
 int error_blocks(const TypeDev* td) { return plan_groups(td).total; }
-int linearize_blocks(const TypeDev* td) { return plan_groups(td).total; }
+int linearize_blocks(const TypeDev* td, const LoneLinDev* lone) { return plan_groups(td, lone).total; }
 
-void launch_linearize(const TypeDev* td, const double* pose, const double* pt, double* arena, double* partials,
-                      unsigned* counter, double* out, hipStream_t s, int n_pre) {
-  const GroupPlan gp = plan_groups(td);
+int launch_linearize(const TypeDev* td, const double* pose, const double* pt, double* arena, double* partials,
+                     unsigned* counter, double* out, hipStream_t s, const LoneLinDev* lone) {
+  if (lone && lone->n_group > 0 && (!lone->blk || !lone->t0.idx))
+    return -1;   // never launched on a null table
+  if (lone && lone->n_group <= 0) lone = nullptr;
+  const GroupPlan gp = plan_groups(td, lone);
   for (int g = 0; g < kNGroups; ++g) {
     if (gp.blocks[g] == 0) continue;
     DH_GROUP_DISPATCH(g, k_linearize, gp.blocks[g], gp.dev[g], pose, pt, arena,
-                      sum_for(gp, g, partials, counter, out, n_pre));
+                      sum_for(gp, g, partials, counter, out));
   }
-  if (gp.last < 0 && out) launch_empty_sum(partials, out, nullptr, nullptr, s, nullptr, 0, nullptr, n_pre);
-}
-
-int launch_lone_lin(const LoneLinDev& d, const double* pose, const double* pt, double* arena, double* partials,
-                    hipStream_t s) {
-  if (d.n_group <= 0) return 0;
-  if (!d.blk || !d.t0.idx || !pose || !pt || !arena || !partials) return -1;   // never launched on a null table
-  k_lone_lin<<<d.n_group, kBlock, 0, s>>>(d, pose, pt, arena, partials);
+  if (gp.last < 0 && out) launch_empty_sum(partials, out, nullptr, nullptr, s);
   return 0;
 }
 
@@ -2133,7 +2161,7 @@ void launch_sep_rhs(int n_sep_tiles, const int32_t* tile, const int32_t* start, 
 
 void launch_chain_factor(const ChainDev& c, double* arena, double lambda, int* fail, const ZeroDev& z,
                          hipStream_t s) {
-  const int64_t nz = std::max(z.n[0], std::max(z.n[1], z.n[2])) / 2;
+  const int64_t nz = std::max(std::max(z.n[0], std::max(z.n[1], z.n[2])), std::max(z.sn[0], z.sn[1])) / 2;
   const int nbz = nz == 0 ? 0 : static_cast<int>(std::min<int64_t>(1024, nblocks(nz)));
   const int nbg = nblocks(static_cast<int64_t>(c.n_long) * kGrp);
   const int nbs = nblocks(c.n_comp - c.n_long);

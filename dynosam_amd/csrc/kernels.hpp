@@ -51,10 +51,13 @@ struct ReducedGatherDev {
   const uint8_t* damp = nullptr;  // partitioned: per reduced row, 1 = this rank adds lambda (null: every row)
 };
 
-// buffers zeroed by the blocks past the chains in k_chain_factor
+// buffers zeroed by the blocks past the chains in k_chain_factor, and
+// buffers filled with kBackSentinel (k_back_poll's x and partials)
 struct ZeroDev {
   double* p[3] = {};
   int64_t n[3] = {};           // doubles, even
+  double* s[2] = {};
+  int64_t sn[2] = {};          // doubles, even
 };
 
 struct ChainDev {
@@ -98,7 +101,6 @@ struct LoneLinDev {
   const int32_t* blk = nullptr;
   TypeDev t0;                             // PoseToPoint factor data (record offset -> factor id via base, stride)
   uint64_t off_W = 0, off_D = 0, off_gp = 0;
-  int pslot = 0;                          // partial slot of block 0 (linear error at delta = 0)
 };
 
 // reduced system in 64x64 tiles; tile (row tile i, column tile j) with
@@ -131,7 +133,13 @@ struct TileSchedDev {
   int workers = 256;           // its workgroups (one per CU)
   int wide_updates = 256;      // levels with more update tasks use the side-stream kernel
   bool level_backward = false; // force one backward launch per level
+  // one-launch backward: hand-offs on the data (k_back_poll; x and partials
+  // sentinel-filled before each solve) instead of epoch flags (k_back_persist)
+  bool back_poll = true;
 };
+
+// the sentinel k_back_poll's consumers wait past (a signalling NaN)
+constexpr uint64_t kBackSentinel = 0xFFF4DEADBEEFCAFEull;
 
 // ---- launchers (all asynchronous on `s`) ----
 // Factor kernels, one launch per type group. Partials are laid out in type
@@ -139,16 +147,13 @@ struct TileSchedDev {
 // all partials into *out (counter: a zeroed device word, left zeroed);
 // launch_linearize's sum is the linear error at delta = 0.
 int error_blocks(const TypeDev* td);
-// n_pre: partial slots [linearize_blocks(td), + n_pre) were written by an
-// earlier launch (k_lone_lin) and join the sum
-int linearize_blocks(const TypeDev* td);
-void launch_linearize(const TypeDev* td, const double* pose, const double* pt, double* arena, double* partials,
-                      unsigned* counter, double* out, hipStream_t s, int n_pre = 0);
-// fused static-landmark linearisation: W, D, g_p of the grouped lone points,
-// the groups' H areas, and partials[pslot + g] (before launch_linearize)
-// (-1 without launching when a table pointer is null)
-int launch_lone_lin(const LoneLinDev& d, const double* pose, const double* pt, double* arena, double* partials,
-                    hipStream_t s);
+// lone (optional): the fused static landmarks' group blocks (W, D, g_p of
+// the grouped lone points, the groups' H areas) run as the first workgroups
+// of the PoseToPoint launch, their linear error joining the sum. Returns -1
+// without launching when lone's tables are null.
+int linearize_blocks(const TypeDev* td, const LoneLinDev* lone = nullptr);
+int launch_linearize(const TypeDev* td, const double* pose, const double* pt, double* arena, double* partials,
+                     unsigned* counter, double* out, hipStream_t s, const LoneLinDev* lone = nullptr);
 // fail_src (optional): accumulated failure bits, moved to *fail_dst and cleared
 // extra_* (optional): the finishing block also sums extra_in[0, extra_n) in
 // order into *extra_out (the back-substitution's cost-change partials)

@@ -567,8 +567,7 @@ int upload_plan(dynohip_solver* s, bool types_done = false) {
   ll.off_W = P.off_W;
   ll.off_D = P.off_D;
   ll.off_gp = P.off_gp;
-  ll.pslot = linearize_blocks(s->td_lin);
-  slots = std::max(1, std::max(error_blocks(s->td), ll.pslot + ll.n_group));
+  slots = std::max(1, std::max(error_blocks(s->td), linearize_blocks(s->td_lin, &ll)));
   s->partial_slots = slots;
   HIPCHK(s, s->partials.alloc(2ull * slots));
   HIPCHK(s, s->result.alloc(8));
@@ -821,9 +820,8 @@ int enqueue_linearize(dynohip_solver* s, const double* pose, const double* pt, d
                           s->gW.dev(P.gW.ntargets())};
   double* const dst[4] = {A + P.off_D, A + P.off_E, A + P.off_gp, A + P.off_W};
   if (fused_lone(s) && !all_records) {
-    if (launch_lone_lin(s->lld, pose, pt, A, s->partials.p, s->stream))
+    if (launch_linearize(s->td_lin, pose, pt, A, s->partials.p, s->sumctr.p, lin0, s->stream, &s->lld))
       return set_err(s, DYNOHIP_EHIP, "internal: fused static-landmark linearisation without its tables");
-    launch_linearize(s->td_lin, pose, pt, A, s->partials.p, s->sumctr.p, lin0, s->stream, s->lld.n_group);
     launch_gather_point(g, dst, A, s->stream);
     return 0;
   }
@@ -850,6 +848,12 @@ int enqueue_try(dynohip_solver* s, double lambda) {
   z.n[1] = static_cast<int64_t>(nrp);
   z.p[2] = reinterpret_cast<double*>(s->fsync.p);
   z.n[2] = static_cast<int64_t>(s->fsync.n) / 2;
+  if (s->sd.back_poll) {   // k_back_poll's hand-off buffers
+    z.s[0] = s->xy.p + nrp;
+    z.sn[0] = static_cast<int64_t>(nrp);
+    z.s[1] = s->bpartials.p;
+    z.sn[1] = static_cast<int64_t>(P.n_partials) * kTile;
+  }
   launch_chain_factor(s->cd, A, lambda, s->failp, z, st);
   launch_chain_solve_y(s->cd, A, st);
   s->ld.fused = fused_lone(s) ? 1 : 0;
@@ -1206,6 +1210,7 @@ int dynohip_create(int device_id, dynohip_solver** out) {
   s->device = device_id;
   if (const char* e = std::getenv("DYNOHIP_LINERR_DIRECT")) s->linerr_direct = std::atoi(e) != 0;
   if (const char* e = std::getenv("DYNOHIP_FUSED_LONE")) s->fused_env = std::atoi(e) != 0;
+  if (const char* e = std::getenv("DYNOHIP_BACK_POLL")) s->sd.back_poll = std::atoi(e) != 0;
   s->stream = r.stream;
   s->side = r.side;
   s->ev_main = r.ev_main;

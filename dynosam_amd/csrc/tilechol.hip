@@ -1240,6 +1240,135 @@ __global__ __launch_bounds__(kBackThreads) void k_back_persist(TileDev b, const 
   }
 }
 
+// The backward substitution in one launch with the hand-offs on the data
+// itself (the default; k_back_persist above is the flag form). Before each
+// solve the solution x and the part partials are filled with kBackSent, a
+// signalling-NaN pattern that no arithmetic produces (an FP64 operation
+// returns quiet NaNs), so a consumer knows a value is this solve's by seeing
+// anything else. Per level that is one memory round trip instead of the
+// flag form's drain, flag poll and then payload load, and a column split
+// into parts needs no arrival counter:
+//   * a part polls the x rows of its entries (sc1 loads, each lane its own
+//     element) with its L tiles and L_kk^-1 fetched before;
+//   * a column of one part solves x_k at once;
+//   * otherwise parts 1.. store their partial sums and leave, and part 0
+//     polls them and adds them in part order (the same order and operations
+//     as the counter form: the results are bit-identical), then solves x_k.
+// Every part is resident (the same kBackPersistMax bound), so each wait is
+// for a running workgroup. A wait that times out (~2^22 polls) sets bit 1 of
+// *fail and the part stores a quiet NaN instead, so the chain drains quickly
+// and the step is rejected.
+constexpr uint64_t kBackSent = 0xFFF4DEADBEEFCAFEull;
+__device__ __forceinline__ bool back_sent(double v) { return __builtin_bit_cast(uint64_t, v) == kBackSent; }
+// an sc1 load of *p repeated until it is not the sentinel (false on timeout)
+__device__ __forceinline__ bool poll_value(const double* p, double& v) {
+  v = ld_sc1(p);
+  int spins = 0;
+  while (back_sent(v)) {
+    if (++spins > kSpinLimit) return false;
+    __builtin_amdgcn_s_sleep(1);
+    v = ld_sc1(p);
+  }
+  return true;
+}
+
+__global__ __launch_bounds__(kBackThreads) void k_back_poll(TileDev b, const BackPart* __restrict__ parts,
+                                                            const int32_t* __restrict__ ent,
+                                                            const double* __restrict__ Linv,
+                                                            const double* __restrict__ y, double* x,
+                                                            double* partials, int* fail) {
+  constexpr int NP = kBackThreads / T;
+  constexpr int CH = DYNOHIP_BACK_CH;
+  __shared__ double part[NP][T];
+  __shared__ double rv[T];
+  __shared__ double xs[CH][T];
+  const BackPart pt = parts[blockIdx.x];
+  const int tid = threadIdx.x, c = tid & (T - 1), q = tid >> 6;
+  const int ne = pt.end - pt.beg;
+  int bad = 0;   // this thread's waits timed out
+  // (1) what does not depend on other columns
+  double lv[CH][16];
+#pragma unroll
+  for (int j = 0; j < CH; ++j)
+    if (j < ne) {
+      const double* L = slot_ptr(b, ent[2 * (pt.beg + j)]);
+#pragma unroll
+      for (int m = 0; m < 16; ++m) lv[j][m] = L[(q + NP * m) * T + c];
+    }
+  const bool solver = pt.nparts == 1 || pt.part == 0;
+  double li[16];
+  if (solver) {
+    const double* Li = Linv + static_cast<int64_t>(pt.k) * T * T;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) li[m] = Li[(q + NP * m) * T + c];
+  }
+  const double yk = (solver && tid < T) ? y[static_cast<int64_t>(pt.k) * T + tid] : 0.0;
+  // (2) the x rows of the entries, chunk by chunk, each element polled
+  double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int j0 = 0; j0 < ne; j0 += CH) {
+    if (j0 > 0) {
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < CH; ++j)
+        if (j0 + j < ne) {
+          const double* L = slot_ptr(b, ent[2 * (pt.beg + j0 + j)]);
+#pragma unroll
+          for (int m = 0; m < 16; ++m) lv[j][m] = L[(q + NP * m) * T + c];
+        }
+    }
+    if (tid < min(CH, ne - j0) * T) {
+      double v;
+      if (!poll_value(x + static_cast<int64_t>(ent[2 * (pt.beg + j0 + (tid >> 6)) + 1]) * T + c, v)) bad = 1;
+      xs[tid >> 6][c] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < CH; ++j)
+      if (j0 + j < ne) {
+#pragma unroll
+        for (int m = 0; m < 16; ++m) s[m & 7] += lv[j][m] * xs[j][q + NP * m];
+      }
+  }
+  part[q][c] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  __syncthreads();
+  double sum = 0.0;
+  if (tid < T) sum = (part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]);
+  if (pt.nparts > 1) {
+    if (!solver) {
+      // hand the partial to part 0 (a quiet NaN after a timed-out wait)
+      bad = __syncthreads_or(bad);
+      if (tid < T) st_sc1(partials + static_cast<int64_t>(pt.pbase + pt.part) * T + tid, bad ? __builtin_nan("") : sum);
+      if (tid == 0 && bad) atomicOr(fail, 2);
+      return;
+    }
+    if (tid < T) {
+      const double own = sum;
+      sum = 0.0;
+      for (int p = 0; p < pt.nparts; ++p) {
+        double v = own;
+        if (p > 0 && !poll_value(partials + static_cast<int64_t>(pt.pbase + p) * T + tid, v)) bad = 1;
+        sum += v;
+      }
+    }
+  }
+  if (tid < T) rv[tid] = yk - sum;
+  __syncthreads();
+  // x_k[c] = sum_{m >= c} Linv[m][c] rv[m]
+  double t = 0.0;
+#pragma unroll
+  for (int m = 0; m < 16; ++m) {
+    const int row = q + NP * m;
+    if (row >= c) t += li[m] * rv[row];
+  }
+  part[q][c] = t;
+  bad = __syncthreads_or(bad);
+  if (tid < T) {
+    const double xv = (part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]);
+    st_sc1(x + static_cast<int64_t>(pt.k) * T + tid, bad ? __builtin_nan("") : xv);
+  }
+  if (tid == 0 && bad) atomicOr(fail, 2);
+}
+
 }  // namespace
 
 #ifdef DYNOHIP_TASK_CLOCK
@@ -1281,8 +1410,11 @@ void launch_tile_backward(const TileDev& b, const TileSchedDev& sd, const std::v
                           const double* Linv, const double* y, double* x, int* fail, hipStream_t s) {
   const int nparts = blevel.empty() ? 0 : blevel.back();
   if (nparts > 0 && nparts <= kBackPersistMax && !sd.level_backward) {
-    k_back_persist<<<nparts, kBackThreads, 0, s>>>(b, sd.bpart, sd.bent, Linv, y, x, sd.partials, sd.arrive, sd.done,
-                                                   sd.epoch, fail);
+    if (sd.back_poll)   // x and the partials hold the sentinel (k_chain_factor's fill)
+      k_back_poll<<<nparts, kBackThreads, 0, s>>>(b, sd.bpart, sd.bent, Linv, y, x, sd.partials, fail);
+    else
+      k_back_persist<<<nparts, kBackThreads, 0, s>>>(b, sd.bpart, sd.bent, Linv, y, x, sd.partials, sd.arrive,
+                                                     sd.done, sd.epoch, fail);
     return;
   }
   for (size_t lv = 0; lv + 1 < blevel.size(); ++lv) {

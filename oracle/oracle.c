@@ -497,6 +497,10 @@ struct oracle_problem {
   factor_t* f;
   size_t nft[F_NT];
   int dense;
+  /* control (oracle_set_reverse_sums): the Schur solve accumulates the
+     factors and eliminates the point components in reverse order, which
+     changes only the rounding of the reduced system */
+  int reverse_sums;
   char err[256];
   /* structure for the Schur solve */
   int* comp_of;        /* per variable: component id (points) or -1 */
@@ -540,6 +544,7 @@ static void set_err(oracle_problem* p, const char* fmt, ...) {
 }
 const char* oracle_last_error(const oracle_problem* p) { return p ? p->err : "null"; }
 void oracle_set_dense(oracle_problem* p, int dense) { p->dense = dense; }
+void oracle_set_reverse_sums(oracle_problem* p, int reverse) { p->reverse_sums = reverse; }
 
 static int cmp_keyidx(const void* a, const void* b) {
   const keyidx_t* x = (const keyidx_t*)a;
@@ -1073,7 +1078,8 @@ static int solve_schur(oracle_problem* p, double lambda, double* delta, const si
     for (int k = 0; k < C->npts; ++k) local[C->pts[k]] = k;
   }
   /* accumulate normal-equation blocks */
-  for (size_t f = 0; f < p->nf; ++f) {
+  for (size_t f0 = 0; f0 < p->nf; ++f0) {
+    const size_t f = p->reverse_sums ? p->nf - 1 - f0 : f0;
     const factor_t* F = &p->f[f];
     const int d = kDim[F->type], cols = oracle_factor_cols(F->type), nk = kNKeys[F->type];
     const double* A = p->A + p->foffA[f];
@@ -1122,7 +1128,8 @@ static int solve_schur(oracle_problem* p, double lambda, double* delta, const si
   free(local);
   for (size_t i = 0; i < nd; ++i) *sky_at(p, i, i) += lambda;
   /* eliminate point components */
-  for (int c = 0; c < p->ncomp; ++c) {
+  for (int c0 = 0; c0 < p->ncomp; ++c0) {
+    const int c = p->reverse_sums ? p->ncomp - 1 - c0 : c0;
     comp_t* C = &p->comps[c];
     const size_t n3 = 3 * (size_t)C->npts, m6 = 6 * (size_t)C->nnb;
     for (size_t i = 0; i < n3; ++i) C->C[i * n3 + i] += lambda;
@@ -1208,8 +1215,193 @@ static size_t make_doff(const oracle_problem* p, size_t* doff) {
 static int solve_schur_mt(oracle_problem* p, double lambda, double* delta, const size_t* doff);
 static int solve_system(oracle_problem* p, double lambda, double* delta, const size_t* doff, size_t N) {
   if (p->dense) return solve_dense(p, lambda, delta, doff, N);
-  if (p->nthreads > 1) return solve_schur_mt(p, lambda, delta, doff);
+  if (p->nthreads > 1 && !p->reverse_sums) return solve_schur_mt(p, lambda, delta, doff);
   return solve_schur(p, lambda, delta, doff);
+}
+
+/* The same Schur solve with every sum, product and factorisation of the
+   solve in x87 extended precision (64-bit significand, eps 5.4e-20): a
+   reference for the deep-convergence steps, whose reduced systems are
+   conditioned beyond 1/eps of double. The linearisation is
+   the double one (the records), only the solve is extended. Serial. */
+typedef long double ldbl;
+static int chol_dense_ld(ldbl* A, size_t n) {
+  for (size_t j = 0; j < n; ++j) {
+    ldbl d = A[j * n + j];
+    for (size_t k = 0; k < j; ++k) d -= A[j * n + k] * A[j * n + k];
+    if (!(d > 0.0L)) return 0;
+    const ldbl ljj = sqrtl(d);
+    A[j * n + j] = ljj;
+    for (size_t i = j + 1; i < n; ++i) {
+      ldbl s = A[i * n + j];
+      for (size_t k = 0; k < j; ++k) s -= A[i * n + k] * A[j * n + k];
+      A[i * n + j] = s / ljj;
+    }
+  }
+  return 1;
+}
+static void chol_solve_ld(const ldbl* L, size_t n, ldbl* B, size_t nrhs) {
+  for (size_t c = 0; c < nrhs; ++c) {
+    for (size_t i = 0; i < n; ++i) {
+      ldbl s = B[i * nrhs + c];
+      for (size_t k = 0; k < i; ++k) s -= L[i * n + k] * B[k * nrhs + c];
+      B[i * nrhs + c] = s / L[i * n + i];
+    }
+    for (size_t ii = n; ii-- > 0;) {
+      ldbl s = B[ii * nrhs + c];
+      for (size_t k = ii + 1; k < n; ++k) s -= L[k * n + ii] * B[k * nrhs + c];
+      B[ii * nrhs + c] = s / L[ii * n + ii];
+    }
+  }
+}
+static int solve_schur_ld(oracle_problem* p, double lambda, double* delta, const size_t* doff) {
+  const size_t nd = p->ndim_red, nsky = p->rowoff[nd];
+  ldbl* sky = (ldbl*)calloc(nsky ? nsky : 1, sizeof(ldbl));
+  ldbl* gc = (ldbl*)calloc(nd ? nd : 1, sizeof(ldbl));
+  ldbl** cC = (ldbl**)calloc((size_t)p->ncomp + 1, sizeof(ldbl*));
+  ldbl** cW = (ldbl**)calloc((size_t)p->ncomp + 1, sizeof(ldbl*));
+  ldbl** cg = (ldbl**)calloc((size_t)p->ncomp + 1, sizeof(ldbl*));
+  int* local = (int*)malloc((p->nvars ? p->nvars : 1) * sizeof(int));
+  int ok = 1;
+#define SKY(i, j) sky[p->rowoff[i] + ((j) - p->first[i])]
+  for (int c = 0; c < p->ncomp; ++c) {
+    comp_t* C = &p->comps[c];
+    const size_t n3 = 3 * (size_t)C->npts, m6 = 6 * (size_t)C->nnb;
+    cC[c] = (ldbl*)calloc(n3 * n3 + 1, sizeof(ldbl));
+    cW[c] = (ldbl*)calloc(n3 * m6 + 1, sizeof(ldbl));
+    cg[c] = (ldbl*)calloc(n3 + 1, sizeof(ldbl));
+    for (int k = 0; k < C->npts; ++k) local[C->pts[k]] = k;
+  }
+  for (size_t f = 0; f < p->nf; ++f) {
+    const factor_t* F = &p->f[f];
+    const int d = kDim[F->type], cols = oracle_factor_cols(F->type), nk = kNKeys[F->type];
+    const double* A = p->A + p->foffA[f];
+    const double* b = p->b + p->foffb[f];
+    int comp = -1;
+    for (int sl = 0; sl < nk; ++sl)
+      if (kSlotKind[F->type][sl] == 1) comp = p->comp_of[F->var[sl]];
+    comp_t* C = comp >= 0 ? &p->comps[comp] : NULL;
+    if (C)
+      for (int k = 0; k < C->nnb; ++k) p->nb_local[C->nb[k]] = k;
+    int c0 = 0;
+    for (int sa = 0; sa < nk; ++sa) {
+      const int da = slot_dim(F->type, sa), va = F->var[sa], pa = kSlotKind[F->type][sa] == 1;
+      for (int ia = 0; ia < da; ++ia) {
+        ldbl sg = 0.0L;
+        for (int r = 0; r < d; ++r) sg += (ldbl)A[r * cols + c0 + ia] * (ldbl)b[r];
+        if (pa) cg[comp][3 * local[va] + ia] += sg;
+        else gc[6 * (size_t)p->red_of[va] + ia] += sg;
+      }
+      int c1 = 0;
+      for (int sb = 0; sb < nk; ++sb) {
+        const int db = slot_dim(F->type, sb), vb = F->var[sb], pb = kSlotKind[F->type][sb] == 1;
+        for (int ia = 0; ia < da; ++ia)
+          for (int ib = 0; ib < db; ++ib) {
+            ldbl t = 0.0L;
+            for (int r = 0; r < d; ++r) t += (ldbl)A[r * cols + c0 + ia] * (ldbl)A[r * cols + c1 + ib];
+            if (pa && pb) {
+              cC[comp][(3 * (size_t)local[va] + ia) * (3 * (size_t)C->npts) + 3 * (size_t)local[vb] + ib] += t;
+            } else if (pa && !pb) {
+              cW[comp][(3 * (size_t)local[va] + ia) * (6 * (size_t)C->nnb) + 6 * (size_t)p->nb_local[p->red_of[vb]] + ib] += t;
+            } else if (!pa && !pb) {
+              const size_t gi = 6 * (size_t)p->red_of[va] + ia, gj = 6 * (size_t)p->red_of[vb] + ib;
+              if (gi >= gj) SKY(gi, gj) += t;
+            }
+          }
+        c1 += db;
+      }
+      c0 += da;
+    }
+  }
+  for (size_t i = 0; i < nd; ++i) SKY(i, i) += (ldbl)lambda;
+  ldbl** cY = (ldbl**)calloc((size_t)p->ncomp + 1, sizeof(ldbl*));
+  for (int c = 0; c < p->ncomp && ok; ++c) {
+    comp_t* C = &p->comps[c];
+    const size_t n3 = 3 * (size_t)C->npts, m6 = 6 * (size_t)C->nnb;
+    for (size_t i = 0; i < n3; ++i) cC[c][i * n3 + i] += (ldbl)lambda;
+    if (!chol_dense_ld(cC[c], n3)) { ok = 0; break; }
+    cY[c] = (ldbl*)malloc((n3 * m6 + 1) * sizeof(ldbl));
+    memcpy(cY[c], cW[c], n3 * m6 * sizeof(ldbl));
+    chol_solve_ld(cC[c], n3, cY[c], m6);
+    ldbl* v = (ldbl*)malloc((n3 + 1) * sizeof(ldbl));
+    memcpy(v, cg[c], n3 * sizeof(ldbl));
+    chol_solve_ld(cC[c], n3, v, 1);
+    for (int a = 0; a < C->nnb; ++a)
+      for (int ia = 0; ia < 6; ++ia) {
+        const size_t gi = 6 * (size_t)C->nb[a] + ia;
+        ldbl sv = 0.0L;
+        for (size_t k = 0; k < n3; ++k) sv += cW[c][k * m6 + 6 * a + ia] * v[k];
+        gc[gi] -= sv;
+        for (int bb = 0; bb <= a; ++bb)
+          for (int ib = 0; ib < 6; ++ib) {
+            const size_t gj = 6 * (size_t)C->nb[bb] + ib;
+            if (gj > gi) continue;
+            ldbl t = 0.0L;
+            for (size_t k = 0; k < n3; ++k) t += cW[c][k * m6 + 6 * a + ia] * cY[c][k * m6 + 6 * bb + ib];
+            SKY(gi, gj) -= t;
+          }
+      }
+    free(v);
+  }
+  for (size_t i = 0; i < nd && ok; ++i) {
+    const size_t fi = p->first[i];
+    for (size_t j = fi; j <= i; ++j) {
+      const size_t fj = p->first[j], k0 = fi > fj ? fi : fj;
+      ldbl t = SKY(i, j);
+      for (size_t k = k0; k < j; ++k) t -= SKY(i, k) * SKY(j, k);
+      if (j == i) {
+        if (!(t > 0.0L)) { ok = 0; break; }
+        SKY(i, i) = sqrtl(t);
+      } else {
+        SKY(i, j) = t / SKY(j, j);
+      }
+    }
+  }
+  if (ok) {
+    ldbl* x = (ldbl*)malloc((nd ? nd : 1) * sizeof(ldbl));
+    for (size_t i = 0; i < nd; ++i) {
+      ldbl t = gc[i];
+      for (size_t k = p->first[i]; k < i; ++k) t -= SKY(i, k) * x[k];
+      x[i] = t / SKY(i, i);
+    }
+    for (size_t ii = nd; ii-- > 0;) {
+      x[ii] /= SKY(ii, ii);
+      const ldbl xi = x[ii];
+      for (size_t k = p->first[ii]; k < ii; ++k) x[k] -= SKY(ii, k) * xi;
+    }
+    for (int r = 0; r < p->npose; ++r)
+      for (int k = 0; k < 6; ++k) delta[doff[p->pose_var[r]] + k] = (double)x[6 * (size_t)r + k];
+    for (int c = 0; c < p->ncomp; ++c) {
+      comp_t* C = &p->comps[c];
+      const size_t n3 = 3 * (size_t)C->npts, m6 = 6 * (size_t)C->nnb;
+      ldbl* rhs = (ldbl*)malloc((n3 + 1) * sizeof(ldbl));
+      for (size_t k = 0; k < n3; ++k) {
+        ldbl t = cg[c][k];
+        for (int a = 0; a < C->nnb; ++a)
+          for (int ia = 0; ia < 6; ++ia) t -= cW[c][k * m6 + 6 * a + ia] * x[6 * (size_t)C->nb[a] + ia];
+        rhs[k] = t;
+      }
+      chol_solve_ld(cC[c], n3, rhs, 1);
+      for (int k = 0; k < C->npts; ++k)
+        for (int j = 0; j < 3; ++j) delta[doff[C->pts[k]] + j] = (double)rhs[3 * k + j];
+      free(rhs);
+    }
+    free(x);
+  }
+#undef SKY
+  for (int c = 0; c < p->ncomp; ++c) { free(cC[c]); free(cW[c]); free(cg[c]); free(cY[c]); }
+  free(cC); free(cW); free(cg); free(cY); free(local); free(sky); free(gc);
+  return ok;
+}
+
+int oracle_solve_damped_ld(oracle_problem* p, double lambda, double* delta_out, size_t n_doubles) {
+  size_t* doff = (size_t*)malloc((p->nvars ? p->nvars : 1) * sizeof(size_t));
+  size_t N = make_doff(p, doff);
+  if (n_doubles < N) { free(doff); return DYNOHIP_EINVAL; }
+  linearize_all(p);
+  int ok = solve_schur_ld(p, lambda, delta_out, doff);
+  free(doff);
+  return ok;
 }
 
 int oracle_solve_damped(oracle_problem* p, double lambda, double* delta_out, size_t n_doubles) {

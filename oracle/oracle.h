@@ -48,6 +48,9 @@ void oracle_destroy(oracle_problem* p);
 const char* oracle_last_error(const oracle_problem* p);
 /* 0 = Schur + skyline (default), 1 = dense full-system Cholesky */
 void oracle_set_dense(oracle_problem* p, int dense);
+/* rounding control: the Schur solve sums factors and point components in
+   reverse order (serial solve); the same mathematics, other rounding */
+void oracle_set_reverse_sums(oracle_problem* p, int reverse);
 /* threads of the Schur + skyline LM (default 1); the trajectory is
    bit-identical for every thread count (the all-cores CPU baseline) */
 int oracle_set_threads(oracle_problem* p, int nthreads);
@@ -69,6 +72,9 @@ int oracle_linearize(oracle_problem* p, double* out, size_t n_doubles);
    returns 1 if solved, 0 if indefinite, <0 on error */
 int oracle_solve_damped(oracle_problem* p, double lambda, double* delta_out,
                         size_t n_doubles);
+/* the same step with the Schur solve in x87 extended precision (a reference
+   for ill-conditioned deep-convergence systems); 1 = solved */
+int oracle_solve_damped_ld(oracle_problem* p, double lambda, double* delta_out, size_t n_doubles);
 
 /* factor-level hooks: type as in dynohip_graph_view order (0..5).
    vars: the factor's variable values in key order (12 per pose, 3 per

@@ -29,6 +29,8 @@ def lib():
         L.oracle_last_error.argtypes = [vp]
         L.oracle_last_error.restype = C.c_char_p
         L.oracle_set_dense.argtypes = [vp, C.c_int]
+        L.oracle_set_reverse_sums.argtypes = [vp, C.c_int]
+        L.oracle_set_reverse_sums.restype = None
         L.oracle_set_threads.argtypes = [vp, C.c_int]
         L.oracle_set_threads.restype = C.c_int
         L.oracle_error.argtypes = [vp]
@@ -43,6 +45,7 @@ def lib():
         L.oracle_linearize_size.restype = C.c_size_t
         L.oracle_linearize.argtypes = [vp, P(C.c_double), C.c_size_t]
         L.oracle_solve_damped.argtypes = [vp, C.c_double, P(C.c_double), C.c_size_t]
+        L.oracle_solve_damped_ld.argtypes = [vp, C.c_double, P(C.c_double), C.c_size_t]
         L.oracle_eval_factor.argtypes = [C.c_int, P(C.c_double), P(C.c_double), P(C.c_double), P(C.c_double)]
         for fn in ("oracle_factor_dim", "oracle_factor_cols", "oracle_factor_nkeys"):
             getattr(L, fn).argtypes = [C.c_int]
@@ -70,7 +73,7 @@ def dptr(a):
 class Oracle:
     """CPU restatement of LevenbergMarquardtOptimizer(graph, values).optimize()."""
 
-    def __init__(self, graph, values, dense=False, threads=1):
+    def __init__(self, graph, values, dense=False, threads=1, reverse_sums=False):
         L = lib()
         self.graph = graph
         self.values = values
@@ -87,6 +90,8 @@ class Oracle:
             self.h = None
             raise ValueError(f"oracle_create: {rc} {msg}")
         L.oracle_set_dense(self.h, 1 if dense else 0)
+        if reverse_sums:
+            L.oracle_set_reverse_sums(self.h, 1)
         if threads > 1:
             L.oracle_set_threads(self.h, int(threads))
         self.ndata = data.shape[0]
@@ -140,6 +145,14 @@ class Oracle:
         n = int((np.where(self.values.kinds == _abi.POSE3, 6, 3)).sum())
         out = np.zeros(n)
         ok = lib().oracle_solve_damped(self.h, lam, dptr(out), n)
+        return ok, out
+
+    def solve_damped_ld(self, lam):
+        """the same step with the Schur solve in extended precision (a
+        reference for ill-conditioned systems)"""
+        n = int((np.where(self.values.kinds == _abi.POSE3, 6, 3)).sum())
+        out = np.zeros(n)
+        ok = lib().oracle_solve_damped_ld(self.h, lam, dptr(out), n)
         return ok, out
 
 
