@@ -32,12 +32,14 @@ if gpu:
     s = Solver(0)
     s.set_graph(g)
     s.set_values(v)
-vals = v.__class__ if False else None
 p = _abi.LMParams.gtsam_default()
 lam = 1e-5
 o.reset(p)
 for it in range(iters):
-    data = o.values_data()
+    # the run follows the GPU's iterates when it is there (as the
+    # conditioned parity test does), else the oracle's
+    data = s.values_data() if s is not None else o.values_data()
+    o.set_values_data(data)
     r.set_values_data(data)
     vn = np.linalg.norm(data)
     ok_l, dl = o.solve_damped_ld(lam)
@@ -48,13 +50,15 @@ for it in range(iters):
         line.append(f"{tag} {np.linalg.norm(d - dl) / vn:.2e} ({np.linalg.norm(d - dl) / np.linalg.norm(dl):.1e})"
                     if ok and ok_l else f"{tag} fail")
     if s is not None:
-        s.set_values_data(data)
-        ok_g, dg = s.solve_delta(lam)
+        ok_g, dg = s.solve_delta(lam)   # the GPU is on `data` (it drives the run)
         line.append(f"gpu {np.linalg.norm(dg - dl) / vn:.2e} ({np.linalg.norm(dg - dl) / np.linalg.norm(dl):.1e})"
                     if ok_g and ok_l else "gpu fail")
         line.append(f"gpu-oracle {np.linalg.norm(dg - do) / vn:.2e}")
     print("  ".join(line), flush=True)
     p.lambda_initial = lam
-    o.reset(p)
-    so = o.iterate()
-    lam = so.final_lambda
+    if s is not None:
+        s.reset(p)
+        lam = s.iterate().final_lambda
+    else:
+        o.reset(p)
+        lam = o.iterate().final_lambda
