@@ -293,12 +293,9 @@ __device__ __forceinline__ void factor_vars(const TypeDev& tp, int i, const doub
 // (the fused static landmarks) consumes them in registers. Both get the same
 // bits.
 template <int T>
-__device__ __forceinline__ double eval_whitened(const TypeDev& tp, int i, const double* __restrict__ pose,
-                                                const double* __restrict__ pt, double (&Jw)[kDim[T] * kCols[T]],
-                                                double (&bw)[kDim[T]]) {
+__device__ __forceinline__ double eval_whitened_v(const TypeDev& tp, int i, const double* const (&v)[4],
+                                                  double (&Jw)[kDim[T] * kCols[T]], double (&bw)[kDim[T]]) {
   constexpr int d = kDim[T], cols = kCols[T];
-  const double* v[4];
-  factor_vars<T>(tp, i, pose, pt, v);
   const double* meas = kMeasDim[T] ? tp.meas + static_cast<int64_t>(i) * kMeasDim[T] : nullptr;
   double r[6];
   evaluate<T>(v, meas, r, Jw);
@@ -335,6 +332,15 @@ __device__ __forceinline__ double eval_whitened(const TypeDev& tp, int i, const 
     e += rk * rk;
   }
   return e * 0.5;
+}
+
+template <int T>
+__device__ __forceinline__ double eval_whitened(const TypeDev& tp, int i, const double* __restrict__ pose,
+                                                const double* __restrict__ pt, double (&Jw)[kDim[T] * kCols[T]],
+                                                double (&bw)[kDim[T]]) {
+  const double* v[4];
+  factor_vars<T>(tp, i, pose, pt, v);
+  return eval_whitened_v<T>(tp, i, v, Jw, bw);
 }
 
 template <int T>
@@ -443,7 +449,7 @@ constexpr int kLoneJ = 21;                            // staged per (point, a): 
 __device__ double lone_lin_block(const LoneLinDev& d, int gb, const double* __restrict__ pose,
                                  const double* __restrict__ pt, double* __restrict__ arena) {
   __shared__ int32_t hdr[kLoneBlk];
-  __shared__ double sJ[kLoneSub * kLoneMaxNb * kLoneJ];
+  __shared__ double sJ[256 * kLoneJ];   // a (point, neighbour) per lane: npt m <= 256
   const int tid = threadIdx.x;
   for (int q = tid; q < kLoneBlk; q += kBlock) hdr[q] = d.blk[static_cast<int64_t>(gb) * kLoneBlk + q];
   __syncthreads();
@@ -456,10 +462,12 @@ __device__ double lone_lin_block(const LoneLinDev& d, int gb, const double* __re
   for (int k = 0; k < 9; ++k) Dp[k] = 0.0;
   gp[0] = gp[1] = gp[2] = 0.0;
   if (valid) {
-    const uint32_t rec = static_cast<uint32_t>(hdr[4 + 2 * kLoneSub + m * u + a]);
+    const uint32_t rec = static_cast<uint32_t>(hdr[kLoneHdrRec + m * u + a]);
     const int f = static_cast<int>((rec - d.t0.base) / kRec0);
+    // the pose and the point from the header (no dependent index load)
+    const double* const v[4] = {pose + 12ll * hdr[kLoneHdrPose + a], pt + 3ll * hdr[kLoneHdrPt + u], nullptr, nullptr};
     double J[kDim[0] * kCols[0]], bb[3];
-    e = eval_whitened<0>(d.t0, f, pose, pt, J, bb);
+    e = eval_whitened_v<0>(d.t0, f, v, J, bb);
     // the record's blocks: J_x (3x6) and J_p (3x3), row-major
     double Jx[18], Jp[9];
 #pragma unroll
@@ -469,7 +477,7 @@ __device__ double lone_lin_block(const LoneLinDev& d, int gb, const double* __re
 #pragma unroll
       for (int c = 0; c < 3; ++c) Jp[3 * k + c] = J[kCols[0] * k + 6 + c];
     }
-    double* W = arena + d.off_W + 18ll * (hdr[4 + kLoneSub + u] + a);
+    double* W = arena + d.off_W + 18ll * (hdr[kLoneHdrE0 + u] + a);
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
 #pragma unroll
@@ -497,7 +505,7 @@ __device__ double lone_lin_block(const LoneLinDev& d, int gb, const double* __re
     for (int k = 0; k < 3; ++k) gs[k] += __shfl(gp[k], src);
   }
   if (valid && a == 0) {
-    const int p = hdr[4 + u];
+    const int p = hdr[kLoneHdrPt + u];
     double* D = arena + d.off_D + 9ll * p;
 #pragma unroll
     for (int k = 0; k < 9; ++k) D[k] = Ds[k];
@@ -837,7 +845,7 @@ __device__ __forceinline__ void gather_thread(const GatherDev& g, int blk, const
 // b, 30 contiguous doubles), writes W_a = J_p^T J_x, and the m lanes of a
 // point (consecutive, floor(64 / m) points per wave) sum J_p^T J_p and
 // J_p^T b into D and g_p in neighbour order (deterministic).
-static_assert(4 * (64 / kLoneMaxNb) >= kLoneSub, "a group block's points fit the workgroup's waves");
+// (plan.cpp caps a block at lone_cap(m) <= 4 floor(64 / m) points)
 __device__ __forceinline__ void lone_point_block(const PointGatherDev& pg, int g, const double* __restrict__ arena) {
   const int32_t* blk = pg.lone_blk + static_cast<int64_t>(g) * kLoneBlk;
   const int m = blk[0], npt = blk[1];
@@ -849,7 +857,7 @@ __device__ __forceinline__ void lone_point_block(const PointGatherDev& pg, int g
   for (int k = 0; k < 9; ++k) Dp[k] = 0.0;
   gp[0] = gp[1] = gp[2] = 0.0;
   if (valid) {
-    const double* R = arena + static_cast<uint32_t>(blk[4 + 2 * kLoneSub + m * u + a]);
+    const double* R = arena + static_cast<uint32_t>(blk[kLoneHdrRec + m * u + a]);
     double Jx[18], Jp[9], bb[3];
 #pragma unroll
     for (int k = 0; k < 18; ++k) Jx[k] = R[k];
@@ -857,7 +865,7 @@ __device__ __forceinline__ void lone_point_block(const PointGatherDev& pg, int g
     for (int k = 0; k < 9; ++k) Jp[k] = R[18 + k];
 #pragma unroll
     for (int k = 0; k < 3; ++k) bb[k] = R[27 + k];
-    double* W = pg.dst[3] + 18ll * (blk[4 + kLoneSub + u] + a);
+    double* W = pg.dst[3] + 18ll * (blk[kLoneHdrE0 + u] + a);
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
 #pragma unroll
@@ -880,7 +888,7 @@ __device__ __forceinline__ void lone_point_block(const PointGatherDev& pg, int g
     for (int k = 0; k < 3; ++k) gs[k] += __shfl(gp[k], src);
   }
   if (valid && a == 0) {
-    const int pt = blk[4 + u];
+    const int pt = blk[kLoneHdrPt + u];
     double* D = pg.dst[0] + 9ll * pt;
 #pragma unroll
     for (int k = 0; k < 9; ++k) D[k] = Ds[k];
@@ -1485,10 +1493,21 @@ __global__ __launch_bounds__(kBlock) void k_chain_solve_y(ChainDev cd, double* _
 // row: row r of pair (a, b) (6 sums) or of gradient a. Sums run over the
 // points in member order (deterministic). Each point's data is read once
 // per solve, instead of once per reduced-block entry it feeds.
-constexpr int kLoneStage = (kLoneSub * 18 * kLoneMaxNb + kBlock - 1) / kBlock;   // W (and J) loads per thread
-static_assert(kLoneSub * 3 * kLoneMaxNb <= 2 * kBlock && 9 * kLoneSub <= kBlock, "lone staging of b, L");
+// a block holds npt m <= 256 (point, neighbour) pairs (plan.hpp lone_cap)
+constexpr int kLoneStage = 18 * 256 / kBlock;   // W (and J) loads per thread
+static_assert(3 * 256 <= 3 * kBlock && 9 * kLoneSub <= 2 * kBlock && 42 * kLoneMaxNb <= 2 * kBlock,
+              "lone staging of b, L and the H area");
 __host__ __device__ constexpr int lone_point_doubles(int m) { return 39 * m + 12; }  // Z, J, b, z, L
 __host__ __device__ constexpr int lone_point_doubles_fused(int m) { return 18 * m + 12; }  // Z, z, L
+// the staging LDS of the largest block of neighbour count <= max_m
+__host__ __device__ constexpr int lone_lds_doubles(int max_m, bool fused) {
+  int w = 0;
+  for (int m = 1; m <= max_m; ++m) {
+    const int x = lone_cap(m) * (fused ? lone_point_doubles_fused(m) : lone_point_doubles(m));
+    w = x > w ? x : w;
+  }
+  return w;
+}
 constexpr int kLoneNT = (6 * kLoneMaxNb + 15) / 16;                 // 16-column tiles of Z, at most
 constexpr int kLoneWT = (kLoneNT * (kLoneNT + 1) / 2 + 3) / 4;      // lower tiles per wave, at most
 static_assert(6 * kLoneMaxNb <= 64, "one lane per J_a^T J_a / gradient row");
@@ -1508,6 +1527,7 @@ __device__ unsigned long long g_lclk[8][8192];
   } while (0)
 #endif
 
+template <bool FUSED>
 __global__ __launch_bounds__(kBlock) void k_lone_schur(LoneSchurDev d, double* __restrict__ arena) {
   extern __shared__ double lds[];
   __shared__ int32_t hdr[kLoneBlk];
@@ -1518,68 +1538,76 @@ __global__ __launch_bounds__(kBlock) void k_lone_schur(LoneSchurDev d, double* _
   __syncthreads();
   LCLK(1);
   const int m = hdr[0], npt = hdr[1], m18 = 18 * m, np = m * (m + 1) / 2, ntask = 6 * np + 6 * m;
-  const int32_t* spt = hdr + 4;
-  const int32_t* se0 = hdr + 4 + kLoneSub;
-  const int32_t* srec = hdr + 4 + 2 * kLoneSub;
-  const bool fused = d.fused != 0;
+  const int32_t* spt = hdr + kLoneHdrPt;
+  const int32_t* se0 = hdr + kLoneHdrE0;
+  const int32_t* srec = hdr + kLoneHdrRec;
+  constexpr bool fused = FUSED;
+  const int cap = lone_cap(m);
   double* sZ = lds;                                  // [point][a][k][c]: W, then Z in place
-  double* sJ = sZ + kLoneSub * m18;                  // [point][a][k][c] (records; not fused)
-  double* sB = sJ + kLoneSub * m18;                  // [point][a][k]    (records; not fused)
-  double* sz = fused ? sJ : sB + kLoneSub * 3 * m;   // [point][k]: g_p, then z in place
-  double* sL = sz + 3 * kLoneSub;                    // [point][9]
+  double* sJ = sZ + cap * m18;                       // [point][a][k][c] (records; not fused)
+  double* sB = sJ + cap * m18;                       // [point][a][k]    (records; not fused)
+  double* sz = fused ? sJ : sB + cap * 3 * m;        // [point][k]: g_p, then z in place
+  double* sL = sz + 3 * cap;                         // [point][9]
   __shared__ double sJJ[36 * kLoneMaxNb];            // J_a^T J_a (fused: the H area's)
   __shared__ double sJb[6 * kLoneMaxNb];             // fused: J_a^T b
   const int nW = npt * m18, nB = npt * 3 * m;
   const uint32_t hsrc = static_cast<uint32_t>(hdr[2]) + 36u * np + 6u * m;   // the H area (k_lone_lin)
   {
-    double rw[kLoneStage], rj[kLoneStage], rb[2], rl = 0.0, rg = 0.0;
+    double rw[kLoneStage], rj[fused ? 1 : kLoneStage], rb[3], rl[2], rg = 0.0;
 #pragma unroll
     for (int u = 0; u < kLoneStage; ++u) {
       const int q = tid + kBlock * u;
-      rw[u] = rj[u] = 0.0;
+      rw[u] = 0.0;
+      if constexpr (!fused) rj[u] = 0.0;
       if (q < nW) {
         const int p = q / m18, pa = q / 18;
         rw[u] = arena[d.off_W + 18ll * se0[p] + (q - p * m18)];
-        if (!fused) rj[u] = arena[static_cast<uint32_t>(srec[pa]) + (q - 18 * pa)];
+        if constexpr (!fused) rj[u] = arena[static_cast<uint32_t>(srec[pa]) + (q - 18 * pa)];
       }
     }
-    if (fused) {
+    if constexpr (fused) {
       // the H area, 42 m doubles, in place of the J | b records
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < 3; ++u) {
         const int q = tid + kBlock * u;
         rb[u] = q < 42 * m ? arena[hsrc + q] : 0.0;
       }
     } else {
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < 3; ++u) {
         const int q = tid + kBlock * u, pa = q / 3;
         rb[u] = q < nB ? arena[static_cast<uint32_t>(srec[pa]) + 27 + (q - 3 * pa)] : 0.0;
       }
     }
-    if (tid < 9 * npt) rl = arena[d.off_L + 9ll * spt[tid / 9] + tid % 9];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int q = tid + kBlock * u;
+      rl[u] = q < 9 * npt ? arena[d.off_L + 9ll * spt[q / 9] + q % 9] : 0.0;
+    }
     if (tid < 3 * npt) rg = arena[d.off_gp + 3ll * spt[tid / 3] + tid % 3];
 #pragma unroll
     for (int u = 0; u < kLoneStage; ++u) {
       const int q = tid + kBlock * u;
       if (q < nW) {
         sZ[q] = rw[u];
-        if (!fused) sJ[q] = rj[u];
+        if constexpr (!fused) sJ[q] = rj[u];
       }
     }
-    if (fused) {
+    if constexpr (fused) {
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < 3; ++u) {
         const int q = tid + kBlock * u;
         if (q < 36 * m) sJJ[q] = rb[u];
         else if (q < 42 * m) sJb[q - 36 * m] = rb[u];
       }
     } else {
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < 3; ++u)
         if (tid + kBlock * u < nB) sB[tid + kBlock * u] = rb[u];
     }
-    if (tid < 9 * npt) sL[tid] = rl;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      if (tid + kBlock * u < 9 * npt) sL[tid + kBlock * u] = rl[u];
     if (tid < 3 * npt) sz[tid] = rg;
   }
   __syncthreads();
@@ -1859,7 +1887,7 @@ __device__ double backsub_lone_block(const ChainDev& cd, const int32_t* __restri
   const bool valid = uu < per && u < npt;
   double t[3] = {0.0, 0.0, 0.0};
   if (valid) {
-    const int e = blk[4 + kLoneSub + u] + a;
+    const int e = blk[kLoneHdrE0 + u] + a;
     double W[18], dx[6];
     ldk(arena + cd.off_W + 18ll * e, W);
     ldk(dpose + 6ll * cd.edge_pose[e], dx);
@@ -1876,7 +1904,7 @@ __device__ double backsub_lone_block(const ChainDev& cd, const int32_t* __restri
   }
   double acc = 0.0;
   if (valid && a == 0) {
-    const int pt = blk[4 + u];
+    const int pt = blk[kLoneHdrPt + u];
     const double* gp = arena + cd.off_gp + 3ll * pt;
     double x[3] = {gp[0] - s[0], gp[1] - s[1], gp[2] - s[2]}, L[9];
     ldk(arena + cd.off_L + 9ll * pt, L);
@@ -2187,10 +2215,11 @@ int debug_lone_clock(void* out) {
 extern "C" int dynohip_debug_lone_clock(unsigned long long* out) { return debug_lone_clock(out); }
 
 void launch_lone_schur(const LoneSchurDev& d, double* arena, hipStream_t s) {
-  if (d.n_group > 0)
-    k_lone_schur<<<d.n_group, kBlock,
-                   sizeof(double) * kLoneSub * (d.fused ? lone_point_doubles_fused(d.max_m) : lone_point_doubles(d.max_m)),
-                   s>>>(d, arena);
+  if (d.n_group <= 0) return;
+  if (d.fused)
+    k_lone_schur<true><<<d.n_group, kBlock, sizeof(double) * lone_lds_doubles(d.max_m, true), s>>>(d, arena);
+  else
+    k_lone_schur<false><<<d.n_group, kBlock, sizeof(double) * lone_lds_doubles(d.max_m, false), s>>>(d, arena);
 }
 
 int backsub_blocks(const ChainDev& c, int n_lone, int n_pose) {

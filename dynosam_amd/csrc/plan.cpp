@@ -814,7 +814,7 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
     // one PoseToPoint factor per neighbour (every static landmark of the
     // formulations). Grouped by the neighbour list (bucketed by its first
     // pose, then compared), in point order; a group is split into
-    // near-equal subgroups of at most kLoneSub points.
+    // near-equal subgroups of at most lone_cap(m) points.
     P.lgroup.clear();
     P.lone_pose.clear();
     P.lone_blk.clear();
@@ -889,7 +889,8 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
         for (int32_t k = k0b; k < k1b; ++k)
           if (cls_of[k - k0b] == static_cast<int32_t>(ci)) mem.push_back(byfirst[k]);
         const int32_t e0 = P.pt_edge_start[mem[0]], m = P.pt_edge_start[mem[0] + 1] - e0;
-        const int32_t n = static_cast<int32_t>(mem.size()), nsub = (n + kLoneSub - 1) / kLoneSub;
+        const int32_t cap = lone_cap(m);
+        const int32_t n = static_cast<int32_t>(mem.size()), nsub = (n + cap - 1) / cap;
         for (int32_t u = 0; u < nsub; ++u) {
           const int32_t k0 = static_cast<int32_t>(int64_t{n} * u / nsub), k1 = static_cast<int32_t>(int64_t{n} * (u + 1) / nsub);
           LoneGroup G;
@@ -910,13 +911,14 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
           blk[0] = m;
           blk[1] = G.npt;
           blk[2] = static_cast<int32_t>(G.out);
+          for (int32_t a = 0; a < m; ++a) blk[kLoneHdrPose + a] = P.edge_pose[e0 + a];
           for (int32_t k = k0; k < k1; ++k) {
             const int32_t pt = mem[k], u = k - k0;
-            blk[4 + u] = pt;
-            blk[4 + kLoneSub + u] = P.pt_edge_start[pt];
+            blk[kLoneHdrPt + u] = pt;
+            blk[kLoneHdrE0 + u] = P.pt_edge_start[pt];
             lone_grouped[pt] = 1;
             const int32_t ep = P.pt_edge_start[pt] - e_l0;
-            for (int32_t a = 0; a < m; ++a) blk[4 + 2 * kLoneSub + m * u + a] = static_cast<int32_t>(prec[ep + a]);
+            for (int32_t a = 0; a < m; ++a) blk[kLoneHdrRec + m * u + a] = static_cast<int32_t>(prec[ep + a]);
           }
           P.lgroup.push_back(G);
         }

@@ -53,7 +53,7 @@ struct GEntry {
   int32_t sign;
 };
 
-// Lone-point group (k_lone_schur): up to kLoneSub lone points (static
+// Lone-point group (k_lone_schur): up to lone_cap(m) lone points (static
 // landmarks) sharing one sorted list of m neighbour poses, every point with
 // exactly one PoseToPoint factor per neighbour and no other factor (a group
 // of more points is split into several). Its workgroup sums the group's
@@ -63,14 +63,24 @@ struct GEntry {
 // J_a^T b - W_a^T D^-1 g_p. The reduced gathers read them as (identity,
 // partial) entries. On the device a group is one block of kLoneBlk ints:
 // [m, npt, out, 0, point[kLoneSub], first edge[kLoneSub],
-//  PoseToPoint record offset (J_pose at +0, b at +27)[kLoneSub][m]].
+//  neighbour pose[kLoneMaxNb], PoseToPoint record offset (J_pose at +0, b
+//  at +27)[npt][m]].
 // The group's arena area at `out` holds those per-try partials (36 m(m+1)/2
 // + 6 m doubles), then its H area (42 m: the 6x6 J_a^T J_a per neighbour,
-// then the J_a^T b), written once per linearisation by k_lone_lin.
+// then the J_a^T b), written once per linearisation by the fused
+// linearisation (kernels.hip lone_lin_block).
+// A block's kernels run a lane per (point, neighbour) in four 64-lane waves,
+// floor(64 / m) points per wave: lone_cap(m) points (32 for the 7-pose
+// tracks of the formulations' static landmarks).
 constexpr int kLoneMaxNb = 10;
-constexpr int kLoneSub = 16;
-constexpr int kLoneBlk = 200;
-static_assert(4 + 2 * kLoneSub + kLoneSub * kLoneMaxNb <= kLoneBlk, "lone block");
+constexpr int kLoneSub = 32;
+constexpr int kLoneHdrPt = 4;                             // point[kLoneSub]
+constexpr int kLoneHdrE0 = kLoneHdrPt + kLoneSub;         // first edge[kLoneSub]
+constexpr int kLoneHdrPose = kLoneHdrE0 + kLoneSub;       // neighbour pose[kLoneMaxNb]
+constexpr int kLoneHdrRec = kLoneHdrPose + kLoneMaxNb;    // record offset[npt][m], npt m <= 256
+constexpr int kLoneBlk = (kLoneHdrRec + 256 + 3) / 4 * 4;
+constexpr int lone_cap(int m) { return 4 * (64 / m) < kLoneSub ? 4 * (64 / m) : kLoneSub; }
+static_assert(lone_cap(1) * 1 <= 256 && lone_cap(kLoneMaxNb) * kLoneMaxNb <= 256, "a lane per (point, neighbour)");
 struct LoneGroup {
   int32_t m;        // neighbour poses
   int32_t npt;      // member points

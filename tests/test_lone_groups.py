@@ -3,8 +3,8 @@ static landmarks whose Schur contributions one workgroup per group sums.
 Checked on the host against the graph itself (no GPU): which lone points are
 eligible, that every eligible point is in exactly one group, that a group's
 points share its neighbour-pose list, the device block layout (points,
-first edges, PoseToPoint record offsets) and the near-equal split of a list
-into groups of at most 16."""
+first edges, neighbour poses, PoseToPoint record offsets) and the near-equal
+split of a list into groups of at most lone_cap(m) points."""
 import numpy as np
 import pytest
 
@@ -12,7 +12,16 @@ from dynosam_amd import synth
 from dynosam_amd.optimizer import plan_export
 from graphs_extra import mixed_lone_graph
 
-MAX_NB, SUB, BLK = 10, 16, 200
+# plan.hpp: kLoneMaxNb, kLoneSub, the header offsets and kLoneBlk
+MAX_NB, SUB = 10, 32
+HDR_PT, HDR_E0, HDR_POSE = 4, 4 + SUB, 4 + 2 * SUB
+HDR_REC = HDR_POSE + MAX_NB
+BLK = (HDR_REC + 256 + 3) // 4 * 4
+
+
+def lone_cap(m):
+    """points per block: a lane per (point, neighbour) in four 64-lane waves"""
+    return min(4 * (64 // m), SUB)
 
 
 @pytest.fixture(scope="module", params=[("T2", {}), ("T2", {"formulation": 1}), ("C1", {}), ("mixed", {})],
@@ -55,7 +64,7 @@ def test_groups_cover_the_eligible_lone_points_once(plan):
     elig = eligible_points(ex)
     blk = ex["lone_blk"].reshape(-1, BLK)
     assert blk.shape[0] == ngroups
-    seen = [int(p) for g in range(ngroups) for p in blk[g, 4:4 + blk[g, 1]]]
+    seen = [int(p) for g in range(ngroups) for p in blk[g, HDR_PT:HDR_PT + blk[g, 1]]]
     assert sorted(seen) == sorted(elig)
     assert len(seen) == len(set(seen))
     assert bool(all_grouped) == (len(elig) == n_pt - p_lone)
@@ -74,19 +83,21 @@ def test_group_blocks_match_the_graph(plan):
     for g in range(ngroups):
         m, npt = int(blk[g, 0]), int(blk[g, 1])
         assert (m, npt) == (int(lg[g, 0]), int(lg[g, 1]))
-        assert 1 <= npt <= SUB and 1 <= m <= MAX_NB
+        assert 1 <= m <= MAX_NB and 1 <= npt <= lone_cap(m) and npt * m <= 256
         poses = lp[lg[g, 2]:lg[g, 2] + m].tolist()
         assert poses == sorted(poses)
+        assert blk[g, HDR_POSE:HDR_POSE + m].tolist() == poses
+        assert not blk[g, HDR_POSE + m:HDR_REC].any()
         outs.append(int(blk[g, 2]) & 0xffffffff)
         assert outs[-1] == int(lg[g, 3]) & 0xffffffff
         for u in range(npt):
-            p = int(blk[g, 4 + u])
-            assert int(blk[g, 4 + SUB + u]) == pes[p]
+            p = int(blk[g, HDR_PT + u])
+            assert int(blk[g, HDR_E0 + u]) == pes[p]
             assert ep[pes[p]:pes[p] + m].tolist() == poses
             for a in range(m):
-                rec = int(blk[g, 4 + 2 * SUB + m * u + a]) & 0xffffffff
+                rec = int(blk[g, HDR_REC + m * u + a]) & 0xffffffff
                 assert rec == base0 + stride0 * elig[p][poses[a]]
-        assert not blk[g, 4 + npt:4 + SUB].any()   # unused member slots are zero
+        assert not blk[g, HDR_PT + npt:HDR_PT + SUB].any()   # unused member slots are zero
     # partial areas: disjoint, in group order, m(m+1)/2 6x6 blocks + m gradients each
     for g in range(ngroups - 1):
         m = int(blk[g, 0])
@@ -109,7 +120,7 @@ def test_groups_split_lists_evenly_in_first_pose_order(plan):
         sizes.setdefault(l, []).append(int(blk[g, 1]))
     for l, s in sizes.items():
         assert max(s) - min(s) <= 1, l
-        assert len(s) == -(-sum(s) // SUB), l
+        assert len(s) == -(-sum(s) // lone_cap(len(l))), l
 
 
 def test_ineligible_lone_points_stay_out():
@@ -119,7 +130,7 @@ def test_ineligible_lone_points_stay_out():
     keys = np.asarray(v.keys)
     pes = plan_export(g, v, "pt_edges")
     assert info[0] == 0   # not every lone point grouped: CSR gathers, lone Y and per-point back-substitution stay on
-    grouped = {int(p) for g_ in range(blk.shape[0]) for p in blk[g_, 4:4 + blk[g_, 1]]}
+    grouped = {int(p) for g_ in range(blk.shape[0]) for p in blk[g_, HDR_PT:HDR_PT + blk[g_, 1]]}
     assert len(grouped) == sum(int(blk[g_, 1]) for g_ in range(blk.shape[0]))
     # the two ineligible landmarks are lone points (in the lone range), not grouped
     assert len(grouped) == int(info[4] - info[3]) - 2
