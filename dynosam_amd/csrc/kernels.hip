@@ -1232,9 +1232,10 @@ __device__ void chain_factor_group(const ChainDev& cd, double* __restrict__ aren
 // [nbg, nbg + nbs) a thread per singleton chain, then blocks that zero the
 // solve's accumulation buffers (the tile slots the reduced gather scatters
 // into, the reduced gradient) in 16-byte stores, in place of memsets.
-__global__ __launch_bounds__(kBlock) void k_chain_factor(ChainDev cd, double* __restrict__ arena, double lambda,
-                                                         int* fail, ZeroDev zb, int nbg, int nbs) {
-  const int blk = blockIdx.x;
+// workgroup blk of nblk (the chains' and the fill blocks' range of a launch)
+__device__ __forceinline__ void chain_factor_blocks(const ChainDev& cd, double* __restrict__ arena, double lambda,
+                                                    int* fail, const ZeroDev& zb, int nbg, int nbs, int blk,
+                                                    int nblk) {
   if (blk < nbg) {
     const int c = (blk * kBlock + static_cast<int>(threadIdx.x)) / kGrp;
     if (c < cd.n_long) chain_factor_group(cd, arena, lambda, fail, c, threadIdx.x % kGrp);
@@ -1245,7 +1246,7 @@ __global__ __launch_bounds__(kBlock) void k_chain_factor(ChainDev cd, double* __
     if (c < cd.n_comp) chain_factor_thread(cd, arena, lambda, fail, c);
     return;
   }
-  const int64_t stride = static_cast<int64_t>(gridDim.x - nbg - nbs) * kBlock;
+  const int64_t stride = static_cast<int64_t>(nblk - nbg - nbs) * kBlock;
   const int64_t i0 = static_cast<int64_t>(blk - nbg - nbs) * kBlock + threadIdx.x;
   const double2 zero = {0.0, 0.0};
 #pragma unroll
@@ -1262,6 +1263,11 @@ __global__ __launch_bounds__(kBlock) void k_chain_factor(ChainDev cd, double* __
     const int64_t n = zb.sn[k] / 2;
     for (int64_t i = i0; i < n; i += stride) p[i] = sent;
   }
+}
+
+__global__ __launch_bounds__(kBlock) void k_chain_factor(ChainDev cd, double* __restrict__ arena, double lambda,
+                                                         int* fail, ZeroDev zb, int nbg, int nbs) {
+  chain_factor_blocks(cd, arena, lambda, fail, zb, nbg, nbs, blockIdx.x, gridDim.x);
 }
 
 // Y = C^-1 W for one (chain, neighbour pose) pair and one column `col` of
@@ -1527,14 +1533,20 @@ __device__ unsigned long long g_lclk[8][8192];
   } while (0)
 #endif
 
-template <bool FUSED>
-__global__ __launch_bounds__(kBlock) void k_lone_schur(LoneSchurDev d, double* __restrict__ arena) {
+// Group block gb. LFACT: the block also factors its points' damped blocks,
+// L = chol(D + lambda I), and stores L and v = D^-1 g_p for the back-
+// substitution, as k_chain_factor's thread per singleton chain did (the same
+// operations): the groups then run in the chain launch, beside the chain
+// recurrences (k_chain_lone). Without LFACT it reads L from k_chain_factor.
+template <bool FUSED, bool LFACT>
+__device__ void lone_schur_block(const LoneSchurDev& d, int gb, double* __restrict__ arena, double lambda,
+                                 int* fail) {
   extern __shared__ double lds[];
   __shared__ int32_t hdr[kLoneBlk];
   const int tid = threadIdx.x;
   LCLK(0);
-  if (blockIdx.x == 0 && tid < 36) arena[d.off_I6 + tid] = (tid % 7 == 0) ? 1.0 : 0.0;
-  for (int q = tid; q < kLoneBlk; q += kBlock) hdr[q] = d.blk[static_cast<int64_t>(blockIdx.x) * kLoneBlk + q];
+  if (gb == 0 && tid < 36) arena[d.off_I6 + tid] = (tid % 7 == 0) ? 1.0 : 0.0;
+  for (int q = tid; q < kLoneBlk; q += kBlock) hdr[q] = d.blk[static_cast<int64_t>(gb) * kLoneBlk + q];
   __syncthreads();
   LCLK(1);
   const int m = hdr[0], npt = hdr[1], m18 = 18 * m, np = m * (m + 1) / 2, ntask = 6 * np + 6 * m;
@@ -1580,9 +1592,9 @@ __global__ __launch_bounds__(kBlock) void k_lone_schur(LoneSchurDev d, double* _
       }
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < 2; ++u) {   // L (LFACT: D, factored below)
       const int q = tid + kBlock * u;
-      rl[u] = q < 9 * npt ? arena[d.off_L + 9ll * spt[q / 9] + q % 9] : 0.0;
+      rl[u] = q < 9 * npt ? arena[(LFACT ? d.off_D : d.off_L) + 9ll * spt[q / 9] + q % 9] : 0.0;
     }
     if (tid < 3 * npt) rg = arena[d.off_gp + 3ll * spt[tid / 3] + tid % 3];
 #pragma unroll
@@ -1611,6 +1623,34 @@ __global__ __launch_bounds__(kBlock) void k_lone_schur(LoneSchurDev d, double* _
     if (tid < 3 * npt) sz[tid] = rg;
   }
   __syncthreads();
+  if constexpr (LFACT) {
+    // chain_factor_thread for a chain of one point: L = chol(D + lambda I),
+    // z = L^-1 g_p, v = L^-T z; L and v to the arena
+    if (tid < npt) {
+      double Dm[9], L[9], g[3];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) Dm[k] = sL[9 * tid + k];
+      Dm[0] += lambda; Dm[4] += lambda; Dm[8] += lambda;
+      if (!chol3(Dm, L)) {
+        *fail = 1;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) L[k] = (k % 4 == 0) ? 1.0 : 0.0;
+      }
+#pragma unroll
+      for (int k = 0; k < 3; ++k) g[k] = sz[3 * tid + k];
+      lsolve<1>(L, g);
+      ltsolve<1>(L, g);
+      const int p = spt[tid];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        sL[9 * tid + k] = L[k];
+        arena[d.off_L + 9ll * p + k] = L[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 3; ++k) arena[d.off_v + 3ll * p + k] = g[k];
+    }
+    __syncthreads();
+  }
   LCLK(2);
   // Z = L^-1 W in place, a thread per (point, a, column); z = L^-1 g_p
   for (int q = tid; q < npt * m * 6 + npt; q += kBlock) {
@@ -1742,6 +1782,26 @@ __global__ __launch_bounds__(kBlock) void k_lone_schur(LoneSchurDev d, double* _
     }
   }
   LCLK(4);
+}
+
+template <bool FUSED>
+__global__ __launch_bounds__(kBlock) void k_lone_schur(LoneSchurDev d, double* __restrict__ arena) {
+  lone_schur_block<FUSED, false>(d, blockIdx.x, arena, 0.0, nullptr);
+}
+
+// The chain launch with the lone groups in it (every lone point grouped):
+// workgroups [0, n_group) are group blocks (lone_schur_block with the point
+// factorisation), then k_chain_factor's long chains and fill blocks. The
+// groups need nothing from the chains, so the two run side by side.
+template <bool FUSED>
+__global__ __launch_bounds__(kBlock) void k_chain_lone(ChainDev cd, LoneSchurDev d, double* __restrict__ arena,
+                                                       double lambda, int* fail, ZeroDev zb, int nbg) {
+  const int b = blockIdx.x;
+  if (b < d.n_group) {
+    lone_schur_block<FUSED, true>(d, b, arena, lambda, fail);
+    return;
+  }
+  chain_factor_blocks(cd, arena, lambda, fail, zb, nbg, 0, b - d.n_group, gridDim.x - d.n_group);
 }
 
 // dp = C^-1 (gp - W dX), the products W dX formed per edge (edge_wdx). Every back-
@@ -2213,6 +2273,20 @@ int debug_lone_clock(void* out) {
 }
 
 extern "C" int dynohip_debug_lone_clock(unsigned long long* out) { return debug_lone_clock(out); }
+
+void launch_chain_lone(const ChainDev& c, const LoneSchurDev& d, double* arena, double lambda, int* fail,
+                       const ZeroDev& z, hipStream_t s) {
+  const int64_t nz = std::max(std::max(z.n[0], std::max(z.n[1], z.n[2])), std::max(z.sn[0], z.sn[1])) / 2;
+  const int nbz = nz == 0 ? 0 : static_cast<int>(std::min<int64_t>(1024, nblocks(nz)));
+  const int nbg = nblocks(static_cast<int64_t>(c.n_long) * kGrp);
+  const int nb = d.n_group + nbg + std::max(nbz, 1);
+  if (d.fused)
+    k_chain_lone<true><<<nb, kBlock, sizeof(double) * lone_lds_doubles(d.max_m, true), s>>>(c, d, arena, lambda,
+                                                                                           fail, z, nbg);
+  else
+    k_chain_lone<false><<<nb, kBlock, sizeof(double) * lone_lds_doubles(d.max_m, false), s>>>(c, d, arena, lambda,
+                                                                                             fail, z, nbg);
+}
 
 void launch_lone_schur(const LoneSchurDev& d, double* arena, hipStream_t s) {
   if (d.n_group <= 0) return;

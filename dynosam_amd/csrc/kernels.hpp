@@ -87,8 +87,9 @@ struct LoneSchurDev {
   int max_m = 0;                          // largest m (sizes the staging LDS)
   const int32_t* blk = nullptr;           // kLoneBlk ints per group
   uint64_t off_W = 0, off_L = 0, off_gp = 0, off_I6 = 0;
-  // fused: J_a^T J_a and J_a^T b come from the group's H area (k_lone_lin,
-  // plan.hpp lone_h_off), not from the PoseToPoint records
+  uint64_t off_D = 0, off_v = 0;          // (launch_chain_lone: the groups factor their points)
+  // fused: J_a^T J_a and J_a^T b come from the group's H area (the fused
+  // linearisation, plan.hpp), not from the PoseToPoint records
   int fused = 0;
 };
 
@@ -192,6 +193,11 @@ void launch_chain_solve_y(const ChainDev& c, double* arena, hipStream_t s);
 // the lone-point groups' partial reduced blocks and gradients (after
 // launch_chain_factor: reads L and v of the lone points)
 void launch_lone_schur(const LoneSchurDev& d, double* arena, hipStream_t s);
+// every lone point grouped: the groups (with their points' factorisation,
+// L and v) and k_chain_factor's long chains and fill blocks in one launch,
+// in place of launch_chain_factor + launch_lone_schur
+void launch_chain_lone(const ChainDev& c, const LoneSchurDev& d, double* arena, double lambda, int* fail,
+                       const ZeroDev& z, hipStream_t s);
 int debug_lone_clock(void* out);   // -DDYNOHIP_LONE_CLOCK builds: the stamps of the last launch
 // The tail of a try in the back-substitution launch (LevenbergMarquardt-
 // Optimizer.cpp tryLambda): the candidate values and the linearised cost

@@ -426,6 +426,7 @@ struct dynohip_solver {
   DevBuf<int32_t> lin_list0;
   LoneLinDev lld;
   bool fused_env = true;   // DYNOHIP_FUSED_LONE=0 keeps the record path
+  bool chain_lone = true;  // DYNOHIP_CHAIN_LONE=0: separate chain and lone-group launches
   GatherBufs gD, gE, gGp, gW, gRed, gGred;
   DevBuf<int32_t> redA, redB;
   DevBuf<uint32_t> redslot;
@@ -659,6 +660,8 @@ int upload_plan(dynohip_solver* s, bool types_done = false) {
   ld.off_L = P.off_L;
   ld.off_gp = P.off_gp;
   ld.off_I6 = P.off_I6;
+  ld.off_D = P.off_D;
+  ld.off_v = P.off_v;
   s->lld.blk = s->lone_blk.p;
   HIPCHK(s, s->lcpart.alloc(static_cast<size_t>(backsub_blocks(
                                 c, P.lone_all_grouped ? static_cast<int>(P.lgroup.size()) : 0, P.n_pose)) + 1));
@@ -854,10 +857,16 @@ int enqueue_try(dynohip_solver* s, double lambda) {
     z.s[1] = s->bpartials.p;
     z.sn[1] = static_cast<int64_t>(P.n_partials) * kTile;
   }
-  launch_chain_factor(s->cd, A, lambda, s->failp, z, st);
-  launch_chain_solve_y(s->cd, A, st);
   s->ld.fused = fused_lone(s) ? 1 : 0;
-  launch_lone_schur(s->ld, A, st);
+  if (P.lone_all_grouped && !P.lgroup.empty() && s->chain_lone) {
+    // the groups factor their own points beside the chain recurrences
+    launch_chain_lone(s->cd, s->ld, A, lambda, s->failp, z, st);
+    launch_chain_solve_y(s->cd, A, st);
+  } else {
+    launch_chain_factor(s->cd, A, lambda, s->failp, z, st);
+    launch_chain_solve_y(s->cd, A, st);
+    launch_lone_schur(s->ld, A, st);
+  }
   if (timed) (void)hipEventRecord(s->ev[3], st);
   launch_gather_reduced(s->gRed.dev(P.gRed.ntargets()), s->redA.p, s->redB.p, s->redslot.p,
                         s->gGred.dev(P.gGred.ntargets()),
@@ -1211,6 +1220,7 @@ int dynohip_create(int device_id, dynohip_solver** out) {
   if (const char* e = std::getenv("DYNOHIP_LINERR_DIRECT")) s->linerr_direct = std::atoi(e) != 0;
   if (const char* e = std::getenv("DYNOHIP_FUSED_LONE")) s->fused_env = std::atoi(e) != 0;
   if (const char* e = std::getenv("DYNOHIP_BACK_POLL")) s->sd.back_poll = std::atoi(e) != 0;
+  if (const char* e = std::getenv("DYNOHIP_CHAIN_LONE")) s->chain_lone = std::atoi(e) != 0;
   s->stream = r.stream;
   s->side = r.side;
   s->ev_main = r.ev_main;

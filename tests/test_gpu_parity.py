@@ -378,10 +378,13 @@ def test_execution_paths_agree(gpu_available, name, monkeypatch):
     same per-task arithmetic in the same order, bit for bit."""
     results = []
     for opts in ({}, {"level_factor": True}, {"level_factor": True, "wide_updates": 0}, {"level_backward": True},
-                 {"level_factor": True, "wide_updates": 0, "level_backward": True}, "flags"):
+                 {"level_factor": True, "wide_updates": 0, "level_backward": True}, "flags", "split"):
         monkeypatch.setenv("DYNOHIP_BACK_POLL", "0" if opts == "flags" else "1")
+        # "split": k_chain_factor factors the static landmarks' points and
+        # k_lone_schur runs as its own launch (the same operations)
+        monkeypatch.setenv("DYNOHIP_CHAIN_LONE", "0" if opts == "split" else "1")
         g, v, _, s = make(name)
-        if opts != "flags":
+        if isinstance(opts, dict):
             s.set_exec_options(**opts)
         for _ in range(3):
             s.iterate()
