@@ -137,7 +137,13 @@ struct TileSchedDev {
   // one-launch backward: hand-offs on the data (k_back_poll; x and partials
   // sentinel-filled before each solve) instead of epoch flags (k_back_persist)
   bool back_poll = true;
+  // k_back_wide's items (first part, parts): consecutive parts 2j, 2j+1 of a
+  // column (at most kBackPersistMax items; 0 items: k_back_poll)
+  const int2* witems = nullptr;
+  int n_witems = 0;
 };
+// k_back_wide's items from the part list: (first part, 1 or 2)
+std::vector<int32_t> back_wide_items(const std::vector<BackPart>& parts);
 
 // the sentinel k_back_poll's consumers wait past (a signalling NaN)
 constexpr uint64_t kBackSentinel = 0xFFF4DEADBEEFCAFEull;

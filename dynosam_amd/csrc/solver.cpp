@@ -439,6 +439,8 @@ struct dynohip_solver {
   DevBuf<int32_t> tile_pos, row_start, row_col, row_slot, bent, pairs;
   DevBuf<TileTask> ftask;
   DevBuf<BackPart> bpart;
+  DevBuf<int32_t> witems;   // k_back_wide's (first part, parts) items
+  bool back_wide = true;    // DYNOHIP_BACK_WIDE=0: one part per workgroup (k_back_poll)
   DevBuf<double> bpartials;
   DevBuf<int> arrive;
   DevBuf<int32_t> fdep_start, fdep, fqueue;
@@ -603,6 +605,11 @@ int upload_plan(dynohip_solver* s, bool types_done = false) {
   HIPCHK(s, up.add(s->pairs, P.pairs));
   HIPCHK(s, s->contrib.alloc(static_cast<size_t>(P.n_slots) * kTile));
   HIPCHK(s, up.add(s->bpart, P.bpart));
+  {
+    const std::vector<int32_t> wi = back_wide_items(P.bpart);
+    HIPCHK(s, up.add(s->witems, wi));
+    s->sd.n_witems = s->back_wide ? static_cast<int>(wi.size() / 2) : 0;
+  }
   HIPCHK(s, s->bpartials.alloc(static_cast<size_t>(P.n_partials) * kTile + 1));
   HIPCHK(s, s->arrive.alloc(static_cast<size_t>(P.NT) + 1));
   HIPCHK(s, hipMemsetAsync(s->arrive.p, 0, (static_cast<size_t>(P.NT) + 1) * sizeof(int), st));
@@ -676,6 +683,7 @@ int upload_plan(dynohip_solver* s, bool types_done = false) {
   s->sd.ftask = s->ftask.p;
   s->sd.pairs = s->pairs.p;
   s->sd.bpart = s->bpart.p;
+  s->sd.witems = reinterpret_cast<const int2*>(s->witems.p);
   s->sd.partials = s->bpartials.p;
   s->sd.arrive = s->arrive.p;
   s->sd.done = s->done.p;
@@ -1221,6 +1229,7 @@ int dynohip_create(int device_id, dynohip_solver** out) {
   if (const char* e = std::getenv("DYNOHIP_FUSED_LONE")) s->fused_env = std::atoi(e) != 0;
   if (const char* e = std::getenv("DYNOHIP_BACK_POLL")) s->sd.back_poll = std::atoi(e) != 0;
   if (const char* e = std::getenv("DYNOHIP_CHAIN_LONE")) s->chain_lone = std::atoi(e) != 0;
+  if (const char* e = std::getenv("DYNOHIP_BACK_WIDE")) s->back_wide = std::atoi(e) != 0;
   s->stream = r.stream;
   s->side = r.side;
   s->ev_main = r.ev_main;

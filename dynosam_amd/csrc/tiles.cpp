@@ -714,17 +714,18 @@ bool build_tile_schedule(Plan& P, bool own_threads) {
   P.blevel = std::move(best.blevel);
   P.bent = std::move(best.bent);
   // split every backward task into workgroups of <= back_part_tiles entries:
-  // the smallest power of two (>= 2) whose part count lets the one-launch
-  // backward solve keep every workgroup resident
+  // the smallest power of two (>= 4: the tiles a part holds in registers
+  // before its wait) whose part count lets the one-launch backward solve
+  // keep every workgroup resident
   auto count_parts = [&](int tpp) {
     int64_t n = 0;
     for (const BackTask& t : P.btask) n += std::max<int32_t>(1, (t.end - t.beg + tpp - 1) / tpp);
     return n;
   };
-  P.back_part_tiles = 2;
+  P.back_part_tiles = 4;
   if (const char* e = std::getenv("DYNOHIP_BACK_PART_TILES")) P.back_part_tiles = std::max(1, std::atoi(e));   // sweep knob
   while (count_parts(P.back_part_tiles) > kBackPersistMax && P.back_part_tiles < 64) P.back_part_tiles *= 2;
-  if (count_parts(P.back_part_tiles) > kBackPersistMax) P.back_part_tiles = 2;  // level launches
+  if (count_parts(P.back_part_tiles) > kBackPersistMax) P.back_part_tiles = 4;  // level launches
   const int32_t tpp = P.back_part_tiles;
   P.bpart.clear();
   P.bplevel.assign(1, 0);

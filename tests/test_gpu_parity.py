@@ -378,8 +378,10 @@ def test_execution_paths_agree(gpu_available, name, monkeypatch):
     same per-task arithmetic in the same order, bit for bit."""
     results = []
     for opts in ({}, {"level_factor": True}, {"level_factor": True, "wide_updates": 0}, {"level_backward": True},
-                 {"level_factor": True, "wide_updates": 0, "level_backward": True}, "flags", "split"):
+                 {"level_factor": True, "wide_updates": 0, "level_backward": True}, "flags", "split", "parts"):
         monkeypatch.setenv("DYNOHIP_BACK_POLL", "0" if opts == "flags" else "1")
+        # "parts": one backward part per workgroup (k_back_poll) instead of two (k_back_wide)
+        monkeypatch.setenv("DYNOHIP_BACK_WIDE", "0" if opts == "parts" else "1")
         # "split": k_chain_factor factors the static landmarks' points and
         # k_lone_schur runs as its own launch (the same operations)
         monkeypatch.setenv("DYNOHIP_CHAIN_LONE", "0" if opts == "split" else "1")
