@@ -257,6 +257,7 @@ struct Uploads {
   };
   std::vector<Item> items;
   size_t total = 0;
+  // (v is read at run(): it must outlive the call)
   template <typename T, class Alloc>
   hipError_t add(DevBuf<T>& d, const std::vector<T, Alloc>& v) {
     const hipError_t e = d.alloc(v.size());
@@ -440,6 +441,7 @@ struct dynohip_solver {
   DevBuf<TileTask> ftask;
   DevBuf<BackPart> bpart;
   DevBuf<int32_t> witems;   // k_back_wide's (first part, parts) items
+  std::vector<int32_t> witems_h;   // their host copy (read by Uploads::run)
   bool back_wide = true;    // DYNOHIP_BACK_WIDE=0: one part per workgroup (k_back_poll)
   DevBuf<double> bpartials;
   DevBuf<int> arrive;
@@ -605,11 +607,10 @@ int upload_plan(dynohip_solver* s, bool types_done = false) {
   HIPCHK(s, up.add(s->pairs, P.pairs));
   HIPCHK(s, s->contrib.alloc(static_cast<size_t>(P.n_slots) * kTile));
   HIPCHK(s, up.add(s->bpart, P.bpart));
-  {
-    const std::vector<int32_t> wi = back_wide_items(P.bpart);
-    HIPCHK(s, up.add(s->witems, wi));
-    s->sd.n_witems = s->back_wide ? static_cast<int>(wi.size() / 2) : 0;
-  }
+  // (kept in the solver: Uploads packs the host arrays at up.run below)
+  s->witems_h = back_wide_items(P.bpart);
+  HIPCHK(s, up.add(s->witems, s->witems_h));
+  s->sd.n_witems = s->back_wide ? static_cast<int>(s->witems_h.size() / 2) : 0;
   HIPCHK(s, s->bpartials.alloc(static_cast<size_t>(P.n_partials) * kTile + 1));
   HIPCHK(s, s->arrive.alloc(static_cast<size_t>(P.NT) + 1));
   HIPCHK(s, hipMemsetAsync(s->arrive.p, 0, (static_cast<size_t>(P.NT) + 1) * sizeof(int), st));

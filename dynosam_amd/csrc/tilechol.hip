@@ -1510,6 +1510,11 @@ void launch_tile_forward(const TileDev& b, const TileSchedDev& sd, const std::ve
 
 std::vector<int32_t> back_wide_items(const std::vector<BackPart>& parts) {
   std::vector<int32_t> it;
+  // k_back_wide takes a part's entries in one chunk: with longer parts
+  // (DYNOHIP_BACK_PART_TILES > DYNOHIP_BACK_CH) there are no items, and the
+  // part-per-workgroup kernel runs
+  for (const BackPart& p : parts)
+    if (p.end - p.beg > DYNOHIP_BACK_CH) return it;
   for (size_t p = 0; p < parts.size();) {
     const bool pair = p + 1 < parts.size() && parts[p + 1].k == parts[p].k && parts[p].part % 2 == 0 &&
                       parts[p + 1].part == parts[p].part + 1;

@@ -7,6 +7,7 @@ the oracle is moved onto the GPU's values (same lambda by construction when
 the accept/reject sequences agree), so each comparison isolates one
 linearise + damped solve + retract. Free-running runs are checked too.
 """
+import json
 import os
 
 import numpy as np
@@ -231,16 +232,24 @@ def test_conditioned_vs_oracle_at_scale(gpu_available, name, iters):
 def test_free_running_ns_vs_oracle(gpu_available):
     """The north-star graph (500 frames, 5 objects, 100k landmarks) solved
     free-running by both sides, RGBDBackendModule.cc:207-231's whole LM:
-    the same accept / lambda sequence over the iterations both run, the new
-    errors within 1e-6 while lambda >= 1e-16 (where both sides' steps are
-    within 1e-6 of the exact step, profiles/r04/step_accuracy_ns.log), and
-    the GPU ending at an error no higher than the oracle's. The run length
-    itself is decided at lambda 1e-18 .. 1e-19, where the oracle's
-    double-precision step is 6-53 % off the exact one and the GPU's 2-9 %:
-    the relative cost decrease of that step against GTSAM's 1e-5 tolerance
-    decides whether another iteration follows, so the two runs may stop a
-    few iterations apart (the GPU's more accurate steps keep decreasing the
-    cost for longer)."""
+    the same accept / lambda sequence over the iterations both run, and the
+    GPU ending at an error no higher than the oracle's.
+
+    Two free runs drift apart by their rounding alone: each step is solved
+    in double precision to ~1e-8 of the values (profiles/r04/step_accuracy_ns.log)
+    and the next iteration starts from there. The size of that drift on this
+    graph is pinned by the oracle itself: tests/golden/ns_oracle_spread.json
+    holds its trace in two summation orders (make_ns_oracle_spread.py), whose
+    new errors differ by up to 5e-7 by lambda 1e-12 and 3.6e-6 by 1e-15. The
+    GPU's new error is held to max(1e-6, 4 x that spread so far) of the
+    oracle's while lambda >= 1e-18. The run length is decided at lambda
+    1e-18 .. 1e-19, where the oracle's double-precision step is 6-53 % off
+    the exact one and the GPU's 2-9 %: the relative cost decrease of that
+    step against GTSAM's 1e-5 tolerance decides whether another iteration
+    follows, so runs may stop a few iterations apart (the oracle's two
+    orders stop at 15 and 17)."""
+    spread = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "ns_oracle_spread.json")))
+    fw, rv = spread["forward"]["trace"], spread["reversed"]["trace"]
     g, v, _, s = make("NS")
     sg = s.optimize()
     o = Oracle(g, v, threads=cores())
@@ -249,14 +258,21 @@ def test_free_running_ns_vs_oracle(gpu_available):
     vr = rel(s.values_data(), o.values_data())
     print("NS free run", (sg.iterations, sg.inner_iterations), (so.iterations, so.inner_iterations),
           f"values rel {vr:.2e}", f"error {sg.final_error:.12e} {so.final_error:.12e}")
-    for a, b in zip(tg, to):
-        print(f"  lam {a['lam']:.0e} {b['lam']:.0e} accepted {a['accepted']} {b['accepted']}"
-              f" new {a['new_error']:.12e} {b['new_error']:.12e}")
     n = min(len(tg), len(to))
     assert [(e["accepted"], e["lam"]) for e in tg[:n]] == [(e["accepted"], e["lam"]) for e in to[:n]]
-    for a, b in zip(tg, to):
-        if a["accepted"] and a["lam"] >= 1e-16:
-            assert a["new_error"] == pytest.approx(b["new_error"], rel=1e-6)
+    # the fixture is this oracle's run (up to its thread count's rounding)
+    nf = min(len(fw), len(to))
+    assert [(e["accepted"], e["lam"]) for e in to[:nf]] == [(e["accepted"], e["lam"]) for e in fw[:nf]]
+    worst = 0.0
+    for i, (a, b) in enumerate(zip(tg, to)):
+        if i < len(fw) and i < len(rv) and fw[i]["accepted"] and rv[i]["accepted"]:
+            worst = max(worst, abs(fw[i]["new_error"] - rv[i]["new_error"]) / fw[i]["new_error"])
+        bar = max(1e-6, 4 * worst)
+        d = abs(a["new_error"] - b["new_error"]) / b["new_error"]
+        print(f"  lam {a['lam']:.0e} accepted {a['accepted']} {b['accepted']} new {a['new_error']:.12e}"
+              f" {b['new_error']:.12e} rel {d:.2e} oracle spread {worst:.2e}")
+        if a["accepted"] and a["lam"] >= 1e-18:
+            assert d <= bar, (i, d, bar)
     assert sg.final_error <= so.final_error * (1 + 1e-6)
 
 
