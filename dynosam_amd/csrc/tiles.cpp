@@ -94,32 +94,94 @@ void nd_order(int lo, int hi, int leaf, const std::vector<int32_t>& maxnb, std::
 // Partitioned form: the top log2(nranks) levels of
 // the dissection always split, and rank r owns the r-th leaf subtree in time
 // order (its interior); the separators above them are owned by no rank (-1).
-// Fails (returns false) when a required split is impossible: the graph is
-// too short in time for that many ranks.
-bool nd_order_part(int lo, int hi, int leaf, const std::vector<int32_t>& maxnb, int nr, int r0,
-                   std::vector<int32_t>& out, std::vector<int32_t>& owner) {
-  if (nr == 1) {
-    const size_t b = out.size();
-    nd_order(lo, hi, leaf, maxnb, out);
-    owner.resize(out.size(), r0);
-    (void)b;
-    return true;
-  }
+// A split of [lo, hi) over nr ranks (nl = nr / 2 on the left) is placed
+// where the estimated factorisation work per rank of the two sides is most
+// even: tile t's column weighs (env_t - t + 1)^2, env_t the largest
+// neighbour of any tile up to t inside the range (the envelope a column's
+// fill stays in; a banded column's Cholesky work grows with the square of
+// its reach), so a graph denser in some stretch of time (objects
+// visible for part of the sequence, configs[4]) does not leave one rank with
+// most of the work. Fails (returns false) when a required split is
+// impossible: the graph is too short in time for that many ranks; a
+// balanced split that cannot be split further falls back to the midpoint.
+bool part_split(int lo, int hi, const std::vector<int32_t>& maxnb, int nr, bool balanced, int& m_out,
+                int& s_out) {
   const int n = hi - lo;
   if (n < 3) return false;
-  const int m = lo + n / 2;
-  int reach = m - 1;
-  for (int t = lo; t < m; ++t) reach = std::max(reach, std::min(maxnb[t], hi - 1));
-  const int s_end = reach + 1;
-  if (hi - s_end < 1 || s_end <= m) return false;
   const int nl = nr / 2;
-  if (!nd_order_part(lo, m, leaf, maxnb, nl, r0, out, owner)) return false;
-  if (!nd_order_part(s_end, hi, leaf, maxnb, nr - nl, r0 + nl, out, owner)) return false;
+  auto sep_end = [&](int m) {   // separator [m, s_end) of a split at m
+    int reach = m - 1;
+    for (int t = lo; t < m; ++t) reach = std::max(reach, std::min(maxnb[t], hi - 1));
+    return reach + 1;
+  };
+  int m = lo + n / 2;
+  if (balanced) {
+    std::vector<double> wp(static_cast<size_t>(n) + 1, 0.0);   // prefix work
+    int env = lo;   // the envelope: rows a column can fill down to
+    for (int t = lo; t < hi; ++t) {
+      env = std::max(env, std::min(maxnb[t], hi - 1));
+      const double r = env - t + 1;
+      wp[t - lo + 1] = wp[t - lo] + r * r;
+    }
+    double best = -1.0, at_mid = -1.0;
+    int bm = m;
+    int reach = lo;   // running max over [lo, mm) of the clipped neighbour reach
+    for (int mm = lo + 1; mm < hi - 1; ++mm) {
+      reach = std::max(reach, std::min(maxnb[mm - 1], hi - 1));
+      const int se = std::max(reach, mm - 1) + 1;
+      if (se <= mm || hi - se < 1) continue;
+      // each side's subtree must split again for its ranks (>= 3 tiles)
+      if ((nl > 1 && mm - lo < 3) || (nr - nl > 1 && hi - se < 3)) continue;
+      const double c = std::max((wp[mm - lo] - wp[0]) / nl, (wp[n] - wp[se - lo]) / (nr - nl));
+      if (mm == m) at_mid = c;
+      if (best < 0.0 || c < best) {
+        best = c;
+        bm = mm;
+      }
+    }
+    // the estimate is rough: a graph of even density keeps the midpoint
+    // (within 15 % of the best estimate, the exact schedules favour it)
+    if (best >= 0.0 && (at_mid < 0.0 || best < 0.85 * at_mid)) m = bm;
+  }
+  const int s_end = sep_end(m);
+  if (hi - s_end < 1 || s_end <= m) return false;
+  m_out = m;
+  s_out = s_end;
+  return true;
+}
+
+bool nd_order_part_b(int lo, int hi, int leaf, const std::vector<int32_t>& maxnb, int nr, int r0,
+                     std::vector<int32_t>& out, std::vector<int32_t>& owner, bool balanced) {
+  if (nr == 1) {
+    nd_order(lo, hi, leaf, maxnb, out);
+    owner.resize(out.size(), r0);
+    return true;
+  }
+  int m = 0, s_end = 0;
+  if (!part_split(lo, hi, maxnb, nr, balanced, m, s_end)) return false;
+  const int nl = nr / 2;
+  const size_t o0 = out.size();
+  if (!nd_order_part_b(lo, m, leaf, maxnb, nl, r0, out, owner, balanced) ||
+      !nd_order_part_b(s_end, hi, leaf, maxnb, nr - nl, r0 + nl, out, owner, balanced)) {
+    out.resize(o0);
+    owner.resize(o0);
+    // the balanced split left a side that cannot split again: the midpoint
+    return balanced && nd_order_part_b(lo, hi, leaf, maxnb, nr, r0, out, owner, false);
+  }
   for (int t = m; t < s_end; ++t) {
     out.push_back(t);
     owner.push_back(-1);
   }
   return true;
+}
+
+bool nd_order_part(int lo, int hi, int leaf, const std::vector<int32_t>& maxnb, int nr, int r0,
+                   std::vector<int32_t>& out, std::vector<int32_t>& owner) {
+  static const bool balanced = [] {
+    const char* e = std::getenv("DYNOHIP_PART_BALANCE");   // 0: split at the midpoint tile (round 3)
+    return !(e && e[0] == '0');
+  }();
+  return nd_order_part_b(lo, hi, leaf, maxnb, nr, r0, out, owner, balanced);
 }
 
 void schedule(int NT, const std::vector<std::vector<int32_t>>& adj, const std::vector<int32_t>& maxnb, int leaf,
@@ -610,31 +672,16 @@ std::vector<int32_t> tile_maxnb(const Plan& P) {
   return maxnb;
 }
 
-// the tile owners of nd_order_part's top splits (in natural tile order)
-bool owners_part(int lo, int hi, const std::vector<int32_t>& maxnb, int nr, int r0, std::vector<int32_t>& owner) {
-  if (nr == 1) {
-    for (int t = lo; t < hi; ++t) owner[t] = r0;
-    return true;
-  }
-  const int n = hi - lo;
-  if (n < 3) return false;
-  const int m = lo + n / 2;
-  int reach = m - 1;
-  for (int t = lo; t < m; ++t) reach = std::max(reach, std::min(maxnb[t], hi - 1));
-  const int s_end = reach + 1;
-  if (hi - s_end < 1 || s_end <= m) return false;
-  const int nl = nr / 2;
-  if (!owners_part(lo, m, maxnb, nl, r0, owner)) return false;
-  if (!owners_part(s_end, hi, maxnb, nr - nl, r0 + nl, owner)) return false;
-  for (int t = m; t < s_end; ++t) owner[t] = -1;
-  return true;
-}
-
 }  // namespace
 
+// the tile owners of nd_order_part's top splits (in natural tile order)
 bool partition_tile_owners(const Plan& P, int nranks, std::vector<int32_t>& owner) {
   owner.assign(P.NT, 0);
-  return owners_part(0, P.NT, tile_maxnb(P), std::max(1, nranks), 0, owner);
+  if (nranks <= 1) return true;
+  std::vector<int32_t> out, own;
+  if (!nd_order_part(0, P.NT, 0, tile_maxnb(P), nranks, 0, out, own)) return false;
+  for (size_t q = 0; q < out.size(); ++q) owner[out[q]] = own[q];
+  return true;
 }
 
 bool build_tile_schedule(Plan& P, bool own_threads) {
