@@ -251,6 +251,10 @@ void launch_tile_forward(const TileDev& b, const TileSchedDev& sd, const std::ve
                          const std::vector<int32_t>& fpanels, double* Linv, const double* r, double* contrib,
                          double* y, int* fail, hipStream_t s, hipStream_t side, hipEvent_t ev_main,
                          hipEvent_t ev_side);
+// the whole reduced solve of a system of <= kSmallNT tiles in one workgroup
+// (x = A^-1 r in natural tile order; tilechol.hip k_small_solve)
+constexpr int kSmallNT = 4;
+void launch_small_solve(const TileDev& b, const double* r, double* x, int* fail, hipStream_t s);
 void launch_tile_backward(const TileDev& b, const TileSchedDev& sd, const std::vector<int32_t>& blevel,
                           const double* Linv, const double* y, double* x, int* fail, hipStream_t s);
 void launch_tile_cholesky_solve(const TileDev& b, const TileSchedDev& sd, const std::vector<int32_t>& flevel,

@@ -443,6 +443,7 @@ struct dynohip_solver {
   DevBuf<int32_t> witems;   // k_back_wide's (first part, parts) items
   std::vector<int32_t> witems_h;   // their host copy (read by Uploads::run)
   bool back_wide = true;    // DYNOHIP_BACK_WIDE=0: one part per workgroup (k_back_poll)
+  bool small_solve = true;  // DYNOHIP_SMALL_SOLVE=0: systems of <= kSmallNT tiles on the tile DAG too
   DevBuf<double> bpartials;
   DevBuf<int> arrive;
   DevBuf<int32_t> fdep_start, fdep, fqueue;
@@ -906,6 +907,11 @@ int enqueue_try(dynohip_solver* s, double lambda) {
     // exchange between them)
     if (timed) (void)hipEventRecord(s->ev[5], st);
     launch_tile_backward(s->bd, s->sd, P.bplevel, s->linv.p, y, x, s->failp, st);
+  } else if (s->small_solve && P.NT >= 1 && P.NT <= kSmallNT) {
+    // a window-sized system: factorisation and both substitutions in one
+    // workgroup (k_small_solve; ms_cholesky spans all of it)
+    launch_small_solve(s->bd, s->gred.p, x, s->failp, st);
+    if (timed) (void)hipEventRecord(s->ev[5], st);
   } else {
     launch_tile_forward(s->bd, s->sd, P.flevel, P.fpanels, s->linv.p, s->gred.p, s->contrib.p, y, s->failp, st,
                         s->side, s->ev_main, s->ev_side);
@@ -1231,6 +1237,7 @@ int dynohip_create(int device_id, dynohip_solver** out) {
   if (const char* e = std::getenv("DYNOHIP_BACK_POLL")) s->sd.back_poll = std::atoi(e) != 0;
   if (const char* e = std::getenv("DYNOHIP_CHAIN_LONE")) s->chain_lone = std::atoi(e) != 0;
   if (const char* e = std::getenv("DYNOHIP_BACK_WIDE")) s->back_wide = std::atoi(e) != 0;
+  if (const char* e = std::getenv("DYNOHIP_SMALL_SOLVE")) s->small_solve = std::atoi(e) != 0;
   s->stream = r.stream;
   s->side = r.side;
   s->ev_main = r.ev_main;

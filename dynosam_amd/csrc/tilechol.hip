@@ -20,6 +20,8 @@
 // like GTSAM's IndeterminantLinearSystemException path.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "kernels.hpp"
 
 namespace dynohip {
@@ -1471,6 +1473,224 @@ __global__ __launch_bounds__(kBackWide) void k_back_wide(TileDev b, const BackPa
   if (tid == 0 && bad) atomicOr(fail, 2);
 }
 
+// ---- small reduced systems (<= kSmallNT tiles): one workgroup ------------
+// The sliding-window solves (backend.flags: 10-frame windows) have reduced
+// systems of at most four tiles, where the tile DAG is a chain of four
+// dependent panels with a global-memory hand-off between each, and the
+// backward substitution four more. k_small_solve does the whole solve in
+// one workgroup of 8 waves instead, the matrix resident in registers:
+//   * the position-ordered matrix as 16x16 blocks in MFMA accumulator
+//     layout (upper triangle, A = U^T U): wave w holds diagonal blocks
+//     w and w + 8 and 15 off-diagonal blocks (enumerated by row, last row
+//     first, dealt round-robin, so every block step leaves each wave a
+//     similar share of the trailing update);
+//   * block step K: the owner of block (K,K) factors it in-wave
+//     (factor16_wave: U_KK and W = U_KK^-1) and forms y_K = W^T r_K; after a
+//     barrier the owners of row K form U[K][J] = W^T A[K][J] into LDS; after
+//     a second barrier every wave applies A[I][J] -= U[K][I]^T U[K][J] and
+//     r_I -= U[K][I]^T y_K to its blocks. The owner of block K+1 updates it
+//     first and factors it at once, ahead of its other updates (lookahead);
+//   * backward, x_K = W_K (y_K - sum_{J>K} U[K][J] x_J): each product
+//     U[K][J] x_J is formed by the block's owner as soon as x_J is out, and
+//     the owner of block K adds them in J order.
+// The forward substitution is the factorisation's extra right-hand-side
+// column; no L^-1 is stored and the backward substitution needs no other
+// launch. Results match the tile DAG's to rounding (another summation
+// order); DYNOHIP_SMALL_SOLVE=0 keeps the DAG.
+constexpr int kSmallNB = 4 * kSmallNT;   // 16x16 blocks per dimension
+constexpr int kSmallWaves = 8;
+constexpr int kSmallOff = (kSmallNB * (kSmallNB - 1) / 2) / kSmallWaves;   // off-diagonal blocks per wave
+static_assert(kSmallOff * kSmallWaves == kSmallNB * (kSmallNB - 1) / 2 && kSmallNB <= 2 * kSmallWaves,
+              "the small solve's block deal");
+
+// off-diagonal block k of the enumeration by row I from the last, then J
+__device__ __forceinline__ void small_off_block(int k, int& I, int& J) {
+  int i = kSmallNB - 2, base = 0;
+  while (k >= base + (kSmallNB - 1 - i)) {
+    base += kSmallNB - 1 - i;
+    --i;
+  }
+  I = i;
+  J = i + 1 + (k - base);
+}
+
+template <int D>
+using small_ic = std::integral_constant<int, D>;
+
+__global__ __launch_bounds__(kSmallWaves * 64) void k_small_solve(TileDev b, const double* __restrict__ r,
+                                                                  double* __restrict__ x, int* fail) {
+  __shared__ double Ws[kSmallNB][256];             // W_K = U_KK^-1 of every block step
+  __shared__ double ys[kSmallNB * 16];             // y
+  __shared__ double Ur[2][kSmallNB + 1][256];      // row K of U (+ y_K at [kSmallNB])
+  __shared__ double dscr[kSmallWaves][16];
+  __shared__ double pb[kSmallNB][kSmallNB][16];    // U[I][J] x_J, I < J
+  __shared__ double xv[kSmallNB * 16];
+  __shared__ double tv[16];
+  __shared__ int ord[kSmallNT];
+  __shared__ int sslot[kSmallNT][kSmallNT];
+  const int tid = threadIdx.x;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63;
+  const int NT = b.NT, nb = 4 * NT;
+  const int li = l & 15, g = l >> 4;
+  if (tid < NT) ord[b.pos[tid]] = tid;
+  __syncthreads();
+  if (tid < NT * NT) {
+    // the stored tile of position block (p, q), p <= q: (row tile ord[q], column tile ord[p])
+    const int p = tid / NT, q = tid % NT;
+    int sl = -1;
+    if (p <= q) {
+      const int tp = ord[p], tq = ord[q];
+      for (int e = b.row_start[tq]; e < b.row_start[tq + 1]; ++e)
+        if (b.row_col[e] == tp) sl = b.row_slot[e];
+    }
+    sslot[p][q] = sl;
+  }
+  __syncthreads();
+  // block (I, J), I <= J, of the position-ordered matrix
+  auto load_blk = [&](int I, int J) {
+    v4d v = v4d{0.0, 0.0, 0.0, 0.0};
+    const int p = I >> 2, q = J >> 2, sl = sslot[p][q];
+    if (sl < 0) return v;
+    const double* t = slot_ptr(b, sl);
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int a = 16 * (I & 3) + g + 4 * rr, c = 16 * (J & 3) + li;
+      v[rr] = p == q ? t[a * T + c] : t[c * T + a];
+    }
+    return v;
+  };
+  auto load_rhs = [&](int I) {
+    v4d v = v4d{0.0, 0.0, 0.0, 0.0};
+    if (li == 0) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) v[rr] = r[static_cast<int64_t>(ord[I >> 2]) * T + 16 * (I & 3) + g + 4 * rr];
+    }
+    return v;
+  };
+  const v4d zero = v4d{0.0, 0.0, 0.0, 0.0};
+  v4d Dg[2], Rg[2], O[kSmallOff];
+  int oI[kSmallOff], oJ[kSmallOff];
+#pragma unroll
+  for (int s = 0; s < kSmallOff; ++s) {
+    small_off_block(kSmallWaves * s + w, oI[s], oJ[s]);
+    if (oJ[s] >= nb) oI[s] = -1;   // outside this system
+    O[s] = oI[s] >= 0 ? load_blk(oI[s], oJ[s]) : zero;
+  }
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {
+    const int K = w + kSmallWaves * d;
+    Dg[d] = K < nb ? load_blk(K, K) : zero;
+    Rg[d] = K < nb ? load_rhs(K) : zero;
+  }
+  bool ok = true;
+  // the owner of diagonal block K = w + 8d: U_KK, W, y_K = W^T r_K (y_K
+  // also into buffer buf for the step's right-hand-side updates)
+  auto factor = [&](auto dc, int buf) {
+    constexpr int d = decltype(dc)::value;
+    const int K = w + kSmallWaves * d;
+    v4d Wm;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) Wm[rr] = (g + 4 * rr == li) ? 1.0 : 0.0;
+    factor16_wave(Dg[d], Wm, l, ok, &dscr[w][0]);
+    st_blk(&Ws[K][0], Wm, l);
+    const v4d Y = mfma_tn(Wm, Rg[d], zero, false);
+    st_blk(&Ur[buf][kSmallNB][0], Y, l);
+    if (li == 0) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) ys[16 * K + g + 4 * rr] = Y[rr];
+    }
+  };
+  // step K's update of diagonal block w + 8d and its right-hand side
+  auto diag_update = [&](auto dc, int K, int buf) {
+    constexpr int d = decltype(dc)::value;
+    const int Kd = w + kSmallWaves * d;
+    if (Kd > K && Kd < nb) {
+      const v4d Uk = ld_blk(&Ur[buf][Kd][0], l);
+      Dg[d] = mfma_tn(Uk, Uk, Dg[d], true);
+      Rg[d] = mfma_tn(Uk, ld_blk(&Ur[buf][kSmallNB][0], l), Rg[d], true);
+    }
+  };
+  if (w == 0 && nb > 0) factor(small_ic<0>{}, 0);
+  for (int K = 0; K < nb; ++K) {
+    const int buf = K & 1;
+    __syncthreads();   // W_K, y_K out
+    const v4d Wc = ld_blk(&Ws[K][0], l);
+#pragma unroll
+    for (int s = 0; s < kSmallOff; ++s)
+      if (oI[s] == K) {
+        O[s] = mfma_tn(Wc, O[s], zero, false);
+        st_blk(&Ur[buf][oJ[s]][0], O[s], l);
+      }
+    __syncthreads();   // row K of U out
+    const int K1 = K + 1;
+    const bool next = K1 < nb && w == (K1 & (kSmallWaves - 1));
+    if (next) {
+      // lookahead: block K+1 updated and factored before this wave's other updates
+      if (K1 < kSmallWaves) {
+        diag_update(small_ic<0>{}, K, buf);
+        factor(small_ic<0>{}, buf ^ 1);
+        diag_update(small_ic<1>{}, K, buf);
+      } else {
+        diag_update(small_ic<1>{}, K, buf);
+        factor(small_ic<1>{}, buf ^ 1);
+        diag_update(small_ic<0>{}, K, buf);
+      }
+    } else {
+      diag_update(small_ic<0>{}, K, buf);
+      diag_update(small_ic<1>{}, K, buf);
+    }
+#pragma unroll
+    for (int s = 0; s < kSmallOff; ++s)
+      if (oI[s] > K)
+        O[s] = mfma_tn(ld_blk(&Ur[buf][oI[s]][0], l), ld_blk(&Ur[buf][oJ[s]][0], l), O[s], true);
+  }
+  if (!ok && l == 0) *fail = 1;
+  // backward substitution
+  auto solve_x = [&](int K) {
+    if (li == 0) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int row = g + 4 * rr;
+        double t = ys[16 * K + row];
+        for (int J = K + 1; J < nb; ++J) t -= pb[K][J][row];
+        tv[row] = t;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const double tc = tv[li];
+    const v4d Wk = ld_blk(&Ws[K][0], l);
+    double xr[4];
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) xr[rr] = sum16(Wk[rr] * tc);
+    if (li == 0) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int row = g + 4 * rr;
+        xv[16 * K + row] = xr[rr];
+        x[static_cast<int64_t>(ord[K >> 2]) * T + 16 * (K & 3) + row] = xr[rr];
+      }
+    }
+  };
+  for (int K = nb - 1; K >= 0; --K) {
+    const int J = K + 1;
+    if (J < nb) {
+      const double xj = xv[16 * J + li];
+#pragma unroll
+      for (int s = 0; s < kSmallOff; ++s)
+        if (oJ[s] == J && oI[s] >= 0) {
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) {
+            const double pr = sum16(O[s][rr] * xj);
+            if (li == 0) pb[oI[s]][J][g + 4 * rr] = pr;
+          }
+        }
+    }
+    __syncthreads();   // every U[K][J] x_J out
+    if (w == (K & (kSmallWaves - 1))) solve_x(K);
+    __syncthreads();   // x_K out
+  }
+}
+
 }  // namespace
 
 #ifdef DYNOHIP_TASK_CLOCK
@@ -1548,6 +1768,11 @@ void launch_tile_backward(const TileDev& b, const TileSchedDev& sd, const std::v
     const int n = blevel[lv + 1] - blevel[lv];
     if (n > 0) k_back<<<n, kBackThreads, 0, s>>>(b, sd.bpart + blevel[lv], sd.bent, Linv, y, x, sd.partials, sd.arrive);
   }
+}
+
+void launch_small_solve(const TileDev& b, const double* r, double* x, int* fail, hipStream_t s) {
+  if (b.NT <= 0 || b.NT > kSmallNT) return;   // the host checks the size (solver.cpp)
+  k_small_solve<<<1, kSmallWaves * 64, 0, s>>>(b, r, x, fail);
 }
 
 void launch_tile_cholesky_solve(const TileDev& b, const TileSchedDev& sd, const std::vector<int32_t>& flevel,

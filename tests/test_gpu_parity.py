@@ -15,7 +15,7 @@ import pytest
 
 from dynosam_amd import _abi, synth
 from dynosam_amd.graph import NonlinearFactorGraph, Values
-from dynosam_amd.optimizer import DynohipError, Solver
+from dynosam_amd.optimizer import DynohipError, Solver, plan_export
 from oracle_binding import Oracle, pose_compose, pose_expmap
 from graphs_extra import mixed_lone_graph
 
@@ -410,6 +410,45 @@ def test_execution_paths_agree(gpu_available, name, monkeypatch):
         s.close()
     for r in results[1:]:
         assert np.array_equal(r, results[0])
+
+
+SMALL_GRAPHS = [("T1", {}), (None, dict(frames=8, objects=1, static_landmarks=80, dyn_slots=4)),
+                (None, dict(frames=10, objects=3, static_landmarks=150, dyn_slots=6))]
+
+
+@pytest.mark.parametrize("name,kw", SMALL_GRAPHS)
+def test_small_solve_matches_tile_dag(gpu_available, name, kw, monkeypatch):
+    """Reduced systems of at most four tiles (the sliding windows) are solved
+    in one workgroup (k_small_solve: factorisation and both substitutions,
+    the matrix in registers) instead of on the tile DAG. Same system, other
+    summation order: one damped solve at three lambdas agrees to rounding
+    (1e-10 relative), and the free-running LM takes the same tries with
+    values within 1e-9 of each other."""
+    g, v, _ = synth.generate(name, **kw)
+    nt = int(plan_export(g, v, "info")[1])
+    assert 1 <= nt <= 4, nt
+    runs = []
+    for small in ("1", "0"):
+        monkeypatch.setenv("DYNOHIP_SMALL_SOLVE", small)
+        s = Solver(0)
+        s.set_graph(g)
+        s.set_values(v)
+        deltas = []
+        for lam in (1e-5, 1e-3, 1e-1):
+            ok, d = s.solve_delta(lam)
+            assert ok
+            deltas.append(d)
+        r = s.optimize()
+        runs.append((deltas, r, s.values_data(), [(e["lam"], e["accepted"]) for e in s.trace()]))
+        s.close()
+    (da, ra, va, ta), (db, rb, vb, tb) = runs
+    for x, y in zip(da, db):
+        print(name, kw, nt, f"delta rel {rel(x, y):.2e}")
+        assert rel(x, y) < 1e-10
+    assert ta == tb
+    assert (ra.iterations, ra.inner_iterations) == (rb.iterations, rb.inner_iterations)
+    assert rel(va, vb) < 1e-9
+    assert ra.final_error == pytest.approx(rb.final_error, rel=1e-9)
 
 
 def first_divergence(tg, to):
