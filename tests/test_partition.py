@@ -232,6 +232,18 @@ def test_partitioned_replay_eight_ranks():
     replay_partitioned("C2", 8, seed=11)
 
 
+def test_partitioned_replay_uneven_density():
+    """Objects visible in the first third of the frames only: the early
+    frames carry more poses per frame and a wider band, so the splits are
+    placed by estimated work (tiles.cpp part_split), not at the middle tile,
+    and the early ranks get fewer tiles. The replayed solve is still exact."""
+    plans, _, _ = replay_partitioned(None, 4, frames=120, objects=6, static_landmarks=4000, dyn_slots=8,
+                                     object_visible_frames=40)
+    own = plans[0]["tile_owner"]
+    tiles = [int((own == r).sum()) for r in range(4)]
+    assert tiles[0] + tiles[1] < tiles[2] + tiles[3], tiles
+
+
 def test_partition_ownership():
     graph, values, _ = synth.generate("C2")
     nranks = 4
