@@ -421,13 +421,22 @@ def test_small_solve_matches_tile_dag(gpu_available, name, kw, monkeypatch):
     """Reduced systems of at most four tiles (the sliding windows) are solved
     in one workgroup (k_small_solve: factorisation and both substitutions,
     the matrix in registers) instead of on the tile DAG. Same system, other
-    summation order: one damped solve at three lambdas agrees to rounding
-    (1e-10 relative; observed ~1e-13), and the free-running LM takes the
-    same tries, ending within the north-star 1e-6 of each other (the runs
-    drift apart through their accumulated rounding: 2.6e-9 on T1)."""
+    summation order: one damped solve at three lambdas, each path against
+    the exact step (the oracle's Schur solve in x87 extended precision): the
+    one-workgroup solve is as accurate as the DAG (within 4x its distance,
+    or 1e-12); and the free-running LM takes the same tries, ending within
+    the north-star 1e-6 of each other (the runs drift apart through their
+    accumulated rounding: 2.6e-9 on T1)."""
     g, v, _ = synth.generate(name, **kw)
     nt = int(plan_export(g, v, "info")[1])
     assert 1 <= nt <= 4, nt
+    o = Oracle(g, v)
+    lams = (1e-5, 1e-3, 1e-1)
+    exact = []
+    for lam in lams:
+        ok_l, dl = o.solve_damped_ld(lam)
+        assert ok_l
+        exact.append(dl)
     runs = []
     for small in ("1", "0"):
         monkeypatch.setenv("DYNOHIP_SMALL_SOLVE", small)
@@ -435,7 +444,7 @@ def test_small_solve_matches_tile_dag(gpu_available, name, kw, monkeypatch):
         s.set_graph(g)
         s.set_values(v)
         deltas = []
-        for lam in (1e-5, 1e-3, 1e-1):
+        for lam in lams:
             ok, d = s.solve_delta(lam)
             assert ok
             deltas.append(d)
@@ -443,9 +452,10 @@ def test_small_solve_matches_tile_dag(gpu_available, name, kw, monkeypatch):
         runs.append((deltas, r, s.values_data(), [(e["lam"], e["accepted"]) for e in s.trace()]))
         s.close()
     (da, ra, va, ta), (db, rb, vb, tb) = runs
-    for x, y in zip(da, db):
-        print(name, kw, nt, f"delta rel {rel(x, y):.2e}")
-        assert rel(x, y) < 1e-10
+    for lam, x, y, e in zip(lams, da, db, exact):
+        es, ed = rel(x, e), rel(y, e)
+        print(name, kw, nt, f"lambda {lam:.0e}: small vs DAG {rel(x, y):.2e}, to the exact step: small {es:.2e}, DAG {ed:.2e}")
+        assert es <= max(1e-12, 4 * ed)
     assert ta == tb
     assert (ra.iterations, ra.inner_iterations) == (rb.iterations, rb.inner_iterations)
     print(name, kw, nt, f"free run values rel {rel(va, vb):.2e}")
