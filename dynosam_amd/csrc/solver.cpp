@@ -443,7 +443,7 @@ struct dynohip_solver {
   DevBuf<int32_t> witems;   // k_back_wide's (first part, parts) items
   std::vector<int32_t> witems_h;   // their host copy (read by Uploads::run)
   bool back_wide = true;    // DYNOHIP_BACK_WIDE=0: one part per workgroup (k_back_poll)
-  bool small_solve = true;  // DYNOHIP_SMALL_SOLVE=0: systems of <= kSmallNT tiles on the tile DAG too
+  bool small_solve = false; // DYNOHIP_SMALL_SOLVE=1: systems of <= kSmallNT tiles in one workgroup (slower)
   DevBuf<double> bpartials;
   DevBuf<int> arrive;
   DevBuf<int32_t> fdep_start, fdep, fqueue;

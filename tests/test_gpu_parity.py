@@ -419,8 +419,8 @@ SMALL_GRAPHS = [("T1", {}), (None, dict(frames=8, objects=1, static_landmarks=80
 @pytest.mark.parametrize("name,kw", SMALL_GRAPHS)
 def test_small_solve_matches_tile_dag(gpu_available, name, kw, monkeypatch):
     """Reduced systems of at most four tiles (the sliding windows) are solved
-    in one workgroup (k_small_solve: factorisation and both substitutions,
-    the matrix in registers) instead of on the tile DAG. Same system, other
+    in one workgroup (k_small_solve, opt-in: factorisation and both
+    substitutions, the matrix in registers) instead of on the tile DAG. Same system, other
     summation order: one damped solve at three lambdas, each path against
     the exact step (the oracle's Schur solve in x87 extended precision): the
     one-workgroup solve is as accurate as the DAG (within 4x its distance,
