@@ -442,7 +442,7 @@ struct dynohip_solver {
   DevBuf<BackPart> bpart;
   DevBuf<int32_t> witems;   // k_back_wide's (first part, parts) items
   std::vector<int32_t> witems_h;   // their host copy (read by Uploads::run)
-  bool back_wide = true;    // DYNOHIP_BACK_WIDE=0: one part per workgroup (k_back_poll)
+  bool back_wide = false;   // DYNOHIP_BACK_WIDE=1: two parts per workgroup (k_back_wide; measured no faster)
   bool small_solve = false; // DYNOHIP_SMALL_SOLVE=1: systems of <= kSmallNT tiles in one workgroup (slower)
   DevBuf<double> bpartials;
   DevBuf<int> arrive;
