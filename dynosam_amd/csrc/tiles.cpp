@@ -184,8 +184,21 @@ bool nd_order_part(int lo, int hi, int leaf, const std::vector<int32_t>& maxnb, 
   return nd_order_part_b(lo, hi, leaf, maxnb, nr, r0, out, owner, balanced);
 }
 
+constexpr int kUpdGroupTiles = 128;   // systems of this many tiles and more group update levels
+
 void schedule(int NT, const std::vector<std::vector<int32_t>>& adj, const std::vector<int32_t>& maxnb, int leaf,
               Sched& S, int nranks = 1) {
+  // levels of contributions per update task: large systems are throughput-
+  // bound in the dataflow launch (NS: 11.5k update tasks, a top-separator
+  // tile's chain of 22 one-level updates on the critical path), where two
+  // levels per task measured best (NS factorisation 0.809 -> 0.740 ms;
+  // 3: 0.745, 4: 0.747, 6: 0.805); small ones are latency-bound and keep one
+  // (C2: 1: 0.289, 2: 0.291, 3: 0.297 ms). DYNOHIP_UPD_GROUP overrides.
+  static const int32_t upd_env = [] {
+    const char* e = std::getenv("DYNOHIP_UPD_GROUP");
+    return e ? std::max(1, std::atoi(e)) : 0;
+  }();
+  const int32_t upd_group = upd_env > 0 ? upd_env : (NT >= kUpdGroupTiles ? 2 : 1);
   S.leaf = leaf;
   S.order.clear();
   S.owner.clear();
@@ -299,15 +312,21 @@ void schedule(int NT, const std::vector<std::vector<int32_t>>& adj, const std::v
   auto plan_tile = [&](int32_t sl, int32_t P, int32_t* aoff, int32_t* an, int32_t town) {
     all.assign(cpool.begin() + cstart[sl], cpool.begin() + cfill[sl]);
     std::sort(all.begin(), all.end(), [](const Contrib& x, const Contrib& y) { return x.R < y.R; });
+    // an update task takes the contributions ready within upd_group levels
+    // of its first one (1: one task per distinct ready level), so a tile fed
+    // at many levels has a shorter read-modify-write chain of update tasks
     auto emit_updates = [&](const std::vector<Contrib>& v, size_t& q, int32_t limitR, int32_t own) {
       while (q < v.size() && v[q].R <= limitR) {
-        const int32_t t = v[q].R + 1;
-        LT u{t, TileTask{1, -1, -1, sl, -1, 0, 0, 0, 0, 0}, 0, 0, pool_pairs(), 0, own};
-        while (q < v.size() && v[q].R <= t - 1) {
+        const int32_t last = std::min(limitR, v[q].R + upd_group - 1);
+        LT u{0, TileTask{1, -1, -1, sl, -1, 0, 0, 0, 0, 0}, 0, 0, pool_pairs(), 0, own};
+        int32_t rmax = v[q].R;
+        while (q < v.size() && v[q].R <= last) {
+          rmax = std::max(rmax, v[q].R);
           ppool.push_back(v[q].a);
           ppool.push_back(v[q].b);
           ++q;
         }
+        u.lvl = rmax + 1;
         u.po_n = pool_pairs() - u.po_off;
         tasks.push_back(u);
       }
@@ -530,7 +549,20 @@ void build_dataflow_deps(const Plan& P, const std::vector<TileTask>& ftask, cons
 // estimated costs (us, MI355X task clock): a panel and an update task
 // without operand pairs, a 64^3 operand pair, a write-to-reader hand-off
 // (the NS rate moved < 0.5% over panel 16-20, update 5.5-11, hand-off 2.5-6)
-constexpr double kQPanel = 16.0, kQUpdate = 5.5, kQPair = 1.7, kQHandoff = 2.5;
+// the queue order's cost model (us): a panel, an update, per pending pair, a
+// hand-off. DYNOHIP_QCOST="panel,update,pair,handoff" overrides it (tuning).
+struct QCost {
+  double panel = 16.0, update = 5.5, pair = 1.7, handoff = 2.5;
+};
+const QCost& qcost() {
+  static const QCost c = [] {
+    QCost q;
+    if (const char* e = std::getenv("DYNOHIP_QCOST"))
+      std::sscanf(e, "%lf,%lf,%lf,%lf", &q.panel, &q.update, &q.pair, &q.handoff);
+    return q;
+  }();
+  return c;
+}
 constexpr int kQueueSimMax = 100000;
 std::vector<int32_t> queue_order(const Plan& P, const std::vector<TileTask>& ftask,
                                  const std::vector<int32_t>& flevel, const std::vector<int32_t>& fdep_start,
@@ -546,7 +578,7 @@ std::vector<int32_t> queue_order(const Plan& P, const std::vector<TileTask>& fta
   for (int q = 0; q < n; ++q) {
     const TileTask& t = ftask[q];
     const int np = (t.pd_end - t.pd_beg) + (t.po_end - t.po_beg);
-    dur[q] = (t.kind == 0 ? kQPanel : kQUpdate) + kQPair * np;
+    dur[q] = (t.kind == 0 ? qcost().panel : qcost().update) + qcost().pair * np;
   }
   // predecessor lists (the writer of each awaited write, counted in level order)
   std::vector<int32_t> wcount(P.n_slots, 0), wstart(P.n_slots + 1, 0);
@@ -573,7 +605,7 @@ std::vector<int32_t> queue_order(const Plan& P, const std::vector<TileTask>& fta
   std::vector<double> rem(n, 0.0);
   for (int q = n - 1; q >= 0; --q) {
     double m = 0.0;
-    for (int32_t j = sstart[q]; j < sstart[q + 1]; ++j) m = std::max(m, kQHandoff + rem[succ[j]]);
+    for (int32_t j = sstart[q]; j < sstart[q + 1]; ++j) m = std::max(m, qcost().handoff + rem[succ[j]]);
     rem[q] = dur[q] + m;
   }
   // list scheduling: ready heap by remaining path; tasks whose inputs are
@@ -621,7 +653,7 @@ std::vector<int32_t> queue_order(const Plan& P, const std::vector<TileTask>& fta
     ++done;
     for (int32_t j = sstart[fin.second]; j < sstart[fin.second + 1]; ++j) {
       const int32_t sq = succ[j];
-      rdy[sq] = std::max(rdy[sq], now + kQHandoff);
+      rdy[sq] = std::max(rdy[sq], now + qcost().handoff);
       if (--npred[sq] == 0) {
         pending.push_back({rdy[sq], sq});
         std::push_heap(pending.begin(), pending.end(), later);

@@ -162,6 +162,22 @@ def test_schedule_replay_solves(name, leaf):
     assert np.allclose(x, ref, rtol=1e-9, atol=1e-10)
 
 
+def test_large_system_grouped_updates_replay_solves():
+    """A system of >= 128 tiles (tiles.cpp kUpdGroupTiles): its update tasks
+    take the contributions of two ready levels each. The replay still solves
+    exactly, and the grouping leaves fewer update tasks than ready levels."""
+    sched = schedule_for(None, 16, frames=360, objects=3, static_landmarks=6000, dyn_slots=4)
+    ft = sched["ftask"].reshape(-1, 10)
+    assert sched["n_tiles"] >= 128, sched["n_tiles"]
+    rng = np.random.default_rng(9)
+    M = random_reduced(sched, rng)
+    rhs = rng.standard_normal(M.shape[0])
+    x = replay(sched, M, rhs)
+    assert np.allclose(x, np.linalg.solve(M, rhs), rtol=1e-9, atol=1e-10)
+    upd = ft[ft[:, 0] == 1]
+    assert (upd[:, 8] - upd[:, 7]).max() >= 2   # some update applies contributions of two levels
+
+
 def test_llworld_schedule_replay():
     sched = schedule_for("C1", 4, formulation=1)
     rng = np.random.default_rng(3)
