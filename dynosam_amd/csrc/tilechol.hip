@@ -453,9 +453,34 @@ __device__ __forceinline__ void load_tiles_lds(const double* s0, double* d0, con
   if (s3) put(3, d3);
 }
 
+// a 64x64 tile into registers (16 bytes per load, 8 per thread) and from
+// them into LDS (row stride LD)
+template <bool SC1>
+__device__ __forceinline__ void tile_regs(const double* __restrict__ src, d2v (&v)[8], int tid) {
+  if constexpr (SC1) {
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(uniform_ptr(src)), 0, T * T * 8, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      v[i] = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(rs, (tid + 256 * i) * 16, 0, 16));
+  } else {
+    const d2v* s2v = reinterpret_cast<const d2v*>(src);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = s2v[tid + 256 * i];
+  }
+}
+__device__ __forceinline__ void regs_tile(const d2v (&v)[8], double* d, int tid) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int e = tid + 256 * i, rr = (2 * e) / T, cc = (2 * e) % T;
+    d[rr * LD + cc] = v[i].x;
+    d[rr * LD + cc + 1] = v[i].y;
+  }
+}
+
 // dst -= sum over the task's pairs of A B^T: the destination and the first
-// pair's operands are fetched in one round trip; further pairs (rare) one
-// by one
+// pair's operands are fetched in one round trip; each further pair's while
+// the previous pair's MFMAs run
 struct NoWait {
   __device__ void operator()() const {}
 };
@@ -479,14 +504,33 @@ __device__ __forceinline__ void run_update(const TileDev& b, const TileTask& tk,
   late();
   v4d acc[2][2];
   zero_acc(acc);
-  for (int e = tk.po_beg; e < tk.po_end; ++e) {
-    const bool pre = e == tk.po_beg && pa0 >= 0;
-    const int32_t pa = pre ? pa0 : pairs[2 * e], pb = pre ? pb0 : pairs[2 * e + 1];
-    if (e > tk.po_beg) __syncthreads();
+  if (tk.po_end > tk.po_beg) {
+    const int32_t pa = pa0 >= 0 ? pa0 : pairs[2 * tk.po_beg], pb = pa0 >= 0 ? pb0 : pairs[2 * tk.po_beg + 1];
     load_tiles_lds<SC1>(slot_ptr(b, pa), Qs, pb != pa ? slot_ptr(b, pb) : nullptr, Rs, nullptr, nullptr, nullptr,
                         nullptr, tid);
     __syncthreads();
+  }
+  // pair e is in LDS; pair e + 1's tiles are loaded into registers while
+  // pair e's MFMAs run (grouped updates carry ~2 pairs: one round trip less)
+  for (int e = tk.po_beg; e < tk.po_end; ++e) {
+    const int32_t pa = e == tk.po_beg && pa0 >= 0 ? pa0 : pairs[2 * e];
+    const int32_t pb = e == tk.po_beg && pa0 >= 0 ? pb0 : pairs[2 * e + 1];
+    const bool more = e + 1 < tk.po_end;
+    d2v nv[2][8];
+    int32_t na = -1, nb = -1;
+    if (more) {
+      na = pairs[2 * (e + 1)];
+      nb = pairs[2 * (e + 1) + 1];
+      tile_regs<SC1>(slot_ptr(b, na), nv[0], tid);
+      if (nb != na) tile_regs<SC1>(slot_ptr(b, nb), nv[1], tid);
+    }
     mfma_abt_acc(Qs, pb != pa ? Rs : Qs, w, l, acc);
+    if (more) {
+      __syncthreads();
+      regs_tile(nv[0], Qs, tid);
+      if (nb != na) regs_tile(nv[1], Rs, tid);
+      __syncthreads();
+    }
   }
 #pragma unroll
   for (int ti = 0; ti < 2; ++ti)
