@@ -398,22 +398,6 @@ __device__ __forceinline__ void load_tile_lds_t(const double* __restrict__ src, 
   }
 }
 
-// sum over operand pairs [beg, end) of A B^T into acc (operands staged in
-// Qs / Rs; a pair with A == B is loaded once)
-template <bool SC1>
-__device__ __forceinline__ void sum_pairs(const TileDev& b, const int32_t* __restrict__ pairs, int beg, int end,
-                                          double* Qs, double* Rs, int tid, int w, int l, v4d acc[2][2]) {
-  zero_acc(acc);
-  for (int e = beg; e < end; ++e) {
-    const int32_t pa = pairs[2 * e], pb = pairs[2 * e + 1];
-    __syncthreads();
-    load_tile_lds_t<SC1>(slot_ptr(b, pa), Qs, tid);
-    if (pb != pa) load_tile_lds_t<SC1>(slot_ptr(b, pb), Rs, tid);
-    __syncthreads();
-    mfma_abt_acc(Qs, pb != pa ? Rs : Qs, w, l, acc);
-  }
-}
-
 // Issue the loads of up to four 64x64 tiles into LDS before any of the
 // stores, so their latencies overlap (one round trip instead of four). A
 // null source skips its tile. (Fixed operand positions, no pointer arrays:
@@ -823,12 +807,38 @@ __device__ __forceinline__ void panel_task(const TileDev& b, const TileTask& tk,
   }
   TCLK(6, q, rtc());
   if (!p.fast) {
-    // several pending pairs (rare): apply them one by one before the factor
+    // several pending pairs (the first column of a separator, fed by two
+    // subtrees at once): applied before the factor, the own tile and the
+    // first own pair fetched in one round trip, and each further operand
+    // tile fetched into registers while the previous one's MFMAs run
     if (own) {
-      load_tile_lds_t<SC1>(slot_ptr(b, tk.dst), As, tid);
-      if (tk.po_end > tk.po_beg) {
+      const bool hp = tk.po_end > tk.po_beg;
+      const int32_t pa0 = hp ? pairs[2 * tk.po_beg] : -1, pb0 = hp ? pairs[2 * tk.po_beg + 1] : -1;
+      load_tiles_lds<SC1>(slot_ptr(b, tk.dst), As, hp ? slot_ptr(b, pa0) : nullptr, Qs,
+                          hp && pb0 != pa0 ? slot_ptr(b, pb0) : nullptr, Ps, nullptr, nullptr, tid);
+      __syncthreads();
+      if (hp) {
         v4d acc[2][2];
-        sum_pairs<SC1>(b, pairs, tk.po_beg, tk.po_end, Qs, Ps, tid, w, l, acc);   // Ps is free until the pd loop
+        zero_acc(acc);
+        for (int e = tk.po_beg; e < tk.po_end; ++e) {   // Ps is free until the pd loop
+          const int32_t pa = pairs[2 * e], pb = pairs[2 * e + 1];
+          const bool more = e + 1 < tk.po_end;
+          d2v nv[2][8];
+          int32_t na = -1, nb = -1;
+          if (more) {
+            na = pairs[2 * (e + 1)];
+            nb = pairs[2 * (e + 1) + 1];
+            tile_regs<SC1>(slot_ptr(b, na), nv[0], tid);
+            if (nb != na) tile_regs<SC1>(slot_ptr(b, nb), nv[1], tid);
+          }
+          mfma_abt_acc(Qs, pb != pa ? Ps : Qs, w, l, acc);
+          if (more) {
+            __syncthreads();
+            regs_tile(nv[0], Qs, tid);
+            if (nb != na) regs_tile(nv[1], Ps, tid);
+            __syncthreads();
+          }
+        }
 #pragma unroll
         for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
@@ -837,11 +847,21 @@ __device__ __forceinline__ void panel_task(const TileDev& b, const TileTask& tk,
             for (int rr = 0; rr < 4; ++rr) As[MFMA_ROW(w, l, ti, rr) * LD + MFMA_COL(w, l, tj)] -= acc[ti][tj][rr];
       }
     }
+    if (tk.pd_end > tk.pd_beg) {
+      __syncthreads();
+      load_tile_lds_t<SC1>(slot_ptr(b, pairs[2 * tk.pd_beg]), Ps, tid);
+      __syncthreads();
+    }
     for (int e = tk.pd_beg; e < tk.pd_end; ++e) {
-      __syncthreads();
-      load_tile_lds_t<SC1>(slot_ptr(b, pairs[2 * e]), Ps, tid);
-      __syncthreads();
+      const bool more = e + 1 < tk.pd_end;
+      d2v nv[8];
+      if (more) tile_regs<SC1>(slot_ptr(b, pairs[2 * (e + 1)]), nv, tid);
       diag_pending(accA, Ps, w, l);
+      if (more) {
+        __syncthreads();
+        regs_tile(nv, Ps, tid);
+        __syncthreads();
+      }
     }
   }
   __syncthreads();
