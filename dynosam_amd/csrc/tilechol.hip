@@ -1565,10 +1565,14 @@ __global__ __launch_bounds__(kBackWide) void k_back_wide(TileDev b, const BackPa
 // factors the next block also owns a full share of the trailing update,
 // which sits on every step's critical path.
 constexpr int kSmallNB = 4 * kSmallNT;   // 16x16 blocks per dimension
-constexpr int kSmallWaves = 8;
-constexpr int kSmallOff = (kSmallNB * (kSmallNB - 1) / 2) / kSmallWaves;   // off-diagonal blocks per wave
-static_assert(kSmallOff * kSmallWaves == kSmallNB * (kSmallNB - 1) / 2 && kSmallNB <= 2 * kSmallWaves,
-              "the small solve's block deal");
+#ifndef DYNOHIP_SMALL_WAVES
+#define DYNOHIP_SMALL_WAVES 8
+#endif
+constexpr int kSmallWaves = DYNOHIP_SMALL_WAVES;
+constexpr int kSmallNOff = kSmallNB * (kSmallNB - 1) / 2;
+constexpr int kSmallOff = (kSmallNOff + kSmallWaves - 1) / kSmallWaves;   // off-diagonal blocks per wave
+constexpr int kSmallD = (kSmallNB + kSmallWaves - 1) / kSmallWaves;        // diagonal blocks per wave
+static_assert(kSmallOff * kSmallWaves >= kSmallNOff && kSmallD <= 2, "the small solve's block deal");
 
 // off-diagonal block k of the enumeration by row I from the last, then J
 __device__ __forceinline__ void small_off_block(int k, int& I, int& J) {
@@ -1635,16 +1639,17 @@ __global__ __launch_bounds__(kSmallWaves * 64) void k_small_solve(TileDev b, con
     return v;
   };
   const v4d zero = v4d{0.0, 0.0, 0.0, 0.0};
-  v4d Dg[2], Rg[2], O[kSmallOff];
+  v4d Dg[kSmallD], Rg[kSmallD], O[kSmallOff];
   int oI[kSmallOff], oJ[kSmallOff];
 #pragma unroll
   for (int s = 0; s < kSmallOff; ++s) {
-    small_off_block(kSmallWaves * s + w, oI[s], oJ[s]);
+    oI[s] = oJ[s] = -1;
+    if (kSmallWaves * s + w < kSmallNOff) small_off_block(kSmallWaves * s + w, oI[s], oJ[s]);
     if (oJ[s] >= nb) oI[s] = -1;   // outside this system
     O[s] = oI[s] >= 0 ? load_blk(oI[s], oJ[s]) : zero;
   }
 #pragma unroll
-  for (int d = 0; d < 2; ++d) {
+  for (int d = 0; d < kSmallD; ++d) {
     const int K = w + kSmallWaves * d;
     Dg[d] = K < nb ? load_blk(K, K) : zero;
     Rg[d] = K < nb ? load_rhs(K) : zero;
@@ -1696,15 +1701,15 @@ __global__ __launch_bounds__(kSmallWaves * 64) void k_small_solve(TileDev b, con
       if (K1 < kSmallWaves) {
         diag_update(small_ic<0>{}, K, buf);
         factor(small_ic<0>{}, buf ^ 1);
-        diag_update(small_ic<1>{}, K, buf);
-      } else {
+        if constexpr (kSmallD > 1) diag_update(small_ic<1>{}, K, buf);
+      } else if constexpr (kSmallD > 1) {
         diag_update(small_ic<1>{}, K, buf);
         factor(small_ic<1>{}, buf ^ 1);
         diag_update(small_ic<0>{}, K, buf);
       }
     } else {
       diag_update(small_ic<0>{}, K, buf);
-      diag_update(small_ic<1>{}, K, buf);
+      if constexpr (kSmallD > 1) diag_update(small_ic<1>{}, K, buf);
     }
 #pragma unroll
     for (int s = 0; s < kSmallOff; ++s)

