@@ -420,12 +420,13 @@ SMALL_GRAPHS = [("T1", {}), (None, dict(frames=8, objects=1, static_landmarks=80
 def test_small_solve_matches_tile_dag(gpu_available, name, kw, monkeypatch):
     """Reduced systems of at most four tiles (the sliding windows) are solved
     in one workgroup (k_small_solve, opt-in: factorisation and both
-    substitutions, the matrix in registers) instead of on the tile DAG. Same system, other
-    summation order: one damped solve at three lambdas, each path against
-    the exact step (the oracle's Schur solve in x87 extended precision): the
-    one-workgroup solve is as accurate as the DAG up to the summation order
-    (within 10x its distance, observed <= 4x, or 1e-12); and the free-running LM takes the same tries, ending within
-    the north-star 1e-6 of each other (the runs drift apart through their
+    substitutions, the matrix in registers) instead of on the tile DAG.
+    Same system, other summation order: one damped solve at three lambdas,
+    each path against the exact step (the oracle's Schur solve in x87
+    extended precision): the one-workgroup solve is as accurate as the DAG
+    up to the summation order (within 10x its distance, observed <= 4x, or
+    1e-12); and the free-running LM takes the same tries, ending within the
+    north-star 1e-6 of each other (the runs drift apart through their
     accumulated rounding: 2.6e-9 on T1)."""
     g, v, _ = synth.generate(name, **kw)
     nt = int(plan_export(g, v, "info")[1])
