@@ -70,7 +70,8 @@ constexpr int kNPoseSlots[kNTypes] = {pose_slots(0), pose_slots(1), pose_slots(2
 // replaces std::unordered_map on the hot key lookups of planning
 class KeyIndex {
  public:
-  explicit KeyIndex(size_t n) {
+  // storage: vectors owned by the caller (Plan::Scratch), refilled here
+  KeyIndex(size_t n, std::vector<uint64_t>& keys, std::vector<int32_t>& vals) : keys_(keys), vals_(vals) {
     size_t cap = 16;
     while (cap < 2 * n + 1) cap <<= 1;
     mask_ = cap - 1;
@@ -100,8 +101,8 @@ class KeyIndex {
  private:
   size_t hash(uint64_t k) const { return static_cast<size_t>((k * 0x9E3779B97F4A7C15ull) >> 17) & mask_; }
   size_t mask_;
-  std::vector<uint64_t> keys_;
-  std::vector<int32_t> vals_;
+  std::vector<uint64_t>& keys_;
+  std::vector<int32_t>& vals_;
 };
 
 // CSR by target ranges: worker r owns the targets [tcut[r], tcut[r+1]) and
@@ -219,6 +220,7 @@ void plan_recycle(Plan& P) {
   k(f.tile_owner, P.tile_owner); k(f.ftask1, P.ftask1); k(f.flevel1, P.flevel1); k(f.fpanels1, P.fpanels1);
   k(f.fdep_start1, P.fdep_start1); k(f.fdep1, P.fdep1); k(f.fqueue1, P.fqueue1);
   k(f.sep_slot_ranges, P.sep_slot_ranges); k(f.sep_tile_ranges, P.sep_tile_ranges);
+  f.scratch = std::move(P.scratch);   // contents are refilled by build_plan
   P = std::move(f);
 }
 
@@ -229,7 +231,8 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
   P.nranks = nranks;
   P.rank = rank;
   // ---- values: key lookup ----
-  KeyIndex key_to_user(n);
+  Plan::Scratch& sc = P.scratch;
+  KeyIndex key_to_user(n, sc.key_k, sc.key_v);
   for (size_t i = 0; i < n; ++i) {
     if (kind[i] > 1) { err = "bad value kind"; return DYNOHIP_EINVAL; }
     if (!key_to_user.insert(keys[i], static_cast<int32_t>(i))) { err = "duplicate value key"; return DYNOHIP_EINVAL; }
@@ -241,7 +244,7 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
   const dynohip_factor_block* blocks[kNTypes] = {&g.pose_to_point, &g.landmark_motion_ternary, &g.between,
                                                  &g.prior, &g.landmark_motion_pose, &g.landmark_pose_smoothing};
   // user index per factor slot
-  std::vector<int32_t, default_init_allocator<int32_t>> fuser[kNTypes];   // (every entry written below)
+  auto& fuser = sc.fuser;   // user index per factor slot (every entry written below)
   for (int t = 0; t < kNTypes; ++t) {
     const auto* b = blocks[t];
     if (b->n == 0) continue;
@@ -316,7 +319,8 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
   // ---- point chains ----
   // adjacency between points from factors with two point slots: at most two
   // distinct neighbours per point (a chain), held flat
-  std::vector<int32_t> adj(2 * n, -1);
+  std::vector<int32_t>& adj = sc.adj;
+  adj.assign(2 * n, -1);
   std::vector<uint8_t> deg(n, 0);
   bool too_many = false;
   auto link = [&](int32_t a, int32_t b) {
@@ -441,7 +445,8 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
     // point's (short) pose list: the (point, pose)-sorted unique edge list
     // (serial: shared counters on the workers measured slower on the GPU
     // box's host, whose cores do not share one cache)
-    std::vector<int32_t> cnt(P.n_pt + 1, 0);
+    std::vector<int32_t>& cnt = sc.cnt;
+    cnt.assign(P.n_pt + 1, 0);
     auto each = [&](auto&& fn) {
       for (int t = 0; t < kNTypes; ++t) {
         const TypePlan& tp = P.types[t];
@@ -455,7 +460,8 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
     };
     each([&](int32_t pt, int32_t) { cnt[pt + 1]++; });
     for (int i = 0; i < P.n_pt; ++i) cnt[i + 1] += cnt[i];
-    std::vector<int32_t, default_init_allocator<int32_t>> poses(cnt[P.n_pt]);
+    auto& poses = sc.poses;
+    poses.resize(cnt[P.n_pt]);
     {
       std::vector<int32_t> cur(cnt.begin(), cnt.end() - 1);
       each([&](int32_t pt, int32_t pose) { poses[cur[pt]++] = pose; });
@@ -747,7 +753,8 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
   if (!structure_only) {
     // (a serial counting sort: per-worker histograms scatter into shared
     // lines and measured slower on the GPU box's host)
-    std::vector<int64_t> rstart(static_cast<size_t>(P.n_pt) + 1, 0);
+    std::vector<int64_t>& rstart = sc.rstart;
+    rstart.assign(static_cast<size_t>(P.n_pt) + 1, 0);
     for (int t = 0; t < kNTypes; ++t) {
       const TypePlan& tp = P.types[t];
       const int nk = kNKeys[t];
@@ -756,7 +763,8 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
           for (int i = 0; i < tp.n; ++i) rstart[tp.idx[i * nk + s] + 1]++;
     }
     for (int32_t pt = 0; pt < P.n_pt; ++pt) rstart[pt + 1] += rstart[pt];
-    std::vector<uint64_t, default_init_allocator<uint64_t>> refs(rstart[P.n_pt]);
+    auto& refs = sc.refs;
+    refs.resize(rstart[P.n_pt]);
     {
       std::vector<int64_t> cur(rstart.begin(), rstart.end() - 1);
       for (int t = 0; t < kNTypes; ++t) {
@@ -825,7 +833,8 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
     const int32_t e_l0 = p_lone < P.n_pt ? P.pt_edge_start[p_lone] : P.n_edge;
     const int32_t n_lone = P.n_pt - p_lone;
     std::vector<uint8_t> ok(static_cast<size_t>(n_lone), 0);
-    std::vector<uint32_t> prec(static_cast<size_t>(P.n_edge - e_l0));
+    std::vector<uint32_t>& prec = sc.prec;
+    prec.assign(static_cast<size_t>(P.n_edge - e_l0), 0);
     const TypePlan& t0 = P.types[0];
     parallel_for(n_lone, [&](int64_t q0, int64_t q1) {
       for (int64_t q = q0; q < q1; ++q) {
