@@ -442,6 +442,7 @@ __device__ __forceinline__ double linerr_one(const TypeDev& tp, int i, const dou
 __host__ __device__ constexpr uint32_t lone_h_off(int m) { return 36u * static_cast<uint32_t>(m * (m + 1) / 2) + 6u * m; }
 constexpr int kRec0 = kDim[0] * kCols[0] + kDim[0];   // PoseToPoint record stride (plan.cpp)
 constexpr int kLoneJ = 21;                            // staged per (point, a): J_x (3x6) | b (3)
+constexpr int kLoneHalf = kLoneSub / 2;               // points staged per pass (two passes)
 
 // Group block gb; returns this thread's share of the block's linear error at
 // delta = 0 (k_linearize's group_finish sums it with the factor blocks').
@@ -449,7 +450,9 @@ constexpr int kLoneJ = 21;                            // staged per (point, a): 
 __device__ double lone_lin_block(const LoneLinDev& d, int gb, const double* __restrict__ pose,
                                  const double* __restrict__ pt, double* __restrict__ arena) {
   __shared__ int32_t hdr[kLoneBlk];
-  __shared__ double sJ[256 * kLoneJ];   // a (point, neighbour) per lane: npt m <= 256
+  // the (point, neighbour) J | b of one pass: half the points, so the launch
+  // keeps 4 workgroups per CU (all 256 lanes at once took 43 KB)
+  __shared__ double sJ[kLoneHalf * kLoneMaxNb * kLoneJ];
   const int tid = threadIdx.x;
   for (int q = tid; q < kLoneBlk; q += kBlock) hdr[q] = d.blk[static_cast<int64_t>(gb) * kLoneBlk + q];
   __syncthreads();
@@ -458,9 +461,12 @@ __device__ double lone_lin_block(const LoneLinDev& d, int gb, const double* __re
   const int u = (tid >> 6) * per + uu;
   const bool valid = uu < per && u < npt;
   double Dp[9], gp[3], e = 0.0;
+  double sjv[kLoneJ];   // this lane's J_x | b, staged in its point's pass
 #pragma unroll
   for (int k = 0; k < 9; ++k) Dp[k] = 0.0;
   gp[0] = gp[1] = gp[2] = 0.0;
+#pragma unroll
+  for (int k = 0; k < kLoneJ; ++k) sjv[k] = 0.0;
   if (valid) {
     const uint32_t rec = static_cast<uint32_t>(hdr[kLoneHdrRec + m * u + a]);
     const int f = static_cast<int>((rec - d.t0.base) / kRec0);
@@ -486,11 +492,10 @@ __device__ double lone_lin_block(const LoneLinDev& d, int gb, const double* __re
       for (int l = 0; l < 3; ++l) Dp[3 * k + l] = Jp[k] * Jp[l] + Jp[3 + k] * Jp[3 + l] + Jp[6 + k] * Jp[6 + l];
       gp[k] = Jp[k] * bb[0] + Jp[3 + k] * bb[1] + Jp[6 + k] * bb[2];
     }
-    double* sj = sJ + kLoneJ * (m * u + a);
 #pragma unroll
-    for (int k = 0; k < 18; ++k) sj[k] = Jx[k];
+    for (int k = 0; k < 18; ++k) sjv[k] = Jx[k];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) sj[18 + k] = bb[k];
+    for (int k = 0; k < 3; ++k) sjv[18 + k] = bb[k];
   }
   // lane a == 0 of each point sums its m lanes (lone_point_block's order)
   double Ds[9], gs[3];
@@ -513,31 +518,58 @@ __device__ double lone_lin_block(const LoneLinDev& d, int gb, const double* __re
 #pragma unroll
     for (int k = 0; k < 3; ++k) G[k] = gs[k];
   }
-  __syncthreads();   // sJ
-  // the block's J_a^T J_a (lower entries, written to both halves) and J_a^T b
+  // the block's J_a^T J_a (lower entries, written to both halves) and J_a^T
+  // b: a thread per (a, entry), 27 m <= 2 kBlock of them, summing over the
+  // points in point order across the two passes
+  static_assert(27 * kLoneMaxNb <= 2 * kBlock, "two (a, entry) sums per thread at most");
+  double acc[2] = {0.0, 0.0};
+  for (int p0 = 0; p0 < npt; p0 += kLoneHalf) {   // (npt from the header: uniform)
+    const int p1 = min(npt, p0 + kLoneHalf);
+    if (p0 > 0) __syncthreads();   // the previous pass's sums are done with sJ
+    if (valid && u >= p0 && u < p1) {
+      double* sj = sJ + kLoneJ * (m * (u - p0) + a);
+#pragma unroll
+      for (int k = 0; k < kLoneJ; ++k) sj[k] = sjv[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int t = tid + h * kBlock;
+      if (t >= 27 * m) break;
+      const int aa = t / 27, q = t - 27 * aa;
+      if (q < 21) {
+        int r = 0;
+        while ((r + 1) * (r + 2) / 2 <= q) ++r;
+        const int c = q - r * (r + 1) / 2;
+        for (int p = p0; p < p1; ++p) {
+          const double* sj = sJ + kLoneJ * (m * (p - p0) + aa);
+#pragma unroll
+          for (int k = 0; k < 3; ++k) acc[h] += sj[6 * k + r] * sj[6 * k + c];
+        }
+      } else {
+        const int r = q - 21;
+        for (int p = p0; p < p1; ++p) {
+          const double* sj = sJ + kLoneJ * (m * (p - p0) + aa);
+#pragma unroll
+          for (int k = 0; k < 3; ++k) acc[h] += sj[6 * k + r] * sj[18 + k];
+        }
+      }
+    }
+  }
   double* H = arena + static_cast<uint32_t>(hdr[2]) + lone_h_off(m);
-  for (int t = tid; t < 27 * m; t += kBlock) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int t = tid + h * kBlock;
+    if (t >= 27 * m) break;
     const int aa = t / 27, q = t - 27 * aa;
-    double acc = 0.0;
     if (q < 21) {
       int r = 0;
       while ((r + 1) * (r + 2) / 2 <= q) ++r;
       const int c = q - r * (r + 1) / 2;
-      for (int p = 0; p < npt; ++p) {
-        const double* sj = sJ + kLoneJ * (m * p + aa);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) acc += sj[6 * k + r] * sj[6 * k + c];
-      }
-      H[36 * aa + 6 * r + c] = acc;
-      H[36 * aa + 6 * c + r] = acc;
+      H[36 * aa + 6 * r + c] = acc[h];
+      H[36 * aa + 6 * c + r] = acc[h];
     } else {
-      const int r = q - 21;
-      for (int p = 0; p < npt; ++p) {
-        const double* sj = sJ + kLoneJ * (m * p + aa);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) acc += sj[6 * k + r] * sj[18 + k];
-      }
-      H[36 * m + 6 * aa + r] = acc;
+      H[36 * m + 6 * aa + (q - 21)] = acc[h];
     }
   }
   return e;
@@ -802,6 +834,37 @@ __device__ __forceinline__ void group_accumulate(const int64_t* __restrict__ sta
     const double* A = arena + g.a;
     const double* B = arena + g.b;
     const double sg = static_cast<double>(g.sign);
+#ifdef DYNOHIP_GRED_PIPE
+    if constexpr (S == 1) {
+      // the next row's operands are loaded while this row's FMAs run
+      double a[R], b[CC];
+#pragma unroll
+      for (int r = 0; r < R; ++r) a[r] = A[r];
+#pragma unroll
+      for (int c = 0; c < CC; ++c) b[c] = B[c];
+      for (int k = 0; k < g.k; ++k) {
+        double an[R], bn[CC];
+        const int kn = k + 1 < g.k ? k + 1 : k;
+#pragma unroll
+        for (int r = 0; r < R; ++r) an[r] = A[kn * R + r];
+#pragma unroll
+        for (int c = 0; c < CC; ++c) bn[c] = B[kn * CC + c];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const double ar = sg * a[r];
+#pragma unroll
+          for (int c = 0; c < CC; ++c) acc[r * CC + c] += ar * b[c];
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) a[r] = an[r];
+#pragma unroll
+        for (int c = 0; c < CC; ++c) b[c] = bn[c];
+      }
+      e = en;
+      g = gn;
+      continue;
+    }
+#endif
     for (int k0 = 0; k0 < g.k; k0 += S) {
       double a[S][R], b[S][CC];
 #pragma unroll
@@ -907,42 +970,92 @@ __global__ __launch_bounds__(kBlock) void k_gather_point(PointGatherDev p, const
   else lone_point_block(p, b - p.bstart[4], arena);
 }
 
-// a wave per 6x6 target
-__device__ __forceinline__ void gather_band(const GatherDev& g, const int32_t* __restrict__ tA,
-                                            const int32_t* __restrict__ tB, const uint32_t* __restrict__ tslot, int blk,
+// Reduce-scatter of an N-vector over the xor masks M, M/2, ..., 1 (the
+// steps of rs_step): the lane keeps Out values.
+template <int N, int M>
+struct RsTree {
+  static constexpr int H = (N + 1) / 2;
+  static constexpr int Out = RsTree<H, M / 2>::Out;
+  __device__ static __forceinline__ void run(const double (&in)[N], double (&out)[Out], int q) {
+    double mid[H];
+    rs_step<N, M>(in, mid, q & M);
+    RsTree<H, M / 2>::run(mid, out, q);
+  }
+};
+template <int N>
+struct RsTree<N, 0> {
+  static constexpr int Out = N;
+  __device__ static __forceinline__ void run(const double (&in)[N], double (&out)[N], int) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) out[i] = in[i];
+  }
+};
+// which elements of the N0-vector lane q holds after RsTree<N0, M>: values
+// [0, valid) are elements base + i (the rest padding)
+template <int N0, int M>
+__device__ __forceinline__ int rs_span(int q, int& valid) {
+  int o = 0, v = N0, n = N0;
+#pragma unroll
+  for (int m = M; m >= 1; m >>= 1) {
+    const int h = (n + 1) / 2;
+    if (q & m) {
+      o += h;
+      v = max(0, min(v - h, h));
+    } else {
+      v = min(v, h);
+    }
+    n = h;
+  }
+  valid = v;
+  return o;
+}
+
+// G lanes per 6x6 target, targets of class order[0, n). Lane q sums the
+// entries q, q + G, ... of its target; the sums are reduce-scattered over
+// the xor masks G/2 .. 1. A target of at most G entries thus sums them in
+// exactly the pairing of the 64-lane form (whose upper lanes would only add
+// exact zeros), so every class gives the same bits as one wave per target,
+// with fewer idle lanes and more entry loads in flight.
+template <int G>
+__device__ __forceinline__ void gather_band(const GatherDev& g, const int32_t* __restrict__ order, int n,
+                                            const int32_t* __restrict__ tA, const int32_t* __restrict__ tB,
+                                            const uint32_t* __restrict__ tslot, int blk,
                                             const double* __restrict__ arena, const TileDev& b, double lambda,
                                             const uint8_t* __restrict__ damp) {
-  const int t = (blk * kBlock + static_cast<int>(threadIdx.x)) >> 6;
-  const int q = threadIdx.x & 63;
-  if (t >= g.n) return;
+  const int s = (blk * kBlock + static_cast<int>(threadIdx.x)) / G;
+  const int q = threadIdx.x & (G - 1);
+  if (s >= n) return;
+  const int t = order[s];
   // the target's poses and tile slots, fetched ahead of its entries
   const int A = tA[t], B = tB[t];
   const uint32_t ts[4] = {tslot[4 * t], tslot[4 * t + 1], tslot[4 * t + 2], tslot[4 * t + 3]};
-  double acc[36], a18[18], a9[9], a5[5], a3[3], a2[2], a1[1];
-  group_accumulate<6, 6, 64, 1>(g.start, g.ent, t, q, arena, acc);
-  rs_step<36, 32>(acc, a18, q & 32);
-  rs_step<18, 16>(a18, a9, q & 16);
-  rs_step<9, 8>(a9, a5, q & 8);
-  rs_step<5, 4>(a5, a3, q & 4);
-  rs_step<3, 2>(a3, a2, q & 2);
-  rs_step<2, 1>(a2, a1, q & 1);
-  const int idx = rs_index<36>(q);
-  if (idx < 0) return;
-  const int r = idx / 6, c = idx % 6;
-  if (A == B && r < c) return;
-  const int row = 6 * A + r, col = 6 * B + c;
-  const double val = a1[0] + (A == B && r == c && (!damp || damp[row]) ? lambda : 0.0);
-  // the tile from the target's precomputed slots (no lookup chain)
-  const int sel = 2 * ((row >> 6) != ((6 * A) >> 6)) + ((col >> 6) != ((6 * B) >> 6));
-  const uint32_t e = sel == 0 ? ts[0] : sel == 1 ? ts[1] : sel == 2 ? ts[2] : ts[3];
-  const int64_t at = static_cast<int64_t>(e & 0x7fffffffu) * kTile * kTile +
-                     ((e >> 31) ? (col % kTile) * kTile + row % kTile : (row % kTile) * kTile + col % kTile);
-  b.slots[at] = val;
-  // diagonal tiles are stored full (symmetric), so the factorisation reads
-  // them with plain coalesced loads
-  if (row / kTile == col / kTile && row != col) {
-    const int64_t base = at - (row % kTile) * kTile - (col % kTile);
-    b.slots[base + (col % kTile) * kTile + (row % kTile)] = val;
+  double acc[36];
+  group_accumulate<6, 6, G, 1>(g.start, g.ent, t, q, arena, acc);
+  using Tree = RsTree<36, G / 2>;
+  double out[Tree::Out];
+  Tree::run(acc, out, q);
+  int valid;
+  const int base = rs_span<36, G / 2>(q, valid);
+#pragma unroll
+  for (int i = 0; i < Tree::Out; ++i) {
+    if (i >= valid) break;
+    const int idx = base + i;
+    const int r = idx / 6, c = idx % 6;
+    if (A == B && r < c) continue;
+    const int row = 6 * A + r, col = 6 * B + c;
+    const double val = out[i] + (A == B && r == c && (!damp || damp[row]) ? lambda : 0.0);
+    // the tile from the target's precomputed slots (no lookup chain)
+    const int sel = 2 * ((row >> 6) != ((6 * A) >> 6)) + ((col >> 6) != ((6 * B) >> 6));
+    const uint32_t e = sel == 0 ? ts[0] : sel == 1 ? ts[1] : sel == 2 ? ts[2] : ts[3];
+    const int64_t at = static_cast<int64_t>(e & 0x7fffffffu) * kTile * kTile +
+                       ((e >> 31) ? (col % kTile) * kTile + row % kTile : (row % kTile) * kTile + col % kTile);
+    b.slots[at] = val;
+    // diagonal tiles are stored full (symmetric), so the factorisation reads
+    // them with plain coalesced loads
+    if (row / kTile == col / kTile && row != col) {
+      const int64_t tb = at - (row % kTile) * kTile - (col % kTile);
+      b.slots[tb + (col % kTile) * kTile + (row % kTile)] = val;
+    }
   }
 }
 
@@ -971,11 +1084,31 @@ __device__ __forceinline__ void gather_grad(const GatherDev& g, int blk, const d
 // XCD's L2; the parts start at multiples of 8 blocks (the XCD count), so each
 // part is spread over all XCDs (one remap over the whole grid would leave the
 // light gradient blocks to the last XCDs).
-__global__ __launch_bounds__(kBlock) void k_gather_reduced(ReducedGatherDev r, const double* __restrict__ arena,
+#ifndef DYNOHIP_GRED_WAVES
+#define DYNOHIP_GRED_WAVES 4   // 128 VGPRs: the lane classes' reduce trees fit without spilling
+#endif
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DYNOHIP_GRED_WAVES))) void k_gather_reduced(ReducedGatherDev r, const double* __restrict__ arena,
                                                            TileDev b, double lambda) {
   const int hb = blockIdx.x;
   if (hb < r.nb_band) {
-    gather_band(r.band, r.tA, r.tB, r.tslot, xcd_block(hb, r.nb_band), arena, b, lambda, r.damp);
+    // class c: targets order[o_c, o_c + ncls[c]) (o_c: the earlier classes' counts)
+    int c = 0, o = 0;
+#pragma unroll
+    for (int k = 1; k < ReducedGatherDev::kClasses; ++k)
+      if (hb >= r.bstart[k]) {
+        c = k;
+        o += r.ncls[k - 1];
+      }
+    const int nbc = r.bstart[c + 1] - r.bstart[c];
+    const int blk = xcd_block(hb - r.bstart[c], nbc);
+    const int32_t* ord = r.order + o;
+    switch (c) {
+      case 0: gather_band<4>(r.band, ord, r.ncls[0], r.tA, r.tB, r.tslot, blk, arena, b, lambda, r.damp); break;
+      case 1: gather_band<8>(r.band, ord, r.ncls[1], r.tA, r.tB, r.tslot, blk, arena, b, lambda, r.damp); break;
+      case 2: gather_band<16>(r.band, ord, r.ncls[2], r.tA, r.tB, r.tslot, blk, arena, b, lambda, r.damp); break;
+      case 3: gather_band<32>(r.band, ord, r.ncls[3], r.tA, r.tB, r.tslot, blk, arena, b, lambda, r.damp); break;
+      default: gather_band<64>(r.band, ord, r.ncls[4], r.tA, r.tB, r.tslot, blk, arena, b, lambda, r.damp); break;
+    }
   } else if (hb < r.nb_band + r.nb_grad) {
     gather_grad(r.grad, xcd_block(hb - r.nb_band, r.nb_grad), arena, r.gred);
   } else {
@@ -2193,19 +2326,28 @@ void launch_gather_point(const GatherDev (&g)[4], double* const (&dst)[4], const
   k_gather_point<<<nb, kBlock, 0, s>>>(p, arena);
 }
 
-void launch_gather_reduced(const GatherDev& band, const int32_t* tA, const int32_t* tB, const uint32_t* tslot,
-                           const GatherDev& grad,
+void launch_gather_reduced(const GatherDev& band, const int32_t* order, const int32_t* ncls, const int32_t* tA,
+                           const int32_t* tB, const uint32_t* tslot, const GatherDev& grad,
                            double* gred, const double* arena, const TileDev& b, double lambda, hipStream_t s,
                            const uint8_t* damp) {
   ReducedGatherDev r;
   r.damp = damp;
   r.band = band;
+  r.order = order;
+  // each class's blocks start at a multiple of 8 (the XCD count, xcd_block)
+  // (the classes cover every target: checked where the plan is uploaded)
+  r.bstart[0] = 0;
+  for (int c = 0; c < ReducedGatherDev::kClasses; ++c) {
+    r.ncls[c] = ncls[c];
+    const int lanes = 4 << c;
+    r.bstart[c + 1] = r.bstart[c] + (nblocks(static_cast<int64_t>(ncls[c]) * lanes) + 7) / 8 * 8;
+  }
   r.tA = tA;
   r.tB = tB;
   r.tslot = tslot;
   r.grad = grad;
   r.gred = gred;
-  r.nb_band = (nblocks(static_cast<int64_t>(band.n) * 64) + 7) / 8 * 8;
+  r.nb_band = r.bstart[ReducedGatherDev::kClasses];
   r.nb_grad = (nblocks(static_cast<int64_t>(grad.n) * 64) + 7) / 8 * 8;
   const int nb = r.nb_band + r.nb_grad + nblocks(std::max(0, b.NT * kTile - b.n_red));
   if (nb == 0) return;

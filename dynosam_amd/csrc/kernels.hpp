@@ -42,6 +42,13 @@ struct PointGatherDev {
 
 struct ReducedGatherDev {
   GatherDev band;              // 6x6 reduced blocks (targets tA[t], tB[t])
+  // the targets by entry count (Plan::red_order): class c, of <= 4 << c
+  // entries, runs 4 << c lanes per target (the last class 64 lanes);
+  // bstart[c] = first block of class c
+  static constexpr int kClasses = 5;
+  const int32_t* order = nullptr;
+  int ncls[kClasses] = {};
+  int bstart[kClasses + 1] = {};
   const int32_t* tA = nullptr;
   const int32_t* tB = nullptr;
   const uint32_t* tslot = nullptr;   // Plan::red_slot
@@ -174,7 +181,7 @@ void launch_linerr(const TypeDev* td, const double* arena, const double* dpose, 
 void launch_gather_point(const GatherDev (&g)[4], double* const (&dst)[4], const double* arena, hipStream_t s,
                          int n_lone = 0, const int32_t* lone_blk = nullptr);
 // reduced blocks into their tiles (+ lambda), reduced gradient, identity padding
-void launch_gather_reduced(const GatherDev& band, const int32_t* tA, const int32_t* tB, const uint32_t* tslot,
+void launch_gather_reduced(const GatherDev& band, const int32_t* order, const int32_t* ncls, const int32_t* tA, const int32_t* tB, const uint32_t* tslot,
                            const GatherDev& grad,
                            double* gred, const double* arena, const TileDev& b, double lambda, hipStream_t s,
                            const uint8_t* damp = nullptr);

@@ -394,7 +394,7 @@ extern "C" int dynohip_plan_export(const dynohip_graph_view* g, const uint64_t* 
       v(P.types[t].idx); v(P.types[t].meas); v(P.types[t].isig); v(P.types[t].hk);
     }
     for (const GatherList* G : {&P.gD, &P.gE, &P.gGp, &P.gW, &P.gRed, &P.gGred}) { v(G->start); v(G->ent); }
-    v(P.red_A); v(P.red_B); v(P.red_slot);
+    v(P.red_A); v(P.red_B); v(P.red_slot); v(P.red_order);
     v(P.lgroup); v(P.lone_pose); v(P.lone_blk); v(P.lin_list0);
     v(P.band_D); v(P.tile_pos); v(P.row_start); v(P.row_col); v(P.row_slot);
     v(P.ftask); v(P.pairs); v(P.flevel); v(P.fpanels); v(P.fdep_start); v(P.fdep); v(P.fqueue);

@@ -188,6 +188,25 @@ void compute_red_slots(Plan& P) {
       o[3] = (r1 != r0 && c1 != c0) ? lookup(r1, c1) : ~0u;
     }
   });
+  // targets by entry count (class c holds the targets of <= 4 << c entries;
+  // the last class all larger ones), each class in target order
+  const int64_t* st = P.gRed.start.data();
+  auto cls = [&](int64_t t) {
+    const int64_t m = st[t + 1] - st[t];
+    int c = 0;
+    while (c < Plan::kRedClasses - 1 && m > (int64_t{4} << c)) ++c;
+    return c;
+  };
+  int32_t pos[Plan::kRedClasses + 1] = {};
+  for (int c = 0; c < Plan::kRedClasses; ++c) P.red_ncls[c] = 0;
+  if (P.gRed.start.size() != static_cast<size_t>(nt) + 1) {   // no band gather (structure-only plans)
+    P.red_order.clear();
+    return;
+  }
+  for (int64_t t = 0; t < nt; ++t) ++P.red_ncls[cls(t)];
+  for (int c = 0; c < Plan::kRedClasses; ++c) pos[c + 1] = pos[c] + P.red_ncls[c];
+  P.red_order.resize(static_cast<size_t>(nt));
+  for (int64_t t = 0; t < nt; ++t) P.red_order[pos[cls(t)]++] = static_cast<int32_t>(t);
 }
 
 void plan_recycle(Plan& P) {
@@ -211,7 +230,7 @@ void plan_recycle(Plan& P) {
     k((f.*m).start, (P.*m).start);
     k((f.*m).ent, (P.*m).ent);
   }
-  k(f.red_A, P.red_A); k(f.red_B, P.red_B); k(f.red_slot, P.red_slot);
+  k(f.red_A, P.red_A); k(f.red_B, P.red_B); k(f.red_slot, P.red_slot); k(f.red_order, P.red_order);
   k(f.lgroup, P.lgroup); k(f.lone_pose, P.lone_pose); k(f.lone_blk, P.lone_blk); k(f.lin_list0, P.lin_list0);
   k(f.band_D, P.band_D); k(f.tile_pos, P.tile_pos); k(f.row_start, P.row_start); k(f.row_col, P.row_col);
   k(f.row_slot, P.row_slot); k(f.ftask, P.ftask); k(f.pairs, P.pairs); k(f.flevel, P.flevel);

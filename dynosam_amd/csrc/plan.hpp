@@ -187,6 +187,12 @@ struct Plan {
   // [row tile of 6A / of 6A+5][col tile of 6B / of 6B+5], bit 31 = the tile is
   // stored transposed (its column tile is eliminated later); ~0u: not stored
   std::vector<uint32_t> red_slot;
+  // the targets by entry count, for k_gather_reduced's lane groups: targets
+  // of <= 4, <= 8, <= 16, <= 32 and more entries (kRedClasses), each class in
+  // target order; red_ncls = targets per class
+  static constexpr int kRedClasses = 5;
+  std::vector<int32_t> red_order;
+  int32_t red_ncls[kRedClasses] = {};
   // lone-point groups (k_lone_schur); their points' factor pairs and
   // component pairs are not in gRed / gGred
   std::vector<LoneGroup> lgroup;

@@ -431,6 +431,7 @@ struct dynohip_solver {
   GatherBufs gD, gE, gGp, gW, gRed, gGred;
   DevBuf<int32_t> redA, redB;
   DevBuf<uint32_t> redslot;
+  DevBuf<int32_t> redorder;   // Plan::red_order (targets by entry count)
   DevBuf<int32_t> comp_start, comp_nb_start, nb_comp, nbedge_start, nbedge_pt, pt_edge_start, edge_pose, edge_pt;
   DevBuf<int64_t> comp_y_base;
   DevBuf<uint32_t> nbedge_w;
@@ -588,6 +589,13 @@ int upload_plan(dynohip_solver* s, bool types_done = false) {
   HIPCHK(s, up.add(s->redA, P.red_A));
   HIPCHK(s, up.add(s->redB, P.red_B));
   HIPCHK(s, up.add(s->redslot, P.red_slot));
+  {
+    int64_t covered = 0;
+    for (int c = 0; c < Plan::kRedClasses; ++c) covered += P.red_ncls[c];
+    if (covered != static_cast<int64_t>(P.gRed.ntargets()) || P.red_order.size() != P.gRed.ntargets())
+      return set_err(s, DYNOHIP_ESTRUCT, "internal: reduced-gather target classes do not cover the targets");
+  }
+  HIPCHK(s, up.add(s->redorder, P.red_order));
   HIPCHK(s, up.add(s->comp_start, P.comp_start));
   HIPCHK(s, up.add(s->comp_nb_start, P.comp_nb_start));
   HIPCHK(s, up.add(s->nb_comp, P.nb_comp));
@@ -878,7 +886,7 @@ int enqueue_try(dynohip_solver* s, double lambda) {
     launch_lone_schur(s->ld, A, st);
   }
   if (timed) (void)hipEventRecord(s->ev[3], st);
-  launch_gather_reduced(s->gRed.dev(P.gRed.ntargets()), s->redA.p, s->redB.p, s->redslot.p,
+  launch_gather_reduced(s->gRed.dev(P.gRed.ntargets()), s->redorder.p, P.red_ncls, s->redA.p, s->redB.p, s->redslot.p,
                         s->gGred.dev(P.gGred.ntargets()),
                         s->gred.p, A, s->bd, lambda, st, s->nranks > 1 ? s->damp.p : nullptr);
   if (timed) (void)hipEventRecord(s->ev[4], st);
