@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
+#include <cstdlib>
+#include <string>
 
 #include "kernels.hpp"
 #include "se3.hpp"
@@ -833,6 +835,15 @@ __device__ __forceinline__ void group_accumulate(const int64_t* __restrict__ sta
     const GEntry gn = en < e1 ? ent[en] : GEntry{0, 0, 0, 0};
     const double* A = arena + g.a;
     const double* B = arena + g.b;
+    if (g.sign == kAddBlock) {
+      // a partial block (lone groups): added as it is, the identity's
+      // product bit for bit, its loads issued at once
+#pragma unroll
+      for (int j = 0; j < R * CC; ++j) acc[j] += B[j];
+      e = en;
+      g = gn;
+      continue;
+    }
     const double sg = static_cast<double>(g.sign);
 #ifdef DYNOHIP_GRED_PIPE
     if constexpr (S == 1) {
@@ -970,33 +981,33 @@ __global__ __launch_bounds__(kBlock) void k_gather_point(PointGatherDev p, const
   else lone_point_block(p, b - p.bstart[4], arena);
 }
 
-// Reduce-scatter of an N-vector over the xor masks M, M/2, ..., 1 (the
-// steps of rs_step): the lane keeps Out values.
-template <int N, int M>
+// Reduce-scatter of an N-vector over Steps xor masks M, M/2, ... (the steps
+// of rs_step): the lane keeps Out values.
+template <int N, int M, int Steps>
 struct RsTree {
   static constexpr int H = (N + 1) / 2;
-  static constexpr int Out = RsTree<H, M / 2>::Out;
+  static constexpr int Out = RsTree<H, M / 2, Steps - 1>::Out;
   __device__ static __forceinline__ void run(const double (&in)[N], double (&out)[Out], int q) {
     double mid[H];
     rs_step<N, M>(in, mid, q & M);
-    RsTree<H, M / 2>::run(mid, out, q);
+    RsTree<H, M / 2, Steps - 1>::run(mid, out, q);
   }
 };
-template <int N>
-struct RsTree<N, 0> {
+template <int N, int M>
+struct RsTree<N, M, 0> {
   static constexpr int Out = N;
   __device__ static __forceinline__ void run(const double (&in)[N], double (&out)[N], int) {
 #pragma unroll
     for (int i = 0; i < N; ++i) out[i] = in[i];
   }
 };
-// which elements of the N0-vector lane q holds after RsTree<N0, M>: values
-// [0, valid) are elements base + i (the rest padding)
-template <int N0, int M>
+// which elements of the N0-vector lane q holds after RsTree<N0, M, Steps>:
+// values [0, valid) are elements base + i (the rest padding)
+template <int N0, int M, int Steps>
 __device__ __forceinline__ int rs_span(int q, int& valid) {
   int o = 0, v = N0, n = N0;
 #pragma unroll
-  for (int m = M; m >= 1; m >>= 1) {
+  for (int s = 0, m = M; s < Steps; ++s, m >>= 1) {
     const int h = (n + 1) / 2;
     if (q & m) {
       o += h;
@@ -1009,6 +1020,69 @@ __device__ __forceinline__ int rs_span(int q, int& valid) {
   valid = v;
   return o;
 }
+constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x / 2); }
+
+// the tile element of reduced entry (row, col) of target (A, B), from the
+// target's precomputed slots (no lookup chain); the diagonal tiles are stored
+// full (symmetric), so the factorisation reads them with plain coalesced loads
+__device__ __forceinline__ void store_reduced(const TileDev& b, const uint32_t (&ts)[4], int A, int B, int r, int c,
+                                              double v, double lambda, const uint8_t* __restrict__ damp) {
+  if (A == B && r < c) return;
+  const int row = 6 * A + r, col = 6 * B + c;
+  const double val = v + (A == B && r == c && (!damp || damp[row]) ? lambda : 0.0);
+  const int sel = 2 * ((row >> 6) != ((6 * A) >> 6)) + ((col >> 6) != ((6 * B) >> 6));
+  const uint32_t e = sel == 0 ? ts[0] : sel == 1 ? ts[1] : sel == 2 ? ts[2] : ts[3];
+  const int64_t at = static_cast<int64_t>(e & 0x7fffffffu) * kTile * kTile +
+                     ((e >> 31) ? (col % kTile) * kTile + row % kTile : (row % kTile) * kTile + col % kTile);
+  b.slots[at] = val;
+  if (row / kTile == col / kTile && row != col) {
+    const int64_t tb = at - (row % kTile) * kTile - (col % kTile);
+    b.slots[tb + (col % kTile) * kTile + (row % kTile)] = val;
+  }
+}
+
+// Two lanes per entry (row halves h = q & 1 of the 6x6 product, 18 sums
+// each), entries (q >> 1) + G/2 j: every row of an entry's operands loaded
+// at once (one round trip for a 3-row entry instead of one per row). Each
+// sum keeps the FMA sequence of the one-lane form (rows in order).
+template <int G>
+__device__ __forceinline__ void accumulate_half(const int64_t* __restrict__ start, const GEntry* __restrict__ ent,
+                                                int t, int q, const double* __restrict__ arena, double (&acc)[18]) {
+  constexpr int GS = G / 2;
+  const int h = q & 1;
+#pragma unroll
+  for (int j = 0; j < 18; ++j) acc[j] = 0.0;
+  const int64_t e1 = start[t + 1];
+  for (int64_t e = start[t] + (q >> 1); e < e1; e += GS) {
+    const GEntry g = ent[e];
+    const double* A = arena + g.a;
+    const double* B = arena + g.b + 18 * h;
+    if (g.sign == kAddBlock) {
+#pragma unroll
+      for (int j = 0; j < 18; ++j) acc[j] += B[j];
+      continue;
+    }
+    const double sg = static_cast<double>(g.sign);
+    for (int k0 = 0; k0 < g.k; k0 += 3) {   // k is 3 or 6
+      double a[3][3], bb[3][6];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+#pragma unroll
+        for (int r = 0; r < 3; ++r) a[k][r] = A[(k0 + k) * 6 + 3 * h + r];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) bb[k][c] = arena[g.b + (k0 + k) * 6 + c];
+      }
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          const double ar = sg * a[k][r];
+#pragma unroll
+          for (int c = 0; c < 6; ++c) acc[r * 6 + c] += ar * bb[k][c];
+        }
+    }
+  }
+}
 
 // G lanes per 6x6 target, targets of class order[0, n). Lane q sums the
 // entries q, q + G, ... of its target; the sums are reduce-scattered over
@@ -1016,7 +1090,10 @@ __device__ __forceinline__ int rs_span(int q, int& valid) {
 // exactly the pairing of the 64-lane form (whose upper lanes would only add
 // exact zeros), so every class gives the same bits as one wave per target,
 // with fewer idle lanes and more entry loads in flight.
-template <int G>
+// Half: two lanes per entry (accumulate_half), a target of at most G/2
+// entries; the row halves are reduce-scattered over the lane masks G/2 .. 2,
+// which pair the entries exactly as the masks G/4 .. 1 of the one-lane form.
+template <int G, bool Half>
 __device__ __forceinline__ void gather_band(const GatherDev& g, const int32_t* __restrict__ order, int n,
                                             const int32_t* __restrict__ tA, const int32_t* __restrict__ tB,
                                             const uint32_t* __restrict__ tslot, int blk,
@@ -1029,32 +1106,36 @@ __device__ __forceinline__ void gather_band(const GatherDev& g, const int32_t* _
   // the target's poses and tile slots, fetched ahead of its entries
   const int A = tA[t], B = tB[t];
   const uint32_t ts[4] = {tslot[4 * t], tslot[4 * t + 1], tslot[4 * t + 2], tslot[4 * t + 3]};
-  double acc[36];
-  group_accumulate<6, 6, G, 1>(g.start, g.ent, t, q, arena, acc);
-  using Tree = RsTree<36, G / 2>;
-  double out[Tree::Out];
-  Tree::run(acc, out, q);
-  int valid;
-  const int base = rs_span<36, G / 2>(q, valid);
+  if constexpr (Half) {
+    double acc[18];
+    accumulate_half<G>(g.start, g.ent, t, q, arena, acc);
+    constexpr int steps = ilog2(G) - 1;
+    using Tree = RsTree<18, G / 2, steps>;
+    double out[Tree::Out];
+    Tree::run(acc, out, q);
+    int valid;
+    const int base = rs_span<18, G / 2, steps>(q, valid);
+    const int r0 = 3 * (q & 1);
 #pragma unroll
-  for (int i = 0; i < Tree::Out; ++i) {
-    if (i >= valid) break;
-    const int idx = base + i;
-    const int r = idx / 6, c = idx % 6;
-    if (A == B && r < c) continue;
-    const int row = 6 * A + r, col = 6 * B + c;
-    const double val = out[i] + (A == B && r == c && (!damp || damp[row]) ? lambda : 0.0);
-    // the tile from the target's precomputed slots (no lookup chain)
-    const int sel = 2 * ((row >> 6) != ((6 * A) >> 6)) + ((col >> 6) != ((6 * B) >> 6));
-    const uint32_t e = sel == 0 ? ts[0] : sel == 1 ? ts[1] : sel == 2 ? ts[2] : ts[3];
-    const int64_t at = static_cast<int64_t>(e & 0x7fffffffu) * kTile * kTile +
-                       ((e >> 31) ? (col % kTile) * kTile + row % kTile : (row % kTile) * kTile + col % kTile);
-    b.slots[at] = val;
-    // diagonal tiles are stored full (symmetric), so the factorisation reads
-    // them with plain coalesced loads
-    if (row / kTile == col / kTile && row != col) {
-      const int64_t tb = at - (row % kTile) * kTile - (col % kTile);
-      b.slots[tb + (col % kTile) * kTile + (row % kTile)] = val;
+    for (int i = 0; i < Tree::Out; ++i) {
+      if (i >= valid) break;
+      const int idx = base + i;
+      store_reduced(b, ts, A, B, r0 + idx / 6, idx % 6, out[i], lambda, damp);
+    }
+  } else {
+    double acc[36];
+    group_accumulate<6, 6, G, 1>(g.start, g.ent, t, q, arena, acc);
+    constexpr int steps = ilog2(G);
+    using Tree = RsTree<36, G / 2, steps>;
+    double out[Tree::Out];
+    Tree::run(acc, out, q);
+    int valid;
+    const int base = rs_span<36, G / 2, steps>(q, valid);
+#pragma unroll
+    for (int i = 0; i < Tree::Out; ++i) {
+      if (i >= valid) break;
+      const int idx = base + i;
+      store_reduced(b, ts, A, B, idx / 6, idx % 6, out[i], lambda, damp);
     }
   }
 }
@@ -1091,24 +1172,34 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DYNOHIP_
                                                            TileDev b, double lambda) {
   const int hb = blockIdx.x;
   if (hb < r.nb_band) {
-    // class c: targets order[o_c, o_c + ncls[c]) (o_c: the earlier classes' counts)
-    int c = 0, o = 0;
+    // dispatch position d runs class cls[d]: targets order[ooff[c], + ncls[c])
+    int d = 0;
 #pragma unroll
     for (int k = 1; k < ReducedGatherDev::kClasses; ++k)
-      if (hb >= r.bstart[k]) {
-        c = k;
-        o += r.ncls[k - 1];
+      if (hb >= r.bstart[k]) d = k;
+    const int c = r.cls[d];
+    const int nbc = r.bstart[d + 1] - r.bstart[d];
+    const int blk = xcd_block(hb - r.bstart[d], nbc);
+    const int32_t* ord = r.order + r.ooff[c];
+#define DH_GB(G, H) gather_band<G, H>(r.band, ord, r.ncls[c], r.tA, r.tB, r.tslot, blk, arena, b, lambda, r.damp)
+    if (r.half) {
+      switch (c) {
+        case 0: DH_GB(8, true); break;
+        case 1: DH_GB(16, true); break;
+        case 2: DH_GB(32, true); break;
+        case 3: DH_GB(64, true); break;
+        default: DH_GB(64, false); break;
       }
-    const int nbc = r.bstart[c + 1] - r.bstart[c];
-    const int blk = xcd_block(hb - r.bstart[c], nbc);
-    const int32_t* ord = r.order + o;
-    switch (c) {
-      case 0: gather_band<4>(r.band, ord, r.ncls[0], r.tA, r.tB, r.tslot, blk, arena, b, lambda, r.damp); break;
-      case 1: gather_band<8>(r.band, ord, r.ncls[1], r.tA, r.tB, r.tslot, blk, arena, b, lambda, r.damp); break;
-      case 2: gather_band<16>(r.band, ord, r.ncls[2], r.tA, r.tB, r.tslot, blk, arena, b, lambda, r.damp); break;
-      case 3: gather_band<32>(r.band, ord, r.ncls[3], r.tA, r.tB, r.tslot, blk, arena, b, lambda, r.damp); break;
-      default: gather_band<64>(r.band, ord, r.ncls[4], r.tA, r.tB, r.tslot, blk, arena, b, lambda, r.damp); break;
+    } else {
+      switch (c) {
+        case 0: DH_GB(4, false); break;
+        case 1: DH_GB(8, false); break;
+        case 2: DH_GB(16, false); break;
+        case 3: DH_GB(32, false); break;
+        default: DH_GB(64, false); break;
+      }
     }
+#undef DH_GB
   } else if (hb < r.nb_band + r.nb_grad) {
     gather_grad(r.grad, xcd_block(hb - r.nb_band, r.nb_grad), arena, r.gred);
   } else {
@@ -2336,11 +2427,31 @@ void launch_gather_reduced(const GatherDev& band, const int32_t* order, const in
   r.order = order;
   // each class's blocks start at a multiple of 8 (the XCD count, xcd_block)
   // (the classes cover every target: checked where the plan is uploaded)
-  r.bstart[0] = 0;
+  // The classes of the most entries are dispatched first: their lanes run
+  // the longest entry chains, and behind them the short targets fill in
+  // (DYNOHIP_GRED_ORDER=small restores the smallest-first order)
+  static const bool small_first = [] {
+    const char* e = std::getenv("DYNOHIP_GRED_ORDER");
+    return e && std::string(e) == "small";
+  }();
+  // classes of <= 32 entries: two lanes per entry (DYNOHIP_GRED_HALF=0: one)
+  static const bool half = [] {
+    const char* e = std::getenv("DYNOHIP_GRED_HALF");
+    return !(e && std::string(e) == "0");
+  }();
+  r.half = half ? 1 : 0;
+  int ooff = 0;
   for (int c = 0; c < ReducedGatherDev::kClasses; ++c) {
     r.ncls[c] = ncls[c];
-    const int lanes = 4 << c;
-    r.bstart[c + 1] = r.bstart[c] + (nblocks(static_cast<int64_t>(ncls[c]) * lanes) + 7) / 8 * 8;
+    r.ooff[c] = ooff;
+    ooff += ncls[c];
+  }
+  r.bstart[0] = 0;
+  for (int d = 0; d < ReducedGatherDev::kClasses; ++d) {
+    const int c = small_first ? d : ReducedGatherDev::kClasses - 1 - d;
+    r.cls[d] = c;
+    const int lanes = half ? std::min(64, 8 << c) : 4 << c;
+    r.bstart[d + 1] = r.bstart[d] + (nblocks(static_cast<int64_t>(ncls[c]) * lanes) + 7) / 8 * 8;
   }
   r.tA = tA;
   r.tB = tB;

@@ -43,12 +43,16 @@ struct PointGatherDev {
 struct ReducedGatherDev {
   GatherDev band;              // 6x6 reduced blocks (targets tA[t], tB[t])
   // the targets by entry count (Plan::red_order): class c, of <= 4 << c
-  // entries, runs 4 << c lanes per target (the last class 64 lanes);
-  // bstart[c] = first block of class c
+  // entries, runs 4 << c lanes per target (the last class 64 lanes), its
+  // targets at order[ooff[c], + ncls[c]); dispatch position d (blocks
+  // [bstart[d], bstart[d+1])) runs class cls[d]
   static constexpr int kClasses = 5;
   const int32_t* order = nullptr;
   int ncls[kClasses] = {};
+  int ooff[kClasses] = {};
+  int cls[kClasses] = {};
   int bstart[kClasses + 1] = {};
+  int half = 0;                // classes 0-3 with two lanes per entry
   const int32_t* tA = nullptr;
   const int32_t* tB = nullptr;
   const uint32_t* tslot = nullptr;   // Plan::red_slot

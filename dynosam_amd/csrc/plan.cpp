@@ -1101,7 +1101,7 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
                                     if (ps[G.m - 1] < p0 || ps[0] >= p1) return;
                                     const uint32_t g0 = G.out + 36u * (G.m * (G.m + 1) / 2);
                                     for (int a = 0; a < G.m; ++a)
-                                      fn(ps[a], GEntry{static_cast<uint32_t>(P.off_I6), g0 + 6u * a, 6, 1});
+                                      fn(ps[a], GEntry{static_cast<uint32_t>(P.off_I6), g0 + 6u * a, 6, kAddBlock});
                                   });
                           },
                           P.gGred);
@@ -1137,7 +1137,7 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
                                   for (int a = 0; a < G.m; ++a)
                                     for (int b = 0; b <= a; ++b)
                                       pf(ps[a], ps[b], GEntry{static_cast<uint32_t>(P.off_I6),
-                                                              G.out + 36u * (a * (a + 1) / 2 + b), 6, 1});
+                                                              G.out + 36u * (a * (a + 1) / 2 + b), 6, kAddBlock});
                                 });
                         },
                         P.gRed);

@@ -45,7 +45,11 @@ constexpr int kColStart[kNTypes][4] = {{0, 6, 0, 0}, {0, 3, 6, 0}, {0, 6, 0, 0},
                                        {0, 0, 0, 0}, {0, 3, 6, 12}, {0, 6, 12, 0}};
 constexpr int kTile = 64;
 
-// sum_e sign * A_e^T B_e, A_e: k x R, B_e: k x C (row-major blocks)
+// sum_e sign * A_e^T B_e, A_e: k x R, B_e: k x C (row-major blocks);
+// sign kAddBlock: A_e is the R x R identity (a = Plan::off_I6), and the
+// R x C block B_e is added as it is (the same bits as the identity product:
+// every other row adds an exact zero), without the identity's row loads
+constexpr int32_t kAddBlock = 2;
 struct GEntry {
   uint32_t a;
   uint32_t b;
