@@ -816,6 +816,15 @@ __device__ __forceinline__ int rs_index(int q) {
   return idx < N0 ? idx : -1;
 }
 
+// two doubles with one 16-byte load (p 16-byte aligned: the arena regions
+// and every block a reduced-gather entry reads start at even offsets, plan.cpp
+// "arena layout"; tests/test_plan_alignment.py)
+__device__ __forceinline__ void ld2(const double* p, double& x, double& y) {
+  const double2 v = *reinterpret_cast<const double2*>(p);
+  x = v.x;
+  y = v.y;
+}
+
 // Entry dimensions k are 3 or 6 (the row counts of the factor and point
 // blocks), so each entry is consumed in slices of S rows (S divides 3) whose
 // operand loads are all issued before the FMAs; the next entry's
@@ -880,10 +889,17 @@ __device__ __forceinline__ void group_accumulate(const int64_t* __restrict__ sta
       double a[S][R], b[S][CC];
 #pragma unroll
       for (int k = 0; k < S; ++k) {
+        if constexpr (R == 6 && CC == 6) {   // the reduced blocks: 16-byte row loads
 #pragma unroll
-        for (int r = 0; r < R; ++r) a[k][r] = A[(k0 + k) * R + r];
+          for (int r = 0; r < 6; r += 2) ld2(A + (k0 + k) * 6 + r, a[k][r], a[k][r + 1]);
 #pragma unroll
-        for (int c = 0; c < CC; ++c) b[k][c] = B[(k0 + k) * CC + c];
+          for (int c = 0; c < 6; c += 2) ld2(B + (k0 + k) * 6 + c, b[k][c], b[k][c + 1]);
+        } else {
+#pragma unroll
+          for (int r = 0; r < R; ++r) a[k][r] = A[(k0 + k) * R + r];
+#pragma unroll
+          for (int c = 0; c < CC; ++c) b[k][c] = B[(k0 + k) * CC + c];
+        }
       }
 #pragma unroll
       for (int k = 0; k < S; ++k)
@@ -1041,25 +1057,30 @@ __device__ __forceinline__ void store_reduced(const TileDev& b, const uint32_t (
   }
 }
 
-// Two lanes per entry (row halves h = q & 1 of the 6x6 product, 18 sums
-// each), entries (q >> 1) + G/2 j: every row of an entry's operands loaded
-// at once (one round trip for a 3-row entry instead of one per row). Each
-// sum keeps the FMA sequence of the one-lane form (rows in order).
-template <int G>
+// Two lanes per entry (row halves h of the 6x6 product, 18 sums each), the
+// entries sl + GS j of slot sl: every row of an entry's operands loaded at
+// once (one round trip for a 3-row entry instead of one per row). Each sum
+// keeps the FMA sequence of the one-lane form (rows in order, a slot's
+// entries in turn).
+template <int GS>
 __device__ __forceinline__ void accumulate_half(const int64_t* __restrict__ start, const GEntry* __restrict__ ent,
-                                                int t, int q, const double* __restrict__ arena, double (&acc)[18]) {
-  constexpr int GS = G / 2;
-  const int h = q & 1;
+                                                int t, int sl, int h, const double* __restrict__ arena,
+                                                double (&acc)[18]) {
 #pragma unroll
   for (int j = 0; j < 18; ++j) acc[j] = 0.0;
   const int64_t e1 = start[t + 1];
-  for (int64_t e = start[t] + (q >> 1); e < e1; e += GS) {
+  for (int64_t e = start[t] + sl; e < e1; e += GS) {
     const GEntry g = ent[e];
     const double* A = arena + g.a;
     const double* B = arena + g.b + 18 * h;
     if (g.sign == kAddBlock) {
 #pragma unroll
-      for (int j = 0; j < 18; ++j) acc[j] += B[j];
+      for (int j = 0; j < 18; j += 2) {
+        double x, y;
+        ld2(B + j, x, y);
+        acc[j] += x;
+        acc[j + 1] += y;
+      }
       continue;
     }
     const double sg = static_cast<double>(g.sign);
@@ -1070,7 +1091,7 @@ __device__ __forceinline__ void accumulate_half(const int64_t* __restrict__ star
 #pragma unroll
         for (int r = 0; r < 3; ++r) a[k][r] = A[(k0 + k) * 6 + 3 * h + r];
 #pragma unroll
-        for (int c = 0; c < 6; ++c) bb[k][c] = arena[g.b + (k0 + k) * 6 + c];
+        for (int c = 0; c < 6; c += 2) ld2(arena + g.b + (k0 + k) * 6 + c, bb[k][c], bb[k][c + 1]);
       }
 #pragma unroll
       for (int k = 0; k < 3; ++k)
@@ -1108,7 +1129,7 @@ __device__ __forceinline__ void gather_band(const GatherDev& g, const int32_t* _
   const uint32_t ts[4] = {tslot[4 * t], tslot[4 * t + 1], tslot[4 * t + 2], tslot[4 * t + 3]};
   if constexpr (Half) {
     double acc[18];
-    accumulate_half<G>(g.start, g.ent, t, q, arena, acc);
+    accumulate_half<G / 2>(g.start, g.ent, t, q >> 1, q & 1, arena, acc);
     constexpr int steps = ilog2(G) - 1;
     using Tree = RsTree<18, G / 2, steps>;
     double out[Tree::Out];
@@ -1137,6 +1158,61 @@ __device__ __forceinline__ void gather_band(const GatherDev& g, const int32_t* _
       const int idx = base + i;
       store_reduced(b, ts, A, B, idx / 6, idx % 6, out[i], lambda, damp);
     }
+  }
+}
+
+// Targets of more than 32 entries, two lanes per entry: 128 lanes (two waves)
+// per target, 64 slots, slot sl summing the entries sl, sl + 64, ... in turn
+// as lane sl of the 64-lane one-lane form does; the first reduce step (slot
+// mask 32, here the other wave) goes through LDS, the rest as gather_band's
+// (slot masks 16 .. 1): the same bits. Two targets per workgroup; every
+// thread reaches the barrier (no early exit).
+__device__ __forceinline__ void gather_band_wide(const GatherDev& g, const int32_t* __restrict__ order, int n,
+                                                 const int32_t* __restrict__ tA, const int32_t* __restrict__ tB,
+                                                 const uint32_t* __restrict__ tslot, int blk,
+                                                 const double* __restrict__ arena, const TileDev& b, double lambda,
+                                                 const uint8_t* __restrict__ damp) {
+  __shared__ double xch[kBlock * 9];
+  const int tid = threadIdx.x;
+  const int s = blk * (kBlock / 128) + tid / 128;
+  const int v = tid & 127;   // lane of the target's 128: slot v >> 1, half v & 1
+  const bool valid = s < n;
+  double acc[18];
+  int A = 0, B = 0;
+  uint32_t ts[4] = {0u, 0u, 0u, 0u};
+  if (valid) {
+    const int t = order[s];
+    A = tA[t];
+    B = tB[t];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ts[k] = tslot[4 * t + k];
+    accumulate_half<64>(g.start, g.ent, t, v >> 1, v & 1, arena, acc);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 18; ++j) acc[j] = 0.0;
+  }
+  // rs_step<18, 64> across the wave pair: keep one half, send the other
+  const bool up = (v & 64) != 0;
+  double* mine = xch + 9 * tid;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) mine[i] = up ? acc[i] : acc[9 + i];
+  __syncthreads();
+  const double* theirs = xch + 9 * (tid ^ 64);
+  double m9[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) m9[i] = (up ? acc[9 + i] : acc[i]) + theirs[i];
+  using Tree = RsTree<9, 32, 5>;
+  double out[Tree::Out];
+  Tree::run(m9, out, v);
+  int nv;
+  const int base = rs_span<18, 64, 6>(v, nv);
+  if (!valid) return;
+  const int r0 = 3 * (v & 1);
+#pragma unroll
+  for (int i = 0; i < Tree::Out; ++i) {
+    if (i >= nv) break;
+    const int idx = base + i;
+    store_reduced(b, ts, A, B, r0 + idx / 6, idx % 6, out[i], lambda, damp);
   }
 }
 
@@ -1188,7 +1264,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DYNOHIP_
         case 1: DH_GB(16, true); break;
         case 2: DH_GB(32, true); break;
         case 3: DH_GB(64, true); break;
-        default: DH_GB(64, false); break;
+        default:
+          if (r.wide) gather_band_wide(r.band, ord, r.ncls[c], r.tA, r.tB, r.tslot, blk, arena, b, lambda, r.damp);
+          else DH_GB(64, false);
+          break;
       }
     } else {
       switch (c) {
@@ -2440,6 +2519,13 @@ void launch_gather_reduced(const GatherDev& band, const int32_t* order, const in
     return !(e && std::string(e) == "0");
   }();
   r.half = half ? 1 : 0;
+  // with two lanes per entry, the last class on two waves per target
+  // (DYNOHIP_GRED_WIDE=0: one wave, one lane per entry)
+  static const bool wide = [] {
+    const char* e = std::getenv("DYNOHIP_GRED_WIDE");
+    return !(e && std::string(e) == "0");
+  }();
+  r.wide = half && wide ? 1 : 0;
   int ooff = 0;
   for (int c = 0; c < ReducedGatherDev::kClasses; ++c) {
     r.ncls[c] = ncls[c];
@@ -2450,7 +2536,7 @@ void launch_gather_reduced(const GatherDev& band, const int32_t* order, const in
   for (int d = 0; d < ReducedGatherDev::kClasses; ++d) {
     const int c = small_first ? d : ReducedGatherDev::kClasses - 1 - d;
     r.cls[d] = c;
-    const int lanes = half ? std::min(64, 8 << c) : 4 << c;
+    const int lanes = !half ? 4 << c : c < ReducedGatherDev::kClasses - 1 ? 8 << c : r.wide ? 128 : 64;
     r.bstart[d + 1] = r.bstart[d] + (nblocks(static_cast<int64_t>(ncls[c]) * lanes) + 7) / 8 * 8;
   }
   r.tA = tA;

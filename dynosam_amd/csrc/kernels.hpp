@@ -53,6 +53,7 @@ struct ReducedGatherDev {
   int cls[kClasses] = {};
   int bstart[kClasses + 1] = {};
   int half = 0;                // classes 0-3 with two lanes per entry
+  int wide = 0;                // (half) the last class on 128 lanes (gather_band_wide)
   const int32_t* tA = nullptr;
   const int32_t* tB = nullptr;
   const uint32_t* tslot = nullptr;   // Plan::red_slot

@@ -327,6 +327,7 @@ extern "C" int dynohip_plan_export(const dynohip_graph_view* g, const uint64_t* 
   else if (nm == "sep_slot_ranges") vec(P.sep_slot_ranges);
   else if (nm == "sep_tile_ranges") vec(P.sep_tile_ranges);
   else if (nm == "red_a") vec(P.red_A);
+  else if (nm == "red_order") vec(P.red_order);
   else if (nm.size() > 6 && nm.compare(nm.size() - 6, 6, "_start") == 0) {  // gather lists, e.g. "gRed_start"
     const std::string gl = nm.substr(0, nm.size() - 6);
     const GatherList* G = gl == "gD" ? &P.gD : gl == "gE" ? &P.gE : gl == "gGp" ? &P.gGp : gl == "gW" ? &P.gW
