@@ -1246,7 +1246,16 @@ __device__ __forceinline__ void gather_grad(const GatherDev& g, int blk, const d
 #endif
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DYNOHIP_GRED_WAVES))) void k_gather_reduced(ReducedGatherDev r, const double* __restrict__ arena,
                                                            TileDev b, double lambda) {
-  const int hb = blockIdx.x;
+  // the gradient's few, long waves (a wave per pose, ~75 entries) first,
+  // unless r.grad_first is 0: then after the band
+  int hb = blockIdx.x;
+  if (r.grad_first) {
+    if (hb < r.nb_grad) {
+      gather_grad(r.grad, xcd_block(hb, r.nb_grad), arena, r.gred);
+      return;
+    }
+    if (hb < r.nb_grad + r.nb_band) hb -= r.nb_grad;
+  }
   if (hb < r.nb_band) {
     // dispatch position d runs class cls[d]: targets order[ooff[c], + ncls[c])
     int d = 0;
@@ -2519,6 +2528,11 @@ void launch_gather_reduced(const GatherDev& band, const int32_t* order, const in
     return !(e && std::string(e) == "0");
   }();
   r.half = half ? 1 : 0;
+  static const bool grad_first = [] {
+    const char* e = std::getenv("DYNOHIP_GRED_GRAD_FIRST");
+    return !(e && std::string(e) == "0");
+  }();
+  r.grad_first = grad_first ? 1 : 0;
   // with two lanes per entry, the last class on two waves per target
   // (DYNOHIP_GRED_WIDE=0: one wave, one lane per entry)
   static const bool wide = [] {
