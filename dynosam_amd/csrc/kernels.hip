@@ -718,7 +718,10 @@ __global__ __launch_bounds__(kBlock) void k_linearize(GroupDev g, const double* 
 }
 
 template <unsigned M>
-__global__ __launch_bounds__(kBlock) void k_error(GroupDev g, const double* __restrict__ pose,
+#ifndef DYNOHIP_ERR_WAVES
+#define DYNOHIP_ERR_WAVES 1   // (1: the compiler's choice; a variant knob for A/B runs)
+#endif
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DYNOHIP_ERR_WAVES))) void k_error(GroupDev g, const double* __restrict__ pose,
                                                   const double* __restrict__ pt, SumDev sd) {
   // the extra sum (inputs from an earlier launch) by the first workgroup,
   // off the finishing block's path
