@@ -822,13 +822,31 @@ struct Formulation {
 
   // ---- WorldMotionAccessor::postUpdateCallback (WorldMotionEstimator.cc:68-152)
   //      + propogateObjectPoses (DynamicObjects.cc:48-190) ----
+  // object_centroid of every object seen at f, in one pass over the frame's
+  // dynamic landmarks (each object's float sums in the same landmark order)
   std::map<int32_t, std::array<double, 3>> centroids(uint64_t f) const {
     std::map<int32_t, std::array<double, 3>> out;
     const FrameNode* fn = map->frame(f);
-    if (!fn) return out;
-    for (int32_t obj : fn->objects_seen) {
-      double c[3];
-      if (object_centroid(f, obj, c)) out[obj] = {c[0], c[1], c[2]};
+    if (!fn || fn->objects_seen.empty()) return out;
+    struct Acc {
+      float s[3] = {0.f, 0.f, 0.f};
+      size_t n = 0;
+    };
+    std::map<int32_t, Acc> acc;
+    for (int32_t obj : fn->objects_seen) acc.emplace(obj, Acc{});
+    for (int64_t t : fn->dynamic_landmarks) {
+      auto a = acc.find(map->landmarks.at(t).object_id);
+      if (a == acc.end()) continue;
+      double p[3];
+      if (!dynamic_landmark(f, t, p)) continue;
+      for (int d = 0; d < 3; ++d) a->second.s[d] += static_cast<float>(p[d]);
+      ++a->second.n;
+    }
+    for (const auto& kv : acc) {
+      if (kv.second.n == 0) continue;
+      const float n = static_cast<float>(kv.second.n);
+      out[kv.first] = {static_cast<double>(kv.second.s[0] / n), static_cast<double>(kv.second.s[1] / n),
+                       static_cast<double>(kv.second.s[2] / n)};
     }
     return out;
   }
@@ -847,16 +865,25 @@ struct Formulation {
       return;
     }
     auto it = std::next(map->frames.begin());
+    // centroids(k) of one step is centroids(k_1) of the next (nothing here
+    // changes the estimates), and a frame without motions needs neither
+    std::map<int32_t, std::array<double, 3>> c_prev;
+    bool have_prev = false;
     for (; it != map->frames.end(); ++it) {
       const uint64_t k = it->first, k_1 = std::prev(it)->first;
       DB_CHECK(k_1 + 1 == k, DYNOHIP_ESTATE, "map frames are not consecutive");
-      const auto c_k = centroids(k), c_k_1 = centroids(k_1);
       // getObjectMotions(k): objects seen at k with a motion estimate
       std::vector<std::pair<int32_t, P3>> motions;
       for (int32_t obj : it->second.objects_seen) {
         P3 H;
         if (object_motion(k, obj, &H)) motions.emplace_back(obj, H);
       }
+      if (motions.empty()) {
+        have_prev = false;
+        continue;
+      }
+      const auto c_k_1 = have_prev ? std::move(c_prev) : centroids(k_1);
+      auto c_k = centroids(k);
       for (const auto& om : motions) {
         const int32_t obj = om.first;
         DB_CHECK(c_k.count(obj) && c_k_1.count(obj), DYNOHIP_ESTATE, "motion without object centroids");
@@ -897,6 +924,8 @@ struct Formulation {
           }
         }
       }
+      c_prev = std::move(c_k);   // the next step's c_k_1
+      have_prev = true;
     }
     object_pose_cache = object_poses;
   }
