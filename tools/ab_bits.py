@@ -2,7 +2,11 @@
   python tools/ab_bits.py run <out.npz> [configs...]   (DYNOSAM_AMD_LIB_DIR picks the build)
   python tools/ab_bits.py cmp <a.npz> <b.npz>
 `run` records, per config, one damped solve at lambda 1e-3 (the step, in value
-order) and a full LM run (final values and the per-iteration trace)."""
+order) and a full LM run (final values and the per-iteration trace).
+The round-4 comparisons (tools/r4_gred*.sh) ran against variants/old, the
+build of commit 7944cfa: `git archive 7944cfa dynosam_amd/csrc include | tar -x
+-C /tmp/old` and the hipcc line of tools/build_variant.sh run there, output
+into variants/old (git-ignored)."""
 import sys
 
 import numpy as np
