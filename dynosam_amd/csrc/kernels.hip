@@ -1108,6 +1108,81 @@ __device__ __forceinline__ void accumulate_half(const int64_t* __restrict__ star
   }
 }
 
+// Four lanes per entry (row half rh x column half ch of the 6x6 product, 9
+// sums each), the entries sl + GS j of slot sl; the same FMA sequence per
+// sum as the one-lane form.
+template <int GS>
+__device__ __forceinline__ void accumulate_quarter(const int64_t* __restrict__ start, const GEntry* __restrict__ ent,
+                                                   int t, int sl, int rh, int ch, const double* __restrict__ arena,
+                                                   double (&acc)[9]) {
+#pragma unroll
+  for (int j = 0; j < 9; ++j) acc[j] = 0.0;
+  const int64_t e1 = start[t + 1];
+  for (int64_t e = start[t] + sl; e < e1; e += GS) {
+    const GEntry g = ent[e];
+    const double* A = arena + g.a + 3 * rh;
+    const double* B = arena + g.b + 3 * ch;
+    if (g.sign == kAddBlock) {
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) acc[3 * r + c] += B[(3 * rh + r) * 6 + c];
+      continue;
+    }
+    const double sg = static_cast<double>(g.sign);
+    for (int k0 = 0; k0 < g.k; k0 += 3) {   // k is 3 or 6
+      double a[3][3], bb[3][3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          a[k][r] = A[(k0 + k) * 6 + r];
+          bb[k][r] = B[(k0 + k) * 6 + r];
+        }
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          const double ar = sg * a[k][r];
+#pragma unroll
+          for (int c = 0; c < 3; ++c) acc[3 * r + c] += ar * bb[k][c];
+        }
+    }
+  }
+}
+
+// Quarter: four lanes per entry (accumulate_quarter), a target of at most
+// G/4 entries; the 3x3 quarters reduce-scatter over the lane masks G/2 .. 4,
+// which pair the entries as the masks G/8 .. 1 of the one-lane form.
+template <int G>
+__device__ __forceinline__ void gather_band_quarter(const GatherDev& g, const int32_t* __restrict__ order, int n,
+                                                    const int32_t* __restrict__ tA, const int32_t* __restrict__ tB,
+                                                    const uint32_t* __restrict__ tslot, int blk,
+                                                    const double* __restrict__ arena, const TileDev& b,
+                                                    double lambda, const uint8_t* __restrict__ damp) {
+  const int s = (blk * kBlock + static_cast<int>(threadIdx.x)) / G;
+  const int q = threadIdx.x & (G - 1);
+  if (s >= n) return;
+  const int t = order[s];
+  const int A = tA[t], B = tB[t];
+  const uint32_t ts[4] = {tslot[4 * t], tslot[4 * t + 1], tslot[4 * t + 2], tslot[4 * t + 3]};
+  const int rh = (q >> 1) & 1, ch = q & 1;
+  double acc[9];
+  accumulate_quarter<G / 4>(g.start, g.ent, t, q >> 2, rh, ch, arena, acc);
+  constexpr int steps = ilog2(G) - 2;
+  using Tree = RsTree<9, G / 2, steps>;
+  double out[Tree::Out];
+  Tree::run(acc, out, q);
+  int valid;
+  const int base = rs_span<9, G / 2, steps>(q, valid);
+#pragma unroll
+  for (int i = 0; i < Tree::Out; ++i) {
+    if (i >= valid) break;
+    const int idx = base + i;
+    store_reduced(b, ts, A, B, 3 * rh + idx / 3, 3 * ch + idx % 3, out[i], lambda, damp);
+  }
+}
+
 // G lanes per 6x6 target, targets of class order[0, n). Lane q sums the
 // entries q, q + G, ... of its target; the sums are reduce-scattered over
 // the xor masks G/2 .. 1. A target of at most G entries thus sums them in
@@ -1270,7 +1345,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DYNOHIP_
     const int blk = xcd_block(hb - r.bstart[d], nbc);
     const int32_t* ord = r.order + r.ooff[c];
 #define DH_GB(G, H) gather_band<G, H>(r.band, ord, r.ncls[c], r.tA, r.tB, r.tslot, blk, arena, b, lambda, r.damp)
-    if (r.half) {
+#define DH_GQ(G) gather_band_quarter<G>(r.band, ord, r.ncls[c], r.tA, r.tB, r.tslot, blk, arena, b, lambda, r.damp)
+    if (r.quarter && c <= 2) {
+      switch (c) {
+        case 0: DH_GQ(16); break;
+        case 1: DH_GQ(32); break;
+        default: DH_GQ(64); break;
+      }
+    } else if (r.half) {
       switch (c) {
         case 0: DH_GB(8, true); break;
         case 1: DH_GB(16, true); break;
@@ -1291,6 +1373,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DYNOHIP_
       }
     }
 #undef DH_GB
+#undef DH_GQ
   } else if (hb < r.nb_band + r.nb_grad) {
     gather_grad(r.grad, xcd_block(hb - r.nb_band, r.nb_grad), arena, r.gred);
   } else {
@@ -2543,6 +2626,13 @@ void launch_gather_reduced(const GatherDev& band, const int32_t* order, const in
     return !(e && std::string(e) == "0");
   }();
   r.wide = half && wide ? 1 : 0;
+  // (half) classes of <= 16 entries with four lanes per entry (opt-in,
+  // DYNOHIP_GRED_QUARTER=1)
+  static const bool quarter = [] {
+    const char* e = std::getenv("DYNOHIP_GRED_QUARTER");
+    return e && std::string(e) == "1";
+  }();
+  r.quarter = half && quarter ? 1 : 0;
   int ooff = 0;
   for (int c = 0; c < ReducedGatherDev::kClasses; ++c) {
     r.ncls[c] = ncls[c];
@@ -2553,7 +2643,11 @@ void launch_gather_reduced(const GatherDev& band, const int32_t* order, const in
   for (int d = 0; d < ReducedGatherDev::kClasses; ++d) {
     const int c = small_first ? d : ReducedGatherDev::kClasses - 1 - d;
     r.cls[d] = c;
-    const int lanes = !half ? 4 << c : c < ReducedGatherDev::kClasses - 1 ? 8 << c : r.wide ? 128 : 64;
+    const int lanes = !half                              ? 4 << c
+                      : r.quarter && c <= 2                 ? 16 << c
+                      : c < ReducedGatherDev::kClasses - 1 ? 8 << c
+                      : r.wide                              ? 128
+                                                            : 64;
     r.bstart[d + 1] = r.bstart[d] + (nblocks(static_cast<int64_t>(ncls[c]) * lanes) + 7) / 8 * 8;
   }
   r.tA = tA;

@@ -55,6 +55,7 @@ struct ReducedGatherDev {
   int half = 0;                // classes 0-3 with two lanes per entry
   int wide = 0;                // (half) the last class on 128 lanes (gather_band_wide)
   int grad_first = 0;          // the gradient blocks dispatched before the band
+  int quarter = 0;             // (half) classes 0-2 with four lanes per entry
   const int32_t* tA = nullptr;
   const int32_t* tB = nullptr;
   const uint32_t* tslot = nullptr;   // Plan::red_slot
