@@ -442,7 +442,6 @@ __device__ __forceinline__ double linerr_one(const TypeDev& tp, int i, const dou
 // H area (plan.hpp): after the per-try partial blocks at `out`, [a] 6x6 full
 // (symmetric) J_a^T J_a, then [a] J_a^T b.
 __host__ __device__ constexpr uint32_t lone_h_off(int m) { return 36u * static_cast<uint32_t>(m * (m + 1) / 2) + 6u * m; }
-constexpr int kRec0 = kDim[0] * kCols[0] + kDim[0];   // PoseToPoint record stride (plan.cpp)
 constexpr int kLoneJ = 21;                            // staged per (point, a): J_x (3x6) | b (3)
 constexpr int kLoneHalf = kLoneSub / 2;               // points staged per pass (two passes)
 
@@ -471,7 +470,7 @@ __device__ double lone_lin_block(const LoneLinDev& d, int gb, const double* __re
   for (int k = 0; k < kLoneJ; ++k) sjv[k] = 0.0;
   if (valid) {
     const uint32_t rec = static_cast<uint32_t>(hdr[kLoneHdrRec + m * u + a]);
-    const int f = static_cast<int>((rec - d.t0.base) / kRec0);
+    const int f = static_cast<int>((rec - d.t0.base) / d.t0.stride);   // the planner's record stride
     // the pose and the point from the header (no dependent index load)
     const double* const v[4] = {pose + 12ll * hdr[kLoneHdrPose + a], pt + 3ll * hdr[kLoneHdrPt + u], nullptr, nullptr};
     double J[kDim[0] * kCols[0]], bb[3];
@@ -857,37 +856,6 @@ __device__ __forceinline__ void group_accumulate(const int64_t* __restrict__ sta
       continue;
     }
     const double sg = static_cast<double>(g.sign);
-#ifdef DYNOHIP_GRED_PIPE
-    if constexpr (S == 1) {
-      // the next row's operands are loaded while this row's FMAs run
-      double a[R], b[CC];
-#pragma unroll
-      for (int r = 0; r < R; ++r) a[r] = A[r];
-#pragma unroll
-      for (int c = 0; c < CC; ++c) b[c] = B[c];
-      for (int k = 0; k < g.k; ++k) {
-        double an[R], bn[CC];
-        const int kn = k + 1 < g.k ? k + 1 : k;
-#pragma unroll
-        for (int r = 0; r < R; ++r) an[r] = A[kn * R + r];
-#pragma unroll
-        for (int c = 0; c < CC; ++c) bn[c] = B[kn * CC + c];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const double ar = sg * a[r];
-#pragma unroll
-          for (int c = 0; c < CC; ++c) acc[r * CC + c] += ar * b[c];
-        }
-#pragma unroll
-        for (int r = 0; r < R; ++r) a[r] = an[r];
-#pragma unroll
-        for (int c = 0; c < CC; ++c) b[c] = bn[c];
-      }
-      e = en;
-      g = gn;
-      continue;
-    }
-#endif
     for (int k0 = 0; k0 < g.k; k0 += S) {
       double a[S][R], b[S][CC];
 #pragma unroll
@@ -1108,91 +1076,14 @@ __device__ __forceinline__ void accumulate_half(const int64_t* __restrict__ star
   }
 }
 
-// Four lanes per entry (row half rh x column half ch of the 6x6 product, 9
-// sums each), the entries sl + GS j of slot sl; the same FMA sequence per
-// sum as the one-lane form.
-template <int GS>
-__device__ __forceinline__ void accumulate_quarter(const int64_t* __restrict__ start, const GEntry* __restrict__ ent,
-                                                   int t, int sl, int rh, int ch, const double* __restrict__ arena,
-                                                   double (&acc)[9]) {
-#pragma unroll
-  for (int j = 0; j < 9; ++j) acc[j] = 0.0;
-  const int64_t e1 = start[t + 1];
-  for (int64_t e = start[t] + sl; e < e1; e += GS) {
-    const GEntry g = ent[e];
-    const double* A = arena + g.a + 3 * rh;
-    const double* B = arena + g.b + 3 * ch;
-    if (g.sign == kAddBlock) {
-#pragma unroll
-      for (int r = 0; r < 3; ++r)
-#pragma unroll
-        for (int c = 0; c < 3; ++c) acc[3 * r + c] += B[(3 * rh + r) * 6 + c];
-      continue;
-    }
-    const double sg = static_cast<double>(g.sign);
-    for (int k0 = 0; k0 < g.k; k0 += 3) {   // k is 3 or 6
-      double a[3][3], bb[3][3];
-#pragma unroll
-      for (int k = 0; k < 3; ++k)
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-          a[k][r] = A[(k0 + k) * 6 + r];
-          bb[k][r] = B[(k0 + k) * 6 + r];
-        }
-#pragma unroll
-      for (int k = 0; k < 3; ++k)
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-          const double ar = sg * a[k][r];
-#pragma unroll
-          for (int c = 0; c < 3; ++c) acc[3 * r + c] += ar * bb[k][c];
-        }
-    }
-  }
-}
-
-// Quarter: four lanes per entry (accumulate_quarter), a target of at most
-// G/4 entries; the 3x3 quarters reduce-scatter over the lane masks G/2 .. 4,
-// which pair the entries as the masks G/8 .. 1 of the one-lane form.
+// G lanes per 6x6 target, targets of class order[0, n), two lanes per
+// entry (accumulate_half): lane pair q >> 1 sums the entries q >> 1,
+// (q >> 1) + G/2, ... of its target, each lane one row half; the halves are
+// reduce-scattered over the lane masks G/2 .. 2. A target of at most G/2
+// entries thus sums them in exactly the pairing of a one-wave, one-lane-per-
+// entry form (whose upper lanes would only add exact zeros), with fewer idle
+// lanes and more entry loads in flight.
 template <int G>
-__device__ __forceinline__ void gather_band_quarter(const GatherDev& g, const int32_t* __restrict__ order, int n,
-                                                    const int32_t* __restrict__ tA, const int32_t* __restrict__ tB,
-                                                    const uint32_t* __restrict__ tslot, int blk,
-                                                    const double* __restrict__ arena, const TileDev& b,
-                                                    double lambda, const uint8_t* __restrict__ damp) {
-  const int s = (blk * kBlock + static_cast<int>(threadIdx.x)) / G;
-  const int q = threadIdx.x & (G - 1);
-  if (s >= n) return;
-  const int t = order[s];
-  const int A = tA[t], B = tB[t];
-  const uint32_t ts[4] = {tslot[4 * t], tslot[4 * t + 1], tslot[4 * t + 2], tslot[4 * t + 3]};
-  const int rh = (q >> 1) & 1, ch = q & 1;
-  double acc[9];
-  accumulate_quarter<G / 4>(g.start, g.ent, t, q >> 2, rh, ch, arena, acc);
-  constexpr int steps = ilog2(G) - 2;
-  using Tree = RsTree<9, G / 2, steps>;
-  double out[Tree::Out];
-  Tree::run(acc, out, q);
-  int valid;
-  const int base = rs_span<9, G / 2, steps>(q, valid);
-#pragma unroll
-  for (int i = 0; i < Tree::Out; ++i) {
-    if (i >= valid) break;
-    const int idx = base + i;
-    store_reduced(b, ts, A, B, 3 * rh + idx / 3, 3 * ch + idx % 3, out[i], lambda, damp);
-  }
-}
-
-// G lanes per 6x6 target, targets of class order[0, n). Lane q sums the
-// entries q, q + G, ... of its target; the sums are reduce-scattered over
-// the xor masks G/2 .. 1. A target of at most G entries thus sums them in
-// exactly the pairing of the 64-lane form (whose upper lanes would only add
-// exact zeros), so every class gives the same bits as one wave per target,
-// with fewer idle lanes and more entry loads in flight.
-// Half: two lanes per entry (accumulate_half), a target of at most G/2
-// entries; the row halves are reduce-scattered over the lane masks G/2 .. 2,
-// which pair the entries exactly as the masks G/4 .. 1 of the one-lane form.
-template <int G, bool Half>
 __device__ __forceinline__ void gather_band(const GatherDev& g, const int32_t* __restrict__ order, int n,
                                             const int32_t* __restrict__ tA, const int32_t* __restrict__ tB,
                                             const uint32_t* __restrict__ tslot, int blk,
@@ -1205,38 +1096,22 @@ __device__ __forceinline__ void gather_band(const GatherDev& g, const int32_t* _
   // the target's poses and tile slots, fetched ahead of its entries
   const int A = tA[t], B = tB[t];
   const uint32_t ts[4] = {tslot[4 * t], tslot[4 * t + 1], tslot[4 * t + 2], tslot[4 * t + 3]};
-  if constexpr (Half) {
-    double acc[18];
-    accumulate_half<G / 2>(g.start, g.ent, t, q >> 1, q & 1, arena, acc);
-    constexpr int steps = ilog2(G) - 1;
-    using Tree = RsTree<18, G / 2, steps>;
-    double out[Tree::Out];
-    Tree::run(acc, out, q);
-    int valid;
-    const int base = rs_span<18, G / 2, steps>(q, valid);
-    const int r0 = 3 * (q & 1);
+  double acc[18];
+  accumulate_half<G / 2>(g.start, g.ent, t, q >> 1, q & 1, arena, acc);
+  constexpr int steps = ilog2(G) - 1;
+  using Tree = RsTree<18, G / 2, steps>;
+  double out[Tree::Out];
+  Tree::run(acc, out, q);
+  int valid;
+  const int base = rs_span<18, G / 2, steps>(q, valid);
+  const int r0 = 3 * (q & 1);
 #pragma unroll
-    for (int i = 0; i < Tree::Out; ++i) {
-      if (i >= valid) break;
-      const int idx = base + i;
-      store_reduced(b, ts, A, B, r0 + idx / 6, idx % 6, out[i], lambda, damp);
-    }
-  } else {
-    double acc[36];
-    group_accumulate<6, 6, G, 1>(g.start, g.ent, t, q, arena, acc);
-    constexpr int steps = ilog2(G);
-    using Tree = RsTree<36, G / 2, steps>;
-    double out[Tree::Out];
-    Tree::run(acc, out, q);
-    int valid;
-    const int base = rs_span<36, G / 2, steps>(q, valid);
-#pragma unroll
-    for (int i = 0; i < Tree::Out; ++i) {
-      if (i >= valid) break;
-      const int idx = base + i;
-      store_reduced(b, ts, A, B, idx / 6, idx % 6, out[i], lambda, damp);
-    }
+  for (int i = 0; i < Tree::Out; ++i) {
+    if (i >= valid) break;
+    const int idx = base + i;
+    store_reduced(b, ts, A, B, r0 + idx / 6, idx % 6, out[i], lambda, damp);
   }
+
 }
 
 // Targets of more than 32 entries, two lanes per entry: 128 lanes (two waves)
@@ -1324,16 +1199,13 @@ __device__ __forceinline__ void gather_grad(const GatherDev& g, int blk, const d
 #endif
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DYNOHIP_GRED_WAVES))) void k_gather_reduced(ReducedGatherDev r, const double* __restrict__ arena,
                                                            TileDev b, double lambda) {
-  // the gradient's few, long waves (a wave per pose, ~75 entries) first,
-  // unless r.grad_first is 0: then after the band
+  // the gradient's few, long waves (a wave per pose, ~75 entries) first
   int hb = blockIdx.x;
-  if (r.grad_first) {
-    if (hb < r.nb_grad) {
-      gather_grad(r.grad, xcd_block(hb, r.nb_grad), arena, r.gred);
-      return;
-    }
-    if (hb < r.nb_grad + r.nb_band) hb -= r.nb_grad;
+  if (hb < r.nb_grad) {
+    gather_grad(r.grad, xcd_block(hb, r.nb_grad), arena, r.gred);
+    return;
   }
+  if (hb < r.nb_grad + r.nb_band) hb -= r.nb_grad;
   if (hb < r.nb_band) {
     // dispatch position d runs class cls[d]: targets order[ooff[c], + ncls[c])
     int d = 0;
@@ -1344,38 +1216,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DYNOHIP_
     const int nbc = r.bstart[d + 1] - r.bstart[d];
     const int blk = xcd_block(hb - r.bstart[d], nbc);
     const int32_t* ord = r.order + r.ooff[c];
-#define DH_GB(G, H) gather_band<G, H>(r.band, ord, r.ncls[c], r.tA, r.tB, r.tslot, blk, arena, b, lambda, r.damp)
-#define DH_GQ(G) gather_band_quarter<G>(r.band, ord, r.ncls[c], r.tA, r.tB, r.tslot, blk, arena, b, lambda, r.damp)
-    if (r.quarter && c <= 2) {
-      switch (c) {
-        case 0: DH_GQ(16); break;
-        case 1: DH_GQ(32); break;
-        default: DH_GQ(64); break;
-      }
-    } else if (r.half) {
-      switch (c) {
-        case 0: DH_GB(8, true); break;
-        case 1: DH_GB(16, true); break;
-        case 2: DH_GB(32, true); break;
-        case 3: DH_GB(64, true); break;
-        default:
-          if (r.wide) gather_band_wide(r.band, ord, r.ncls[c], r.tA, r.tB, r.tslot, blk, arena, b, lambda, r.damp);
-          else DH_GB(64, false);
-          break;
-      }
-    } else {
-      switch (c) {
-        case 0: DH_GB(4, false); break;
-        case 1: DH_GB(8, false); break;
-        case 2: DH_GB(16, false); break;
-        case 3: DH_GB(32, false); break;
-        default: DH_GB(64, false); break;
-      }
+#define DH_GB(G) gather_band<G>(r.band, ord, r.ncls[c], r.tA, r.tB, r.tslot, blk, arena, b, lambda, r.damp)
+    switch (c) {
+      case 0: DH_GB(8); break;
+      case 1: DH_GB(16); break;
+      case 2: DH_GB(32); break;
+      case 3: DH_GB(64); break;
+      default: gather_band_wide(r.band, ord, r.ncls[c], r.tA, r.tB, r.tslot, blk, arena, b, lambda, r.damp); break;
     }
 #undef DH_GB
-#undef DH_GQ
-  } else if (hb < r.nb_band + r.nb_grad) {
-    gather_grad(r.grad, xcd_block(hb - r.nb_band, r.nb_grad), arena, r.gred);
   } else {
     const int row = b.n_red + (hb - r.nb_band - r.nb_grad) * kBlock + static_cast<int>(threadIdx.x);
     if (row < b.NT * kTile) b.slots[tile_index(b, row, row)] = 1.0;
@@ -2602,37 +2451,9 @@ void launch_gather_reduced(const GatherDev& band, const int32_t* order, const in
   // each class's blocks start at a multiple of 8 (the XCD count, xcd_block)
   // (the classes cover every target: checked where the plan is uploaded)
   // The classes of the most entries are dispatched first: their lanes run
-  // the longest entry chains, and behind them the short targets fill in
-  // (DYNOHIP_GRED_ORDER=small restores the smallest-first order)
-  static const bool small_first = [] {
-    const char* e = std::getenv("DYNOHIP_GRED_ORDER");
-    return e && std::string(e) == "small";
-  }();
-  // classes of <= 32 entries: two lanes per entry (DYNOHIP_GRED_HALF=0: one)
-  static const bool half = [] {
-    const char* e = std::getenv("DYNOHIP_GRED_HALF");
-    return !(e && std::string(e) == "0");
-  }();
-  r.half = half ? 1 : 0;
-  static const bool grad_first = [] {
-    const char* e = std::getenv("DYNOHIP_GRED_GRAD_FIRST");
-    return !(e && std::string(e) == "0");
-  }();
-  r.grad_first = grad_first ? 1 : 0;
-  // with two lanes per entry, the last class on two waves per target
-  // (DYNOHIP_GRED_WIDE=0: one wave, one lane per entry)
-  static const bool wide = [] {
-    const char* e = std::getenv("DYNOHIP_GRED_WIDE");
-    return !(e && std::string(e) == "0");
-  }();
-  r.wide = half && wide ? 1 : 0;
-  // (half) classes of <= 16 entries with four lanes per entry (opt-in,
-  // DYNOHIP_GRED_QUARTER=1)
-  static const bool quarter = [] {
-    const char* e = std::getenv("DYNOHIP_GRED_QUARTER");
-    return e && std::string(e) == "1";
-  }();
-  r.quarter = half && quarter ? 1 : 0;
+  // the longest entry chains, and behind them the short targets fill in.
+  // Classes of <= 32 entries run two lanes per entry, the last class two
+  // waves per target (gather_band_wide); the gradient's waves go first.
   int ooff = 0;
   for (int c = 0; c < ReducedGatherDev::kClasses; ++c) {
     r.ncls[c] = ncls[c];
@@ -2641,13 +2462,9 @@ void launch_gather_reduced(const GatherDev& band, const int32_t* order, const in
   }
   r.bstart[0] = 0;
   for (int d = 0; d < ReducedGatherDev::kClasses; ++d) {
-    const int c = small_first ? d : ReducedGatherDev::kClasses - 1 - d;
+    const int c = ReducedGatherDev::kClasses - 1 - d;
     r.cls[d] = c;
-    const int lanes = !half                              ? 4 << c
-                      : r.quarter && c <= 2                 ? 16 << c
-                      : c < ReducedGatherDev::kClasses - 1 ? 8 << c
-                      : r.wide                              ? 128
-                                                            : 64;
+    const int lanes = c < ReducedGatherDev::kClasses - 1 ? 8 << c : 128;
     r.bstart[d + 1] = r.bstart[d] + (nblocks(static_cast<int64_t>(ncls[c]) * lanes) + 7) / 8 * 8;
   }
   r.tA = tA;

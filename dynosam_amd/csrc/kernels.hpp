@@ -43,19 +43,15 @@ struct PointGatherDev {
 struct ReducedGatherDev {
   GatherDev band;              // 6x6 reduced blocks (targets tA[t], tB[t])
   // the targets by entry count (Plan::red_order): class c, of <= 4 << c
-  // entries, runs 4 << c lanes per target (the last class 64 lanes), its
-  // targets at order[ooff[c], + ncls[c]); dispatch position d (blocks
-  // [bstart[d], bstart[d+1])) runs class cls[d]
+  // entries, runs 8 << c lanes per target (two per entry; the last class
+  // 128 lanes), its targets at order[ooff[c], + ncls[c]); dispatch position d
+  // (blocks [bstart[d], bstart[d+1])) runs class cls[d]
   static constexpr int kClasses = 5;
   const int32_t* order = nullptr;
   int ncls[kClasses] = {};
   int ooff[kClasses] = {};
   int cls[kClasses] = {};
   int bstart[kClasses + 1] = {};
-  int half = 0;                // classes 0-3 with two lanes per entry
-  int wide = 0;                // (half) the last class on 128 lanes (gather_band_wide)
-  int grad_first = 0;          // the gradient blocks dispatched before the band
-  int quarter = 0;             // (half) classes 0-2 with four lanes per entry
   const int32_t* tA = nullptr;
   const int32_t* tB = nullptr;
   const uint32_t* tslot = nullptr;   // Plan::red_slot
@@ -151,13 +147,7 @@ struct TileSchedDev {
   // one-launch backward: hand-offs on the data (k_back_poll; x and partials
   // sentinel-filled before each solve) instead of epoch flags (k_back_persist)
   bool back_poll = true;
-  // k_back_wide's items (first part, parts): consecutive parts 2j, 2j+1 of a
-  // column (at most kBackPersistMax items; 0 items: k_back_poll)
-  const int2* witems = nullptr;
-  int n_witems = 0;
 };
-// k_back_wide's items from the part list: (first part, 1 or 2)
-std::vector<int32_t> back_wide_items(const std::vector<BackPart>& parts);
 
 // the sentinel k_back_poll's consumers wait past (a signalling NaN)
 constexpr uint64_t kBackSentinel = 0xFFF4DEADBEEFCAFEull;
@@ -259,8 +249,8 @@ void launch_backsub(const ChainDev& c, const double* arena, const double* dpose,
 // Wide levels (many update tasks) run their updates as a separate
 // small-LDS kernel on `side`, concurrently with the level's panels on `s`
 // (joined through ev_main / ev_side).
-// the two halves of launch_tile_cholesky_solve (the partitioned solve runs
-// the forward tasks in two phases around the exchange)
+// (launch_tile_backward after it completes the solve; the partitioned solve
+// runs the forward tasks in two phases around the exchange)
 void launch_tile_forward(const TileDev& b, const TileSchedDev& sd, const std::vector<int32_t>& flevel,
                          const std::vector<int32_t>& fpanels, double* Linv, const double* r, double* contrib,
                          double* y, int* fail, hipStream_t s, hipStream_t side, hipEvent_t ev_main,
@@ -269,12 +259,11 @@ void launch_tile_forward(const TileDev& b, const TileSchedDev& sd, const std::ve
 // (x = A^-1 r in natural tile order; tilechol.hip k_small_solve)
 constexpr int kSmallNT = 4;
 void launch_small_solve(const TileDev& b, const double* r, double* x, int* fail, hipStream_t s);
+// sentinel_filled: x and sd.partials hold kBackSentinel for this solve (the
+// hand-off form k_back_poll needs it; without it the flag form runs)
 void launch_tile_backward(const TileDev& b, const TileSchedDev& sd, const std::vector<int32_t>& blevel,
-                          const double* Linv, const double* y, double* x, int* fail, hipStream_t s);
-void launch_tile_cholesky_solve(const TileDev& b, const TileSchedDev& sd, const std::vector<int32_t>& flevel,
-                                const std::vector<int32_t>& fpanels, const std::vector<int32_t>& blevel,
-                                double* Linv, const double* r, double* contrib, double* y, double* x, int* fail,
-                                hipStream_t s, hipStream_t side, hipEvent_t ev_main, hipEvent_t ev_side);
+                          const double* Linv, const double* y, double* x, int* fail, hipStream_t s,
+                          bool sentinel_filled);
 
 void launch_retract(int n_pose, int n_pt, const double* pose, const double* pt, const double* dpose,
                     const double* dpt, double* pose_out, double* pt_out, hipStream_t s);

@@ -441,9 +441,6 @@ struct dynohip_solver {
   DevBuf<int32_t> tile_pos, row_start, row_col, row_slot, bent, pairs;
   DevBuf<TileTask> ftask;
   DevBuf<BackPart> bpart;
-  DevBuf<int32_t> witems;   // k_back_wide's (first part, parts) items
-  std::vector<int32_t> witems_h;   // their host copy (read by Uploads::run)
-  bool back_wide = false;   // DYNOHIP_BACK_WIDE=1: two parts per workgroup (k_back_wide; measured no faster)
   bool small_solve = false; // DYNOHIP_SMALL_SOLVE=1: systems of <= kSmallNT tiles in one workgroup (slower)
   DevBuf<double> bpartials;
   DevBuf<int> arrive;
@@ -617,9 +614,6 @@ int upload_plan(dynohip_solver* s, bool types_done = false) {
   HIPCHK(s, s->contrib.alloc(static_cast<size_t>(P.n_slots) * kTile));
   HIPCHK(s, up.add(s->bpart, P.bpart));
   // (kept in the solver: Uploads packs the host arrays at up.run below)
-  s->witems_h = back_wide_items(P.bpart);
-  HIPCHK(s, up.add(s->witems, s->witems_h));
-  s->sd.n_witems = s->back_wide ? static_cast<int>(s->witems_h.size() / 2) : 0;
   HIPCHK(s, s->bpartials.alloc(static_cast<size_t>(P.n_partials) * kTile + 1));
   HIPCHK(s, s->arrive.alloc(static_cast<size_t>(P.NT) + 1));
   HIPCHK(s, hipMemsetAsync(s->arrive.p, 0, (static_cast<size_t>(P.NT) + 1) * sizeof(int), st));
@@ -693,7 +687,6 @@ int upload_plan(dynohip_solver* s, bool types_done = false) {
   s->sd.ftask = s->ftask.p;
   s->sd.pairs = s->pairs.p;
   s->sd.bpart = s->bpart.p;
-  s->sd.witems = reinterpret_cast<const int2*>(s->witems.p);
   s->sd.partials = s->bpartials.p;
   s->sd.arrive = s->arrive.p;
   s->sd.done = s->done.p;
@@ -914,7 +907,7 @@ int enqueue_try(dynohip_solver* s, double lambda) {
     // (ms_cholesky of a partitioned handle spans both forward phases and the
     // exchange between them)
     if (timed) (void)hipEventRecord(s->ev[5], st);
-    launch_tile_backward(s->bd, s->sd, P.bplevel, s->linv.p, y, x, s->failp, st);
+    launch_tile_backward(s->bd, s->sd, P.bplevel, s->linv.p, y, x, s->failp, st, s->sd.back_poll);
   } else if (s->small_solve && P.NT >= 1 && P.NT <= kSmallNT) {
     // a window-sized system: factorisation and both substitutions in one
     // workgroup (k_small_solve; ms_cholesky spans all of it)
@@ -924,7 +917,7 @@ int enqueue_try(dynohip_solver* s, double lambda) {
     launch_tile_forward(s->bd, s->sd, P.flevel, P.fpanels, s->linv.p, s->gred.p, s->contrib.p, y, s->failp, st,
                         s->side, s->ev_main, s->ev_side);
     if (timed) (void)hipEventRecord(s->ev[5], st);
-    launch_tile_backward(s->bd, s->sd, P.bplevel, s->linv.p, y, x, s->failp, st);
+    launch_tile_backward(s->bd, s->sd, P.bplevel, s->linv.p, y, x, s->failp, st, s->sd.back_poll);
   }
   if (timed) (void)hipEventRecord(s->ev[6], st);
   // pose deltas are x[0 .. 6 n_pose) in pose-index order
@@ -1244,7 +1237,6 @@ int dynohip_create(int device_id, dynohip_solver** out) {
   if (const char* e = std::getenv("DYNOHIP_FUSED_LONE")) s->fused_env = std::atoi(e) != 0;
   if (const char* e = std::getenv("DYNOHIP_BACK_POLL")) s->sd.back_poll = std::atoi(e) != 0;
   if (const char* e = std::getenv("DYNOHIP_CHAIN_LONE")) s->chain_lone = std::atoi(e) != 0;
-  if (const char* e = std::getenv("DYNOHIP_BACK_WIDE")) s->back_wide = std::atoi(e) != 0;
   if (const char* e = std::getenv("DYNOHIP_SMALL_SOLVE")) s->small_solve = std::atoi(e) != 0;
   s->stream = r.stream;
   s->side = r.side;

@@ -1435,108 +1435,6 @@ __global__ __launch_bounds__(kBackThreads) void k_back_poll(TileDev b, const Bac
   if (tid == 0 && bad) atomicOr(fail, 2);
 }
 
-// Two consecutive parts of one column per workgroup (512 threads, two
-// groups of k_back_poll's 256): both parts' L tiles are in registers before
-// the wait, and a column of at most two parts needs no partial hand-off at
-// all (its parts meet in LDS), so a level costs one memory round trip: the
-// poll of the x rows. Item w = (first part, parts) of the plan's part list
-// (launch_tile_backward pairs parts 2j, 2j+1 of a column). The arithmetic is
-// k_back_poll's part by part, and the parts are added in part order from 0.0
-// as there, so the two kernels give the same bits. One workgroup per CU (the
-// registers of 2 x 4 prefetched tiles).
-constexpr int kBackWide = 2 * kBackThreads;
-__global__ __launch_bounds__(kBackWide) void k_back_wide(TileDev b, const BackPart* __restrict__ parts,
-                                                         const int2* __restrict__ items,
-                                                         const int32_t* __restrict__ ent,
-                                                         const double* __restrict__ Linv,
-                                                         const double* __restrict__ y, double* x,
-                                                         double* partials, int* fail) {
-  constexpr int NP = kBackThreads / T;
-  constexpr int CH = DYNOHIP_BACK_CH;
-  __shared__ double part[2][NP][T];
-  __shared__ double gsum[2][T];
-  __shared__ double rv[T];
-  __shared__ double xs[2][CH][T];
-  const int2 it = items[blockIdx.x];
-  const int tid = threadIdx.x, grp = tid >> 8, gt = tid & (kBackThreads - 1), c = gt & (T - 1), q = gt >> 6;
-  const bool act = grp < it.y;
-  const BackPart pt = parts[it.x + (act ? grp : 0)];
-  const int ne = act ? pt.end - pt.beg : 0;
-  int bad = 0;
-  double lv[CH][16];
-#pragma unroll
-  for (int j = 0; j < CH; ++j)
-    if (j < ne) {
-      const double* L = slot_ptr(b, ent[2 * (pt.beg + j)]);
-#pragma unroll
-      for (int m = 0; m < 16; ++m) lv[j][m] = L[(q + NP * m) * T + c];
-    }
-  const BackPart p0 = parts[it.x];
-  const bool solver = p0.nparts == 1 || p0.part == 0;   // this item holds part 0 of its column
-  double li[16];
-  if (solver) {
-    const double* Li = Linv + static_cast<int64_t>(p0.k) * T * T;
-#pragma unroll
-    for (int m = 0; m < 16; ++m) li[m] = Li[(q + NP * m) * T + c];
-  }
-  const double yk = (solver && tid < T) ? y[static_cast<int64_t>(p0.k) * T + tid] : 0.0;
-  // each group polls its part's x rows (parts of <= CH entries: one chunk)
-  if (gt < ne * T) {
-    double v;
-    if (!poll_value(x + static_cast<int64_t>(ent[2 * (pt.beg + (gt >> 6)) + 1]) * T + c, v)) bad = 1;
-    xs[grp][gt >> 6][c] = v;
-  }
-  __syncthreads();
-  double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-  for (int j = 0; j < CH; ++j)
-    if (j < ne) {
-#pragma unroll
-      for (int m = 0; m < 16; ++m) s[m & 7] += lv[j][m] * xs[grp][j][q + NP * m];
-    }
-  part[grp][q][c] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
-  __syncthreads();
-  if (gt < T) gsum[grp][gt] = (part[grp][0][gt] + part[grp][1][gt]) + (part[grp][2][gt] + part[grp][3][gt]);
-  __syncthreads();
-  if (!solver) {
-    // hand both parts' partials to part 0's workgroup
-    bad = __syncthreads_or(bad);
-    if (act && gt < T)
-      st_sc1(partials + static_cast<int64_t>(pt.pbase + pt.part) * T + gt, bad ? __builtin_nan("") : gsum[grp][gt]);
-    if (tid == 0 && bad) atomicOr(fail, 2);
-    return;
-  }
-  if (tid < T) {
-    double sum;
-    if (p0.nparts == 1) {
-      sum = gsum[0][tid];
-    } else {
-      sum = 0.0;
-      for (int p = 0; p < p0.nparts; ++p) {
-        double v = p < it.y ? gsum[p][tid] : 0.0;
-        if (p >= it.y && !poll_value(partials + static_cast<int64_t>(p0.pbase + p) * T + tid, v)) bad = 1;
-        sum += v;
-      }
-    }
-    rv[tid] = yk - sum;
-  }
-  __syncthreads();
-  // x_k[c] = sum_{m >= c} Linv[m][c] rv[m] (group 0)
-  double t = 0.0;
-#pragma unroll
-  for (int m = 0; m < 16; ++m) {
-    const int row = q + NP * m;
-    if (row >= c) t += li[m] * rv[row];
-  }
-  if (grp == 0) part[0][q][c] = t;
-  bad = __syncthreads_or(bad);
-  if (tid < T) {
-    const double xv = (part[0][0][tid] + part[0][1][tid]) + (part[0][2][tid] + part[0][3][tid]);
-    st_sc1(x + static_cast<int64_t>(p0.k) * T + tid, bad ? __builtin_nan("") : xv);
-  }
-  if (tid == 0 && bad) atomicOr(fail, 2);
-}
-
 // ---- small reduced systems (<= kSmallNT tiles): one workgroup ------------
 // The sliding-window solves (backend.flags: 10-frame windows) have reduced
 // systems of at most four tiles, where the tile DAG is a chain of four
@@ -1800,36 +1698,19 @@ void launch_tile_forward(const TileDev& b, const TileSchedDev& sd, const std::ve
   }
 }
 
-std::vector<int32_t> back_wide_items(const std::vector<BackPart>& parts) {
-  std::vector<int32_t> it;
-  // k_back_wide takes a part's entries in one chunk: with longer parts
-  // (DYNOHIP_BACK_PART_TILES > DYNOHIP_BACK_CH) there are no items, and the
-  // part-per-workgroup kernel runs
-  for (const BackPart& p : parts)
-    if (p.end - p.beg > DYNOHIP_BACK_CH) return it;
-  for (size_t p = 0; p < parts.size();) {
-    const bool pair = p + 1 < parts.size() && parts[p + 1].k == parts[p].k && parts[p].part % 2 == 0 &&
-                      parts[p + 1].part == parts[p].part + 1;
-    it.push_back(static_cast<int32_t>(p));
-    it.push_back(pair ? 2 : 1);
-    p += pair ? 2 : 1;
-  }
-  return it;
-}
-
 void launch_tile_backward(const TileDev& b, const TileSchedDev& sd, const std::vector<int32_t>& blevel,
-                          const double* Linv, const double* y, double* x, int* fail, hipStream_t s) {
+                          const double* Linv, const double* y, double* x, int* fail, hipStream_t s,
+                          bool sentinel_filled) {
   const int nparts = blevel.empty() ? 0 : blevel.back();
   if (nparts > 0 && nparts <= kBackPersistMax && !sd.level_backward) {
-    if (sd.back_poll && sd.witems && sd.n_witems > 0 && sd.n_witems <= kBackPersistMax)
-      // two parts per workgroup. One workgroup fits a CU (its registers), so
-      // past 256 items not all are resident: the items are in backward-level
-      // (topological) order and each XCD dispatches its workgroups in index
-      // order, so the lowest-indexed waiting workgroup only ever waits for a
-      // running one (the part-per-workgroup form relies on the same past 512
-      // parts, two per CU)
-      k_back_wide<<<sd.n_witems, kBackWide, 0, s>>>(b, sd.bpart, sd.witems, sd.bent, Linv, y, x, sd.partials, fail);
-    else if (sd.back_poll)   // x and the partials hold the sentinel (k_chain_factor's fill)
+    // past 512 parts (two per CU) not all are resident: the parts are in
+    // backward-level (topological) order and each XCD dispatches its
+    // workgroups in index order, so the lowest-indexed waiting part only ever
+    // waits for a running one. k_back_poll reads "not written yet" as
+    // kBackSent in x and the partials, so it runs only when the caller has
+    // filled them for this solve (enqueue_try: the chain launch's ZeroDev.s);
+    // otherwise the flag form, which needs no fill
+    if (sd.back_poll && sentinel_filled)
       k_back_poll<<<nparts, kBackThreads, 0, s>>>(b, sd.bpart, sd.bent, Linv, y, x, sd.partials, fail);
     else
       k_back_persist<<<nparts, kBackThreads, 0, s>>>(b, sd.bpart, sd.bent, Linv, y, x, sd.partials, sd.arrive,
@@ -1845,14 +1726,6 @@ void launch_tile_backward(const TileDev& b, const TileSchedDev& sd, const std::v
 void launch_small_solve(const TileDev& b, const double* r, double* x, int* fail, hipStream_t s) {
   if (b.NT <= 0 || b.NT > kSmallNT) return;   // the host checks the size (solver.cpp)
   k_small_solve<<<1, kSmallWaves * 64, 0, s>>>(b, r, x, fail);
-}
-
-void launch_tile_cholesky_solve(const TileDev& b, const TileSchedDev& sd, const std::vector<int32_t>& flevel,
-                                const std::vector<int32_t>& fpanels, const std::vector<int32_t>& blevel,
-                                double* Linv, const double* r, double* contrib, double* y, double* x, int* fail,
-                                hipStream_t s, hipStream_t side, hipEvent_t ev_main, hipEvent_t ev_side) {
-  launch_tile_forward(b, sd, flevel, fpanels, Linv, r, contrib, y, fail, s, side, ev_main, ev_side);
-  launch_tile_backward(b, sd, blevel, Linv, y, x, fail, s);
 }
 
 }  // namespace dynohip

@@ -24,8 +24,17 @@
 
 /* the shared transcendental functions (sin, tan, acos) of the pose
    arithmetic: the same IEEE operations as the kernels (se3.hpp), in place
-   of glibc's, see trig.h */
+   of glibc's, see trig.h. Built with -DORACLE_LIBM_TRIG (liboracle_libm.so)
+   the oracle calls glibc's instead, as GTSAM does: the independent check
+   that trig.h's rounding is not what makes the two sides agree
+   (tests/test_trig.py, tests/test_gpu_parity.py). */
+#ifdef ORACLE_LIBM_TRIG
+#define dht_sin sin
+#define dht_tan tan
+#define dht_acos acos
+#else
 #include "../dynosam_amd/csrc/trig.h"
+#endif
 
 #ifndef M_PI
 #define M_PI 3.14159265358979323846

@@ -12,15 +12,18 @@ from dynosam_amd import _abi
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_SO = os.path.join(ROOT, "oracle", "build", "liboracle.so")
-_lib = None
+# the same restatement with glibc's sin / tan / acos (what GTSAM calls) in
+# place of the shared trig.h: the independent check of trig.h's rounding
+ORACLE_LIBM_SO = os.path.join(ROOT, "oracle", "build", "liboracle_libm.so")
+_libs = {}
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(ORACLE_SO):
-            raise RuntimeError(f"{ORACLE_SO} missing: run `make -C oracle`")
-        L = C.CDLL(ORACLE_SO)
+def lib(libm=False):
+    if libm not in _libs:
+        path = ORACLE_LIBM_SO if libm else ORACLE_SO
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} missing: run `make -C oracle`")
+        L = C.CDLL(path)
         P = C.POINTER
         vp = C.c_void_p
         L.oracle_create.argtypes = [P(_abi.GraphView), P(C.c_uint64), P(C.c_uint8), P(C.c_double), C.c_size_t, P(vp)]
@@ -62,8 +65,8 @@ def lib():
         L.oracle_reconstruct_labeled.argtypes = [C.c_uint64, C.c_ubyte, P(C.c_int), P(C.c_uint64)]
         L.oracle_chr_extract.argtypes = [C.c_uint64]
         L.oracle_chr_extract.restype = C.c_ubyte
-        _lib = L
-    return _lib
+        _libs[libm] = L
+    return _libs[libm]
 
 
 def dptr(a):
@@ -73,8 +76,8 @@ def dptr(a):
 class Oracle:
     """CPU restatement of LevenbergMarquardtOptimizer(graph, values).optimize()."""
 
-    def __init__(self, graph, values, dense=False, threads=1, reverse_sums=False):
-        L = lib()
+    def __init__(self, graph, values, dense=False, threads=1, reverse_sums=False, libm=False):
+        L = self.L = lib(libm)
         self.graph = graph
         self.values = values
         self._gv = graph.view()
@@ -98,53 +101,53 @@ class Oracle:
 
     def __del__(self):
         if getattr(self, "h", None):
-            lib().oracle_destroy(self.h)
+            self.L.oracle_destroy(self.h)
             self.h = None
 
     def error(self):
-        return lib().oracle_error(self.h)
+        return self.L.oracle_error(self.h)
 
     def optimize(self, params=None):
         params = params or _abi.LMParams.gtsam_default()
         s = _abi.LMSummary()
-        lib().oracle_optimize(self.h, C.byref(params), C.byref(s))
+        self.L.oracle_optimize(self.h, C.byref(params), C.byref(s))
         return s
 
     def reset(self, params=None):
         params = params or _abi.LMParams.gtsam_default()
-        lib().oracle_lm_reset(self.h, C.byref(params))
+        self.L.oracle_lm_reset(self.h, C.byref(params))
 
     def iterate(self):
         s = _abi.LMSummary()
-        lib().oracle_iterate(self.h, C.byref(s))
+        self.L.oracle_iterate(self.h, C.byref(s))
         return s
 
     def values_data(self):
         out = np.zeros(self.ndata)
-        lib().oracle_get_values(self.h, dptr(out), self.ndata)
+        self.L.oracle_get_values(self.h, dptr(out), self.ndata)
         return out
 
     def set_values_data(self, data):
         data = np.ascontiguousarray(data, dtype=np.float64)
-        lib().oracle_set_values_data(self.h, dptr(data), data.shape[0])
+        self.L.oracle_set_values_data(self.h, dptr(data), data.shape[0])
 
     def trace(self):
         n = C.c_size_t()
-        lib().oracle_get_trace(self.h, None, 0, C.byref(n))
+        self.L.oracle_get_trace(self.h, None, 0, C.byref(n))
         arr = (_abi.TraceEntry * max(1, n.value))()
-        lib().oracle_get_trace(self.h, arr, n.value, C.byref(n))
+        self.L.oracle_get_trace(self.h, arr, n.value, C.byref(n))
         return _abi.trace_to_dicts(arr[: n.value])
 
     def linearize(self):
-        n = lib().oracle_linearize_size(self.h)
+        n = self.L.oracle_linearize_size(self.h)
         out = np.zeros(n)
-        lib().oracle_linearize(self.h, dptr(out), n)
+        self.L.oracle_linearize(self.h, dptr(out), n)
         return out
 
     def solve_damped(self, lam):
         n = int((np.where(self.values.kinds == _abi.POSE3, 6, 3)).sum())
         out = np.zeros(n)
-        ok = lib().oracle_solve_damped(self.h, lam, dptr(out), n)
+        ok = self.L.oracle_solve_damped(self.h, lam, dptr(out), n)
         return ok, out
 
     def solve_damped_ld(self, lam):
@@ -152,7 +155,7 @@ class Oracle:
         reference for ill-conditioned systems)"""
         n = int((np.where(self.values.kinds == _abi.POSE3, 6, 3)).sum())
         out = np.zeros(n)
-        ok = lib().oracle_solve_damped_ld(self.h, lam, dptr(out), n)
+        ok = self.L.oracle_solve_damped_ld(self.h, lam, dptr(out), n)
         return ok, out
 
 

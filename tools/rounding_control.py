@@ -3,7 +3,7 @@ oracle against itself with the Schur solve's sums reversed (the same
 mathematics, other rounding; oracle_set_reverse_sums), conditioned per LM
 iteration exactly as tests/test_gpu_parity.py conditions the GPU: before
 every iteration both copies are put on the same values and lambda.
-usage: python tools/r4_rounding_control.py [C2] [iters]"""
+usage: python tools/rounding_control.py [C2] [iters]"""
 import os
 import sys
 

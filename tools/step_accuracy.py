@@ -7,7 +7,7 @@ first lambda, the step of:
 against the step with the Schur solve in x87 extended precision
 (oracle_solve_damped_ld, eps 5.4e-20). Printed relative to the values'
 norm (the per-iteration parity metric) and to the reference step's norm.
-usage: python tools/r4_step_accuracy.py [C2] [iters] [--gpu]"""
+usage: python tools/step_accuracy.py [C2] [iters] [--gpu]"""
 import os
 import sys
 
