@@ -2479,10 +2479,11 @@ void launch_gather_reduced(const GatherDev& band, const int32_t* order, const in
   k_gather_reduced<<<nb, kBlock, 0, s>>>(r, arena, b, lambda);
 }
 
-// a 64-thread workgroup per separator tile: lane l owns row 64 s + l
+// a 64-thread workgroup per separator tile: lane l owns row 64 s + l; the
+// listed contributions are cleared, and subtracted from r when `apply`
 __global__ __launch_bounds__(64) void k_sep_rhs(const int32_t* __restrict__ tile, const int32_t* __restrict__ start,
                                                 const int32_t* __restrict__ slot, double* __restrict__ r,
-                                                double* __restrict__ contrib) {
+                                                double* __restrict__ contrib, int apply) {
   const int q = blockIdx.x, l = threadIdx.x;
   double acc = 0.0;
   for (int e = start[q]; e < start[q + 1]; ++e) {
@@ -2490,7 +2491,7 @@ __global__ __launch_bounds__(64) void k_sep_rhs(const int32_t* __restrict__ tile
     acc += *c;
     *c = 0.0;
   }
-  r[static_cast<int64_t>(tile[q]) * kTile + l] -= acc;
+  if (apply) r[static_cast<int64_t>(tile[q]) * kTile + l] -= acc;
 }
 
 // one workgroup per chunk: 16-byte copies, then the tail bytes
@@ -2510,8 +2511,8 @@ void launch_scatter_chunks(const char* data, const CopyChunk* chunks, int n_chun
 }
 
 void launch_sep_rhs(int n_sep_tiles, const int32_t* tile, const int32_t* start, const int32_t* slot, double* r,
-                    double* contrib, hipStream_t s) {
-  if (n_sep_tiles > 0) k_sep_rhs<<<n_sep_tiles, 64, 0, s>>>(tile, start, slot, r, contrib);
+                    double* contrib, int apply, hipStream_t s) {
+  if (n_sep_tiles > 0) k_sep_rhs<<<n_sep_tiles, 64, 0, s>>>(tile, start, slot, r, contrib, apply);
 }
 
 void launch_chain_factor(const ChainDev& c, double* arena, double lambda, int* fail, const ZeroDev& z,

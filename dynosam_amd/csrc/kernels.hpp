@@ -195,7 +195,7 @@ struct CopyChunk {
 void launch_scatter_chunks(const char* data, const CopyChunk* chunks, int n_chunks, hipStream_t s);
 
 void launch_sep_rhs(int n_sep_tiles, const int32_t* tile, const int32_t* start, const int32_t* slot, double* r,
-                    double* contrib, hipStream_t s);
+                    double* contrib, int apply, hipStream_t s);
 
 void launch_chain_factor(const ChainDev& c, double* arena, double lambda, int* fail, const ZeroDev& z,
                          hipStream_t s);

@@ -5,20 +5,23 @@
 // The reference solves the whole graph in one GTSAM process
 // (RGBDBackendModule.cc:207-231). Here the nested dissection of the reduced
 // pose system (tiles.cpp) is forced to split its top log2(nranks) levels, so
-// rank r owns one time-contiguous subtree of tiles (its interior) and the
-// separators above the subtrees belong to no rank. A factor that touches an
-// interior tile of r, and every factor of a landmark chain that does, is
-// linearised and Schur-eliminated on r only; the separators' dissection
-// guarantees no factor or chain touches two interiors. Factors touching only
-// separator tiles go to rank 0. Every rank holds all poses (the reduced
+// rank r owns one time-contiguous subtree of tiles (its interior) and each
+// separator of those splits is a node owned by the group of ranks whose
+// subtrees it splits. A factor that touches an interior tile of r, and every
+// factor of a landmark chain that does, is linearised and Schur-eliminated on
+// r only; the separators' dissection guarantees no factor or chain touches
+// two interiors. Factors touching only one separator's tiles go to the
+// leader (lowest rank) of its group. Every rank holds all poses (the reduced
 // system keeps global numbering) and only its own landmarks.
 //
 // Per LM solve each rank eliminates its landmarks and its interior columns
-// locally; the separator tiles and right-hand side rows then hold that rank's
-// partial Schur complement, which the ranks sum (one all-reduce), and every
-// rank factors the small separator system redundantly (solver.cpp).
+// locally; then, level by level from the deepest separators up, the ranks
+// sum the separator systems of that depth (one all-reduce per depth) and each
+// group factors its own separator (solver.cpp), the leader passing the
+// separator's contributions on to the separators above.
 #include <algorithm>
 #include <chrono>
+#include <climits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -48,12 +51,20 @@ dynohip_graph_view GraphStore::view() const {
 
 namespace {
 
-// owner merge: -1 = no interior seen yet; -2 = conflict
+// owner merge over the tiles a factor or chain touches: a rank (its
+// interior) wins over a separator node (one of the rank's ancestors: a
+// separator is adjacent only to the subtrees it splits); two ranks, or two
+// separator nodes, conflict
+constexpr int32_t kOwnNone = INT32_MIN, kOwnConflict = INT32_MIN + 1;
 int32_t merge_owner(int32_t a, int32_t b) {
-  if (a == -2 || b == -2) return -2;
-  if (a < 0) return b;
-  if (b < 0) return a;
-  return a == b ? a : -2;
+  if (a == kOwnNone) return b;
+  if (b == kOwnNone) return a;
+  if (a == kOwnConflict || b == kOwnConflict) return kOwnConflict;
+  if (a == b) return a;
+  if (a >= 0 && b >= 0) return kOwnConflict;
+  if (a >= 0) return a;
+  if (b >= 0) return b;
+  return kOwnConflict;
 }
 
 }  // namespace
@@ -81,7 +92,8 @@ int build_partitioned_plan(const dynohip_graph_view& g, const uint64_t* keys, co
   int rc = build_plan(g, keys, kind, n, G, err, nranks, rank, false, true);
   if (rc) return rc;
   std::vector<int32_t> towner;
-  if (!partition_tile_owners(G, nranks, towner)) {
+  std::vector<SepNode> nodes;
+  if (!partition_tile_owners(G, nranks, towner, nodes)) {
     err = "graph too short in time for " + std::to_string(nranks) + " partitions";
     return DYNOHIP_ESTRUCT;
   }
@@ -98,10 +110,12 @@ int build_partitioned_plan(const dynohip_graph_view& g, const uint64_t* keys, co
   part.nranks = nranks;
   part.rank = rank;
   auto pose_owner = [&](int32_t p) {
-    int32_t o = -1;
+    int32_t o = kOwnNone;
     for (int t = (6 * p) / kTile; t <= (6 * p + 5) / kTile; ++t) o = merge_owner(o, towner[t]);
     return o;
   };
+  // a separator node's factors and chains go to its group's leader
+  auto to_rank = [&](int32_t o) { return o >= 0 ? o : o == kOwnNone ? 0 : nodes[sep_node(o)].r0; };
   std::vector<int32_t> comp_of(G.n_pt);
   parallel_for(G.n_comp, [&](int64_t c0, int64_t c1) {
     for (int64_t c = c0; c < c1; ++c)
@@ -109,7 +123,7 @@ int build_partitioned_plan(const dynohip_graph_view& g, const uint64_t* keys, co
   });
   // pass 1: every factor's pose owner (on the workers), then landmark chains
   // take the union of their factors' pose owners
-  std::vector<int32_t> comp_own(G.n_comp, -1);
+  std::vector<int32_t> comp_own(G.n_comp, kOwnNone);
   std::vector<int32_t> fown[kNTypes];
   for (int t = 0; t < kNTypes; ++t) {
     const TypePlan& tp = G.types[t];
@@ -117,7 +131,7 @@ int build_partitioned_plan(const dynohip_graph_view& g, const uint64_t* keys, co
     fown[t].resize(tp.n);
     parallel_for(tp.n, [&](int64_t i0, int64_t i1) {
       for (int64_t i = i0; i < i1; ++i) {
-        int32_t o = -1;
+        int32_t o = kOwnNone;
         for (int sl = 0; sl < nk; ++sl)
           if (kSlotKind[t][sl] == 0) o = merge_owner(o, pose_owner(tp.idx[i * nk + sl]));
         fown[t][i] = o;
@@ -131,11 +145,11 @@ int build_partitioned_plan(const dynohip_graph_view& g, const uint64_t* keys, co
         }
   }
   for (int c = 0; c < G.n_comp; ++c) {
-    if (comp_own[c] == -2) {
+    if (comp_own[c] == kOwnConflict) {
       err = "internal: a landmark chain spans two partitions";
       return DYNOHIP_ESTRUCT;
     }
-    if (comp_own[c] < 0) comp_own[c] = 0;  // separator-only chains: rank 0
+    comp_own[c] = to_rank(comp_own[c]);   // separator-only chains: the node's leader
   }
   // pass 2: factor owners, the local graph in the global factor order (an
   // ordered filter on the workers: owners and counts per chunk, then each
@@ -156,8 +170,8 @@ int build_partitioned_plan(const dynohip_graph_view& g, const uint64_t* keys, co
         int32_t o = fown[t][i];
         for (int sl = 0; sl < nk; ++sl)
           if (kSlotKind[t][sl] == 1) o = merge_owner(o, comp_own[comp_of[tp.idx[i * nk + sl]]]);
-        if (o == -2) bad[w] = 1;
-        if (o < 0) o = 0;
+        if (o == kOwnConflict) bad[w] = 1;
+        o = to_rank(o);
         fown[t][i] = o;
         c += o == rank;
       }
@@ -189,12 +203,13 @@ int build_partitioned_plan(const dynohip_graph_view& g, const uint64_t* keys, co
       }
     });
   }
-  // values: every pose, this rank's landmarks
+  // values: every pose, this rank's landmarks. A value's owner is the rank
+  // that solves it and hands it back (a separator pose: its node's leader)
   part.value_owner.assign(n, -1);
   part.local_of.assign(n, -1);
   for (size_t v = 0; v < n; ++v) {
     const int32_t li = G.user_idx[v];
-    const int32_t o = kind[v] == DYNOHIP_POSE3 ? pose_owner(li) : comp_own[comp_of[li]];
+    const int32_t o = kind[v] == DYNOHIP_POSE3 ? to_rank(pose_owner(li)) : comp_own[comp_of[li]];
     part.value_owner[v] = o;
     if (kind[v] == DYNOHIP_POSE3 || o == rank) {
       part.local_of[v] = static_cast<int32_t>(part.keys.size());
@@ -245,25 +260,19 @@ int build_partitioned_plan(const dynohip_graph_view& g, const uint64_t* keys, co
   L.n_partials = G.n_partials;
   L.tile_flops = G.tile_flops;
   L.tile_owner = std::move(G.tile_owner);
-  L.ftask1 = std::move(G.ftask1);
-  L.flevel1 = std::move(G.flevel1);
-  L.fpanels1 = std::move(G.fpanels1);
-  L.fdep_start1 = std::move(G.fdep_start1);
-  L.fdep1 = std::move(G.fdep1);
-  L.fqueue1 = std::move(G.fqueue1);
-  L.sep_slot_ranges = std::move(G.sep_slot_ranges);
-  L.sep_tile_ranges = std::move(G.sep_tile_ranges);
+  L.sep_nodes = std::move(G.sep_nodes);
+  L.phases = std::move(G.phases);
+  L.rhs0_tile = std::move(G.rhs0_tile);
+  L.rhs0_start = std::move(G.rhs0_start);
+  L.rhs0_slot = std::move(G.rhs0_slot);
   L.band_D = std::move(G.band_D);
   L.max_D = G.max_D;
   compute_red_slots(L);
-  // damping: interior rows by their owner, separator rows by rank 0 (the
-  // ranks' diagonals are summed in the exchange)
+  // damping: interior rows by their owner, separator rows by the node's
+  // leader (the ranks' diagonals are summed in the exchange)
   mark("schedule into the local plan");
   part.damp_row.assign(static_cast<size_t>(L.n_red), 0);
-  for (int q = 0; q < L.n_red; ++q) {
-    const int32_t o = L.tile_owner[q / kTile];
-    part.damp_row[q] = (o == rank || (o < 0 && rank == 0)) ? 1 : 0;
-  }
+  for (int q = 0; q < L.n_red; ++q) part.damp_row[q] = to_rank(L.tile_owner[q / kTile]) == rank ? 1 : 0;
   return DYNOHIP_OK;
 }
 
@@ -316,16 +325,39 @@ extern "C" int dynohip_plan_export(const dynohip_graph_view* g, const uint64_t* 
   else if (nm == "fdep_start") vec(P.fdep_start);
   else if (nm == "fdep") vec(P.fdep);
   else if (nm == "fqueue") vec(P.fqueue);
-  else if (nm == "fdep_start1") vec(P.fdep_start1);
-  else if (nm == "fdep1") vec(P.fdep1);
-  else if (nm == "fqueue1") vec(P.fqueue1);
-  else if (nm == "ftask1") raw(P.ftask1.data(), P.ftask1.size() * sizeof(TileTask));
-  else if (nm == "flevel1") vec(P.flevel1);
+  else if (nm == "sep_nodes") raw(P.sep_nodes.data(), P.sep_nodes.size() * sizeof(SepNode));
+  // phase p of the separator phases (deepest first): "phase<p>_<field>", and
+  // "phases": per phase (node, leader)
+  else if (nm == "phases") {
+    for (const PartPhase& F : P.phases) {
+      tmp.push_back(F.node);
+      tmp.push_back(F.leader);
+    }
+    vec(tmp);
+  } else if (nm.size() > 7 && nm.compare(0, 5, "phase") == 0 && nm.find('_') != std::string::npos) {
+    const size_t us = nm.find('_');
+    const int ph = std::atoi(nm.substr(5, us - 5).c_str());
+    if (ph < 0 || ph >= static_cast<int>(P.phases.size())) return DYNOHIP_EINVAL;
+    const PartPhase& F = P.phases[ph];
+    const std::string f = nm.substr(us + 1);
+    if (f == "ftask") raw(F.ftask.data(), F.ftask.size() * sizeof(TileTask));
+    else if (f == "flevel") vec(F.flevel);
+    else if (f == "fdep_start") vec(F.fdep_start);
+    else if (f == "fdep") vec(F.fdep);
+    else if (f == "fqueue") vec(F.fqueue);
+    else if (f == "xslot") vec(F.xslot);
+    else if (f == "xtile") vec(F.xtile);
+    else if (f == "rhs_tile") vec(F.rhs_tile);
+    else if (f == "rhs_start") vec(F.rhs_start);
+    else if (f == "rhs_slot") vec(F.rhs_slot);
+    else return DYNOHIP_EINVAL;
+  }
+  else if (nm == "rhs0_tile") vec(P.rhs0_tile);
+  else if (nm == "rhs0_start") vec(P.rhs0_start);
+  else if (nm == "rhs0_slot") vec(P.rhs0_slot);
   else if (nm == "bpart") raw(P.bpart.data(), P.bpart.size() * sizeof(BackPart));
   else if (nm == "bplevel") vec(P.bplevel);
   else if (nm == "bent") vec(P.bent);
-  else if (nm == "sep_slot_ranges") vec(P.sep_slot_ranges);
-  else if (nm == "sep_tile_ranges") vec(P.sep_tile_ranges);
   else if (nm == "red_a") vec(P.red_A);
   else if (nm == "red_order") vec(P.red_order);
   else if (nm.size() > 6 && nm.compare(nm.size() - 6, 6, "_start") == 0) {  // gather lists, e.g. "gRed_start"
@@ -400,8 +432,13 @@ extern "C" int dynohip_plan_export(const dynohip_graph_view* g, const uint64_t* 
     v(P.band_D); v(P.tile_pos); v(P.row_start); v(P.row_col); v(P.row_slot);
     v(P.ftask); v(P.pairs); v(P.flevel); v(P.fpanels); v(P.fdep_start); v(P.fdep); v(P.fqueue);
     v(P.btask); v(P.blevel); v(P.bent); v(P.bpart); v(P.bplevel);
-    v(P.tile_owner); v(P.ftask1); v(P.flevel1); v(P.fpanels1); v(P.fdep_start1); v(P.fdep1); v(P.fqueue1);
-    v(P.sep_slot_ranges); v(P.sep_tile_ranges);
+    v(P.tile_owner); v(P.sep_nodes); v(P.rhs0_tile); v(P.rhs0_start); v(P.rhs0_slot);
+    for (const PartPhase& F : P.phases) {
+      const int32_t hd[] = {F.node, F.leader};
+      fnv(hd, sizeof(hd));
+      v(F.xslot); v(F.xtile); v(F.ftask); v(F.flevel); v(F.fpanels); v(F.fdep_start); v(F.fdep); v(F.fqueue);
+      v(F.rhs_tile); v(F.rhs_start); v(F.rhs_slot);
+    }
     v(part.value_owner); v(part.damp_row);
     vec(tmp);
   }

@@ -236,9 +236,8 @@ void plan_recycle(Plan& P) {
   k(f.row_slot, P.row_slot); k(f.ftask, P.ftask); k(f.pairs, P.pairs); k(f.flevel, P.flevel);
   k(f.fpanels, P.fpanels); k(f.fdep_start, P.fdep_start); k(f.fdep, P.fdep); k(f.fqueue, P.fqueue);
   k(f.btask, P.btask); k(f.blevel, P.blevel); k(f.bent, P.bent); k(f.bpart, P.bpart); k(f.bplevel, P.bplevel);
-  k(f.tile_owner, P.tile_owner); k(f.ftask1, P.ftask1); k(f.flevel1, P.flevel1); k(f.fpanels1, P.fpanels1);
-  k(f.fdep_start1, P.fdep_start1); k(f.fdep1, P.fdep1); k(f.fqueue1, P.fqueue1);
-  k(f.sep_slot_ranges, P.sep_slot_ranges); k(f.sep_tile_ranges, P.sep_tile_ranges);
+  k(f.tile_owner, P.tile_owner); k(f.sep_nodes, P.sep_nodes); k(f.phases, P.phases);
+  k(f.rhs0_tile, P.rhs0_tile); k(f.rhs0_start, P.rhs0_start); k(f.rhs0_slot, P.rhs0_slot);
   f.scratch = std::move(P.scratch);   // contents are refilled by build_plan
   P = std::move(f);
 }

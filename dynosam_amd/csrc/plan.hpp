@@ -162,6 +162,35 @@ struct TypePlan {
   std::vector<double, default_init_allocator<double>> hk;      // n (Huber k, <= 0 Gaussian)
 };
 
+// Partitioned solve: a separator of the top dissection levels (tiles.cpp
+// nd_order_part). The ranks [r0, r0 + nr) of the subtree it splits factor it
+// after the exchange of its depth (1: the top separator); r0 leads the group
+// (it alone passes the node's contributions on to the separators above).
+// Tiles [t0, t1) in natural order.
+struct SepNode {
+  int32_t r0, nr, depth, t0, t1;
+};
+// tile / task owner of a separator node's columns (ranks are >= 0)
+constexpr int32_t sep_code(int32_t node) { return -1 - node; }
+constexpr int32_t sep_node(int32_t code) { return -1 - code; }
+
+// One phase of a rank's partitioned solve after its interior (phase 0): the
+// exchange of one depth's separator systems, then the tasks of this rank's
+// separator node of that depth.
+struct PartPhase {
+  int32_t node = 0;                     // the node whose columns this phase factors
+  int32_t leader = 0;                   // 1: this rank leads the node's group
+  // summed over all ranks before the phase: [beg, end) slot ranges of every
+  // node of this depth, and their right-hand-side tile ranges (natural order)
+  std::vector<int32_t> xslot, xtile;
+  std::vector<TileTask> ftask;          // the node's tasks on this rank (dataflow form as Plan::ftask)
+  std::vector<int32_t> flevel, fpanels, fdep_start, fdep, fqueue;
+  // after the phase: the node's column contributions L(s,c) y_c to rows s of
+  // separators above it leave the RHS (leader: r_s -= them; every member:
+  // the contribution is cleared), k_sep_rhs's lists
+  std::vector<int32_t> rhs_tile, rhs_start, rhs_slot;
+};
+
 struct Plan {
   // variables
   int n_pose = 0, n_pt = 0;
@@ -246,15 +275,16 @@ struct Plan {
   int32_t n_partials = 0;
   double tile_flops = 0.0;              // tile-level factorisation flops (incl. fill)
   // partitioned full-batch solve. nranks > 1: the
-  // lists above hold this rank's phase-0 tasks and its backward parts
-  // (separator columns first); the *1 lists the separator tasks run after
-  // the exchange
+  // lists above hold this rank's phase-0 tasks (its interior) and its
+  // backward parts (its separator nodes' columns first, then its interior);
+  // `phases` the separator phases, deepest node first, the top one last
   int nranks = 1, rank = 0;
-  std::vector<int32_t> tile_owner;      // per tile: owning rank, -1 = top separator
-  std::vector<TileTask> ftask1;
-  std::vector<int32_t> flevel1, fpanels1, fdep_start1, fdep1, fqueue1;
-  std::vector<int32_t> sep_slot_ranges; // [beg, end) slot ranges of the separator columns
-  std::vector<int32_t> sep_tile_ranges; // [beg, end) tile ranges (natural order) of the separators
+  std::vector<int32_t> tile_owner;      // per tile: owning rank, or sep_code(node)
+  std::vector<SepNode> sep_nodes;
+  std::vector<PartPhase> phases;
+  // phase 0's right-hand-side move (k_sep_rhs): this rank's interior column
+  // contributions to separator rows
+  std::vector<int32_t> rhs0_tile, rhs0_start, rhs0_slot;
   // build_plan's largest temporaries, kept with the plan (not plan content):
   // a re-plan of a similar graph refills memory that is already mapped
   // instead of page-faulting fresh allocations (C2 ~7 MB, NS ~25 MB)
@@ -283,11 +313,12 @@ void plan_recycle(Plan& P);
 // of the planner pool (the schedule then runs beside the gather builds).
 bool build_tile_schedule(Plan& P, bool own_threads = false);
 
-// The tile owners of the partitioned schedule (per natural tile: rank, -1 =
-// top separator) from the pose-pair structure alone: the top splits of the
-// dissection do not depend on the leaf size, so this equals the schedule's
-// tile_owner. False when the graph is too short in time for nranks.
-bool partition_tile_owners(const Plan& P, int nranks, std::vector<int32_t>& owner);
+// The tile owners of the partitioned schedule (per natural tile: rank, or
+// sep_code(node)) and the separator nodes, from the pose-pair structure
+// alone: the top splits of the dissection do not depend on the leaf size, so
+// this equals the schedule's tile_owner. False when the graph is too short in
+// time for nranks.
+bool partition_tile_owners(const Plan& P, int nranks, std::vector<int32_t>& owner, std::vector<SepNode>& nodes);
 
 // Plan::red_slot from the tile structure (after the tile schedule).
 void compute_red_slots(Plan& P);
@@ -314,7 +345,7 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
 // Partitioned full-batch solve: what one rank holds (partition.cpp).
 struct Partition {
   int nranks = 1, rank = 0;
-  std::vector<int32_t> value_owner;     // per global value: owning rank, -1 = replicated (separator pose)
+  std::vector<int32_t> value_owner;     // per global value: owning rank; a pose of a separator: sep_code(node)
   std::vector<int32_t> local_of;        // per global value: index in the local value list, -1 = not held
   std::vector<uint64_t> keys;           // local value list (all poses + this rank's points)
   std::vector<uint8_t> kind;

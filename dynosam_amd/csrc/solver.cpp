@@ -19,6 +19,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <memory>
 #include <vector>
 
 #include "../../include/dynohip.h"
@@ -502,11 +503,19 @@ struct dynohip_solver {
   GraphStore local_graph;
   std::vector<uint8_t> value_kind;   // global value kinds
   DevBuf<uint8_t> damp;
-  DevBuf<TileTask> ftask1;
-  DevBuf<int32_t> fdep_start1, fdep1, fqueue1, seprhs_tile, seprhs_start, seprhs_slot;
-  DevBuf<double> xbuf;
-  TileSchedDev sd1;
+  // phase 0's right-hand-side move, and per separator phase (Plan::phases,
+  // deepest node first) its tasks and right-hand-side move
+  DevBuf<int32_t> seprhs_tile, seprhs_start, seprhs_slot;
   int n_seprhs = 0;
+  struct PhaseDev {
+    DevBuf<TileTask> ftask;
+    DevBuf<int32_t> fdep_start, fdep, fqueue, rhs_tile, rhs_start, rhs_slot;
+    TileSchedDev sd;
+    int n_rhs = 0;
+  };
+  std::vector<std::unique_ptr<PhaseDev>> phd;
+  DevBuf<double> xbuf;   // exchange buffer (the largest phase's)
+  int64_t xtotal = 0;    // doubles exchanged per linear solve (every phase)
 };
 
 namespace {
@@ -726,36 +735,39 @@ int upload_partition(dynohip_solver* s) {
   Plan& P = s->plan;
   hipStream_t st = s->stream;
   HIPCHK(s, s->damp.upload(s->part.damp_row, st));
-  HIPCHK(s, s->ftask1.upload(P.ftask1, st));
-  HIPCHK(s, s->fdep_start1.upload(P.fdep_start1, st));
-  HIPCHK(s, s->fdep1.upload(P.fdep1, st));
-  HIPCHK(s, s->fqueue1.upload(P.fqueue1, st));
-  s->sd1 = s->sd;
-  s->sd1.ftask = s->ftask1.p;
-  s->sd1.fdep_start = s->fdep_start1.p;
-  s->sd1.fdep = s->fdep1.p;
-  s->sd1.forder = s->fqueue1.p;
-  // separator right-hand-side rows: this rank's interior contributions
-  std::vector<int32_t> tl, ts(1, 0), sl;
-  for (size_t r = 0; r + 1 < P.sep_tile_ranges.size(); r += 2)
-    for (int32_t t = P.sep_tile_ranges[r]; t < P.sep_tile_ranges[r + 1]; ++t) {
-      tl.push_back(t);
-      for (int32_t e = P.row_start[t]; e < P.row_start[t + 1]; ++e)
-        if (P.tile_owner[P.row_col[e]] == s->rank) sl.push_back(P.row_slot[e]);
-      ts.push_back(static_cast<int32_t>(sl.size()));
-    }
-  s->n_seprhs = static_cast<int>(tl.size());
-  HIPCHK(s, s->seprhs_tile.upload(tl, st));
-  HIPCHK(s, s->seprhs_start.upload(ts, st));
-  HIPCHK(s, s->seprhs_slot.upload(sl, st));
+  s->n_seprhs = static_cast<int>(P.rhs0_tile.size());
+  HIPCHK(s, s->seprhs_tile.upload(P.rhs0_tile, st));
+  HIPCHK(s, s->seprhs_start.upload(P.rhs0_start, st));
+  HIPCHK(s, s->seprhs_slot.upload(P.rhs0_slot, st));
+  while (s->phd.size() < P.phases.size()) s->phd.push_back(std::make_unique<dynohip_solver::PhaseDev>());
+  s->xtotal = 0;
   size_t nx = 0;
-  for (size_t r = 0; r + 1 < P.sep_slot_ranges.size(); r += 2)
-    nx += static_cast<size_t>(P.sep_slot_ranges[r + 1] - P.sep_slot_ranges[r]) * kTile * kTile;
-  for (size_t r = 0; r + 1 < P.sep_tile_ranges.size(); r += 2)
-    nx += static_cast<size_t>(P.sep_tile_ranges[r + 1] - P.sep_tile_ranges[r]) * kTile;
+  for (size_t ph = 0; ph < P.phases.size(); ++ph) {
+    const PartPhase& F = P.phases[ph];
+    dynohip_solver::PhaseDev& D = *s->phd[ph];
+    HIPCHK(s, D.ftask.upload(F.ftask, st));
+    HIPCHK(s, D.fdep_start.upload(F.fdep_start, st));
+    HIPCHK(s, D.fdep.upload(F.fdep, st));
+    HIPCHK(s, D.fqueue.upload(F.fqueue, st));
+    HIPCHK(s, D.rhs_tile.upload(F.rhs_tile, st));
+    HIPCHK(s, D.rhs_start.upload(F.rhs_start, st));
+    HIPCHK(s, D.rhs_slot.upload(F.rhs_slot, st));
+    D.n_rhs = static_cast<int>(F.rhs_tile.size());
+    D.sd = s->sd;
+    D.sd.ftask = D.ftask.p;
+    D.sd.fdep_start = D.fdep_start.p;
+    D.sd.fdep = D.fdep.p;
+    D.sd.forder = D.fqueue.p;
+    size_t n = 0;
+    for (size_t r = 0; r + 1 < F.xslot.size(); r += 2)
+      n += static_cast<size_t>(F.xslot[r + 1] - F.xslot[r]) * kTile * kTile;
+    for (size_t r = 0; r + 1 < F.xtile.size(); r += 2) n += static_cast<size_t>(F.xtile[r + 1] - F.xtile[r]) * kTile;
+    nx = std::max(nx, n);
+    s->xtotal += static_cast<int64_t>(n);
+  }
   HIPCHK(s, s->xbuf.alloc(nx));
-  // rows and contributions of other ranks' interiors are never written
-  // here: keep them zero (their poses then retract by zero)
+  // rows and contributions of other ranks' interiors and separators are
+  // never written here: keep them zero (their poses then retract by zero)
   HIPCHK(s, hipMemsetAsync(s->contrib.p, 0, s->contrib.n * sizeof(double), st));
   HIPCHK(s, hipMemsetAsync(s->xy.p, 0, s->xy.n * sizeof(double), st));
   HIPCHK(s, hipStreamSynchronize(st));
@@ -770,9 +782,10 @@ int comm_sum(dynohip_solver* s, double* buf, size_t n, int on_device) {
   return 0;
 }
 
-// copies the separator tiles and RHS rows into / out of the exchange buffer
-int sep_copy(dynohip_solver* s, bool pack) {
-  Plan& P = s->plan;
+// copies one depth's separator tiles and RHS rows (phase ph's exchange)
+// into / out of the exchange buffer
+int sep_copy(dynohip_solver* s, size_t ph, bool pack, size_t* n_out = nullptr) {
+  const PartPhase& F = s->plan.phases[ph];
   size_t o = 0;
   auto cp = [&](double* dev, size_t cnt) -> int {
     double* a = pack ? s->xbuf.p + o : dev;
@@ -781,14 +794,15 @@ int sep_copy(dynohip_solver* s, bool pack) {
     o += cnt;
     return 0;
   };
-  for (size_t r = 0; r + 1 < P.sep_slot_ranges.size(); r += 2)
-    if (cp(s->slots.p + static_cast<size_t>(P.sep_slot_ranges[r]) * kTile * kTile,
-           static_cast<size_t>(P.sep_slot_ranges[r + 1] - P.sep_slot_ranges[r]) * kTile * kTile))
+  for (size_t r = 0; r + 1 < F.xslot.size(); r += 2)
+    if (cp(s->slots.p + static_cast<size_t>(F.xslot[r]) * kTile * kTile,
+           static_cast<size_t>(F.xslot[r + 1] - F.xslot[r]) * kTile * kTile))
       return DYNOHIP_EHIP;
-  for (size_t r = 0; r + 1 < P.sep_tile_ranges.size(); r += 2)
-    if (cp(s->gred.p + static_cast<size_t>(P.sep_tile_ranges[r]) * kTile,
-           static_cast<size_t>(P.sep_tile_ranges[r + 1] - P.sep_tile_ranges[r]) * kTile))
+  for (size_t r = 0; r + 1 < F.xtile.size(); r += 2)
+    if (cp(s->gred.p + static_cast<size_t>(F.xtile[r]) * kTile,
+           static_cast<size_t>(F.xtile[r + 1] - F.xtile[r]) * kTile))
       return DYNOHIP_EHIP;
+  if (n_out) *n_out = o;
   return 0;
 }
 
@@ -891,21 +905,28 @@ int enqueue_try(dynohip_solver* s, double lambda) {
     // its interior contributions leave the separator RHS rows
     launch_tile_forward(s->bd, s->sd, P.flevel, P.fpanels, s->linv.p, s->gred.p, s->contrib.p, y, s->failp, st,
                         s->side, s->ev_main, s->ev_side);
-    launch_sep_rhs(s->n_seprhs, s->seprhs_tile.p, s->seprhs_start.p, s->seprhs_slot.p, s->gred.p, s->contrib.p, st);
-    // exchange: the separator system summed over ranks, ordered on the
-    // solver's stream by the callback (no host synchronisation here)
-    if (sep_copy(s, true)) return DYNOHIP_EHIP;
-    int rc = comm_sum(s, s->xbuf.p, s->xbuf.n, 1);
-    if (rc) return rc;
-    if (sep_copy(s, false)) return DYNOHIP_EHIP;
-    HIPCHK(s, hipMemsetAsync(s->fsync.p, 0, s->fsync.n * sizeof(unsigned), st));
-    // phase 1 (every rank, identical inputs): the separator columns, then
-    // the backward substitution of the separators and this rank's interior
-    s->sd1.epoch = s->sd.epoch;
-    launch_tile_forward(s->bd, s->sd1, P.flevel1, P.fpanels1, s->linv.p, s->gred.p, s->contrib.p, y, s->failp, st,
-                        s->side, s->ev_main, s->ev_side);
-    // (ms_cholesky of a partitioned handle spans both forward phases and the
-    // exchange between them)
+    launch_sep_rhs(s->n_seprhs, s->seprhs_tile.p, s->seprhs_start.p, s->seprhs_slot.p, s->gred.p, s->contrib.p, 1, st);
+    // then this rank's separator nodes, deepest first: the exchange of the
+    // node's depth (its separator systems summed over ranks, ordered on the
+    // solver's stream by the callback: no host synchronisation here), the
+    // node's tasks on its group, its contributions to the separators above
+    // into their RHS rows (leader) or dropped (the group's other ranks)
+    for (size_t ph = 0; ph < P.phases.size(); ++ph) {
+      size_t nxd = 0;
+      if (sep_copy(s, ph, true, &nxd)) return DYNOHIP_EHIP;
+      int rc = comm_sum(s, s->xbuf.p, nxd, 1);
+      if (rc) return rc;
+      if (sep_copy(s, ph, false)) return DYNOHIP_EHIP;
+      HIPCHK(s, hipMemsetAsync(s->fsync.p, 0, s->fsync.n * sizeof(unsigned), st));
+      dynohip_solver::PhaseDev& D = *s->phd[ph];
+      D.sd.epoch = s->sd.epoch;
+      launch_tile_forward(s->bd, D.sd, P.phases[ph].flevel, P.phases[ph].fpanels, s->linv.p, s->gred.p, s->contrib.p,
+                          y, s->failp, st, s->side, s->ev_main, s->ev_side);
+      launch_sep_rhs(D.n_rhs, D.rhs_tile.p, D.rhs_start.p, D.rhs_slot.p, s->gred.p, s->contrib.p, P.phases[ph].leader,
+                     st);
+    }
+    // (ms_cholesky of a partitioned handle spans every forward phase and the
+    // exchanges between them)
     if (timed) (void)hipEventRecord(s->ev[5], st);
     launch_tile_backward(s->bd, s->sd, P.bplevel, s->linv.p, y, x, s->failp, st, s->sd.back_poll);
   } else if (s->small_solve && P.NT >= 1 && P.NT <= kSmallNT) {
@@ -1718,7 +1739,7 @@ int dynohip_value_owner(dynohip_solver* s, int32_t* owner_out, size_t n, int64_t
   if (rc) return rc;
   if (n != s->value_kind.size() || (n && !owner_out)) return set_err(s, DYNOHIP_EINVAL, "owner buffer size");
   for (size_t i = 0; i < n; ++i) owner_out[i] = s->nranks > 1 ? s->part.value_owner[i] : 0;
-  if (exchange_doubles) *exchange_doubles = s->nranks > 1 ? static_cast<int64_t>(s->xbuf.n) : 0;
+  if (exchange_doubles) *exchange_doubles = s->nranks > 1 ? s->xtotal : 0;
   return DYNOHIP_OK;
 }
 

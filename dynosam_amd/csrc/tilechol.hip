@@ -23,6 +23,7 @@
 #include <type_traits>
 
 #include "kernels.hpp"
+#include "f16wave.h"
 
 namespace dynohip {
 
@@ -31,7 +32,6 @@ namespace {
 constexpr int T = kTile;
 constexpr int LD = T + 4;            // padded LDS row stride (doubles)
 
-typedef double v4d __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void load_tile_lds(const double* __restrict__ src, double* dst, int tid, int nthreads) {
   const double2* s2 = reinterpret_cast<const double2*>(src);
@@ -78,14 +78,6 @@ __device__ __forceinline__ void mfma_abt(const double* As, const double* Bs, int
 #define MFMA_ROW(wave, lane, ti, r) (32 * ((wave) >> 1) + 16 * (ti) + ((lane) >> 4) + 4 * (r))
 #define MFMA_COL(wave, lane, tj) (32 * ((wave) & 1) + 16 * (tj) + ((lane) & 15))
 
-// 1/sqrt(x): hardware estimate + two Newton steps (full FP64 accuracy)
-__device__ __forceinline__ double rsqrt_nr(double x) {
-  double y = __builtin_amdgcn_rsq(x);
-  y = y * (1.5 - 0.5 * x * y * y);
-  y = y * (1.5 - 0.5 * x * y * y);
-  return y;
-}
-
 #ifdef DYNOHIP_TASK_CLOCK
 // per-task timestamps of the last k_factor_persist launch (s_memrealtime,
 // 100 MHz): dequeue, dependencies met, factor start, factor end, done; and
@@ -110,15 +102,6 @@ __device__ unsigned long long g_tclk[32][32768];
 #endif
 __device__ __forceinline__ unsigned long long rtc() { return __builtin_amdgcn_s_memrealtime(); }
 
-// 1/x: hardware estimate + two Newton steps (full FP64 accuracy); four
-// dependent FMAs, half the chain of the reciprocal square root
-__device__ __forceinline__ double rcp_nr(double x) {
-  double y = __builtin_amdgcn_rcp(x);
-  y = __builtin_fma(__builtin_fma(-x, y, 1.0), y, y);
-  y = __builtin_fma(__builtin_fma(-x, y, 1.0), y, y);
-  return y;
-}
-
 __device__ __forceinline__ double* slot_ptr(const TileDev& b, int32_t slot) {
   return b.slots + static_cast<int64_t>(slot) * T * T;
 }
@@ -128,92 +111,6 @@ __device__ __forceinline__ double* slot_ptr(const TileDev& b, int32_t slot) {
 // (16w + (l>>4) + 4r, 16TJ + (l&15)).
 #define ACC_ROW(w, l, r) (16 * (w) + ((l) >> 4) + 4 * (r))
 #define ACC_COL(TJ, l) (16 * (TJ) + ((l) & 15))
-
-// ---- 16x16 in-wave factorisation (no barriers) --------------------------
-// A 16x16 block in MFMA accumulator layout: lane l, register r holds
-// element (row (l>>4) + 4r, column l&15). The same registers serve as the
-// B operand of v_mfma_f64_16x16x4 for K-slice r, and as the A operand of
-// the block's transpose.
-
-__device__ __forceinline__ double bcast_row_lane(double v, int p) {
-  // lane p of every 16-lane row -> the whole row (DPP row_newbcast)
-  switch (p) {
-// (every source lane exists, so no "old" value is needed: one v_mov_b64_dpp
-// instead of a copy plus an in-place DPP move)
-#define NB(q) case q: return __builtin_amdgcn_update_dpp(__builtin_nan(""), v, 0x150 + q, 0xf, 0xf, true);
-    NB(0) NB(1) NB(2) NB(3) NB(4) NB(5) NB(6) NB(7) NB(8) NB(9) NB(10) NB(11) NB(12) NB(13) NB(14) NB(15)
-#undef NB
-  }
-  return v;
-}
-
-// row group G (lanes 16G..16G+15) of v broadcast to all four row groups with
-// the gfx950 lane swaps: permlane32_swap(v, v) gives [r0 r1 r0 r1] and
-// [r2 r3 r2 r3], permlane16_swap of one of them with itself gives its two
-// rows each broadcast. Four VALU swaps, no LDS round trip (ds_bpermute).
-__device__ __forceinline__ unsigned row_bcast32(unsigned v, int G) {
-  const auto a = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-  const unsigned s = G < 2 ? a[0] : a[1];
-  const auto b = __builtin_amdgcn_permlane16_swap(s, s, false, false);
-  return (G & 1) ? b[1] : b[0];
-}
-__device__ __forceinline__ double row_bcast(double v, int G) {
-  const unsigned lo = row_bcast32(static_cast<unsigned>(__double2loint(v)), G);
-  const unsigned hi = row_bcast32(static_cast<unsigned>(__double2hiint(v)), G);
-  return __hiloint2double(static_cast<int>(hi), static_cast<int>(lo));
-}
-
-__device__ __forceinline__ double pull_lane(double v, int src) {
-  const int a = src << 2;
-  const int lo = __builtin_amdgcn_ds_bpermute(a, __double2loint(v));
-  const int hi = __builtin_amdgcn_ds_bpermute(a, __double2hiint(v));
-  return __hiloint2double(hi, lo);
-}
-
-__device__ __forceinline__ double read_lane(double v, int lane) {
-  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
-  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
-  return __hiloint2double(hi, lo);
-}
-
-// B (symmetric, full) = U^T U; on return W = U^-1 (upper) and B is
-// scratch. Right-looking by rows: pivot p's row is pulled across row
-// groups (ds_bpermute), its column broadcast within them (DPP). Entries
-// of B in rows or columns <= p are never read after pivot p, so the
-// trailing update runs unmasked on the registers that still hold rows > p.
-// W is updated unscaled (W~[c][i] -= W~[c][p] U[p][i] / U[p][p]) and each
-// column is scaled by its 1/U[j][j] once at the end.
-// dscr: 16 doubles of LDS scratch for the pivots. The column masks come from
-// a per-lane counter made opaque every pivot, so the compiler cannot hoist
-// sixteen of them into (spilled) scalar registers.
-__device__ __forceinline__ void factor16_wave(v4d& B, v4d& W, int l, bool& ok, double* dscr) {
-  const int j = l & 15;
-  int jd = j;   // j - p at pivot p
-#pragma unroll
-  for (int p = 0; p < 16; ++p) {
-    const int rp = p >> 2, gp = p & 3;
-    const double d = read_lane(B[rp], 16 * gp + p);
-    const double rowp = row_bcast(B[rp], gp);           // B[p][j]
-    const double f = rowp * rcp_nr(d);                   // U[p][j] / U[p][p]
-    asm volatile("" : "+v"(jd));
-    const double fm = jd > 0 ? f : 0.0;
-    jd -= 1;
-    dscr[p] = d;   // every lane, same value
-
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (4 * r + 3 > p) B[r] -= bcast_row_lane(B[r], p) * f;     // rows g+4r > p
-      if (4 * r <= p) W[r] -= bcast_row_lane(W[r], p) * fm;      // W~[c][p] != 0 only for c <= p
-    }
-  }
-  asm volatile("" ::: "memory");   // read back through LDS, not a 16-way select
-  const double dj = dscr[j];   // this lane's column scale 1/U[j][j] = 1/sqrt(d_j)
-  const double myrs = rsqrt_nr(dj);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) W[r] *= myrs;
-  // every pivot positive and finite (NaN fails both tests), checked once
-  ok = ok && __all((dj > 0.0) && (dj < 1e300));
-}
 
 // acc (+)= Y^T Z for 16x16 blocks Y, Z in accumulator layout (K = 16)
 __device__ __forceinline__ v4d mfma_tn(const v4d& Y, const v4d& Z, v4d acc, bool neg) {
@@ -272,7 +169,7 @@ __device__ bool factor_tile_blk_w(v4d (&accA)[4], v4d (&accX)[4], int l, double*
 #pragma unroll
       for (int r = 0; r < 4; ++r) Wmine[r] = ((l >> 4) + 4 * r == (l & 15)) ? 1.0 : 0.0;
       TCLKW(16 + 4 * KB, q);
-      factor16_wave(accA[KB], Wmine, l, ok, dscr);
+      factor16(accA[KB], Wmine, l, ok, dscr);
       TCLKW(17 + 4 * KB, q);
 #pragma unroll
       for (int TJ = KB + 1; TJ < 4; ++TJ) {
@@ -723,7 +620,7 @@ __device__ bool factor_own_w(v4d (&accA)[4], v4d (&XT)[4], int l, TaskLds& S, Di
 #pragma unroll
       for (int r = 0; r < 4; ++r) Wm[r] = (g + 4 * r == li) ? 1.0 : 0.0;
       TCLKW(16 + 4 * KB, q);
-      factor16_wave(accA[KB], Wm, l, ok, &S.rpart[w][0]);
+      factor16(accA[KB], Wm, l, ok, &S.rpart[w][0]);
       TCLKW(17 + 4 * KB, q);
       st_blk(Ublk(KB, KB), Wm, l);
 #pragma unroll
@@ -1561,7 +1458,7 @@ __global__ __launch_bounds__(kSmallWaves * 64) void k_small_solve(TileDev b, con
     v4d Wm;
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) Wm[rr] = (g + 4 * rr == li) ? 1.0 : 0.0;
-    factor16_wave(Dg[d], Wm, l, ok, &dscr[w][0]);
+    factor16(Dg[d], Wm, l, ok, &dscr[w][0]);
     st_blk(&Ws[K][0], Wm, l);
     const v4d Y = mfma_tn(Wm, Rg[d], zero, false);
     st_blk(&Ur[buf][kSmallNB][0], Y, l);

@@ -48,8 +48,9 @@ struct Sched {
   int leaf = 0;
   std::vector<int32_t> order;               // tile at position p
   std::vector<int32_t> pos;                 // position of tile t
-  std::vector<int32_t> owner;               // per position: rank subtree, -1 = top separator (partitioned)
-  std::vector<int32_t> task_owner;          // per forward task: rank that runs it, -1 = after the exchange
+  std::vector<int32_t> owner;               // per position: rank subtree, or sep_code(node) (partitioned)
+  std::vector<int32_t> task_owner;          // per forward task: its rank, or the separator node it belongs to
+  std::vector<SepNode> nodes;               // partitioned: the separator nodes of the top splits
   bool ok = true;                           // partitioned: every top split succeeded
   std::vector<std::vector<int32_t>> st;     // per column position: row positions (sorted, incl. itself)
   std::vector<int32_t> slot_base;           // per column position
@@ -150,8 +151,13 @@ bool part_split(int lo, int hi, const std::vector<int32_t>& maxnb, int nr, bool 
   return true;
 }
 
+// A split's separator is a node of the partition tree: the ranks [r0, r0 +
+// nr) of the subtree it splits factor it (after the exchange of its depth),
+// depth 1 the top one. Its tiles get owner sep_code(node); nodes are numbered
+// in creation order (children first).
 bool nd_order_part_b(int lo, int hi, int leaf, const std::vector<int32_t>& maxnb, int nr, int r0,
-                     std::vector<int32_t>& out, std::vector<int32_t>& owner, bool balanced) {
+                     std::vector<int32_t>& out, std::vector<int32_t>& owner, bool balanced,
+                     std::vector<SepNode>& nodes, int depth) {
   if (nr == 1) {
     nd_order(lo, hi, leaf, maxnb, out);
     owner.resize(out.size(), r0);
@@ -160,28 +166,32 @@ bool nd_order_part_b(int lo, int hi, int leaf, const std::vector<int32_t>& maxnb
   int m = 0, s_end = 0;
   if (!part_split(lo, hi, maxnb, nr, balanced, m, s_end)) return false;
   const int nl = nr / 2;
-  const size_t o0 = out.size();
-  if (!nd_order_part_b(lo, m, leaf, maxnb, nl, r0, out, owner, balanced) ||
-      !nd_order_part_b(s_end, hi, leaf, maxnb, nr - nl, r0 + nl, out, owner, balanced)) {
+  const size_t o0 = out.size(), n0 = nodes.size();
+  if (!nd_order_part_b(lo, m, leaf, maxnb, nl, r0, out, owner, balanced, nodes, depth + 1) ||
+      !nd_order_part_b(s_end, hi, leaf, maxnb, nr - nl, r0 + nl, out, owner, balanced, nodes, depth + 1)) {
     out.resize(o0);
     owner.resize(o0);
+    nodes.resize(n0);
     // the balanced split left a side that cannot split again: the midpoint
-    return balanced && nd_order_part_b(lo, hi, leaf, maxnb, nr, r0, out, owner, false);
+    return balanced && nd_order_part_b(lo, hi, leaf, maxnb, nr, r0, out, owner, false, nodes, depth);
   }
+  const int32_t code = sep_code(static_cast<int32_t>(nodes.size()));
+  nodes.push_back({r0, nr, depth, m, s_end});
   for (int t = m; t < s_end; ++t) {
     out.push_back(t);
-    owner.push_back(-1);
+    owner.push_back(code);
   }
   return true;
 }
 
 bool nd_order_part(int lo, int hi, int leaf, const std::vector<int32_t>& maxnb, int nr, int r0,
-                   std::vector<int32_t>& out, std::vector<int32_t>& owner) {
+                   std::vector<int32_t>& out, std::vector<int32_t>& owner, std::vector<SepNode>& nodes) {
   static const bool balanced = [] {
     const char* e = std::getenv("DYNOHIP_PART_BALANCE");   // 0: split at the midpoint tile (round 3)
     return !(e && e[0] == '0');
   }();
-  return nd_order_part_b(lo, hi, leaf, maxnb, nr, r0, out, owner, balanced);
+  nodes.clear();
+  return nd_order_part_b(lo, hi, leaf, maxnb, nr, r0, out, owner, balanced, nodes, 1);
 }
 
 constexpr int kUpdGroupTiles = 128;   // systems of this many tiles and more group update levels
@@ -203,7 +213,7 @@ void schedule(int NT, const std::vector<std::vector<int32_t>>& adj, const std::v
   S.order.clear();
   S.owner.clear();
   if (nranks > 1) {
-    S.ok = nd_order_part(0, NT, leaf, maxnb, nranks, 0, S.order, S.owner);
+    S.ok = nd_order_part(0, NT, leaf, maxnb, nranks, 0, S.order, S.owner, S.nodes);
     if (!S.ok) return;
   } else {
     nd_order(0, NT, leaf, maxnb, S.order);
@@ -305,10 +315,10 @@ void schedule(int NT, const std::vector<std::vector<int32_t>>& adj, const std::v
   // split contributions (sorted by R) into update tasks finishing before
   // level P and the pairs the panel at level P absorbs (appended to ppool
   // last: [*aoff, *aoff + *an))
-  // Partitioned: a separator tile (target owner -1) takes the contributions
-  // of interior columns as update tasks of their rank, never absorbed by its
-  // panel, so that the tile leaves phase 0 as that rank's partial Schur
-  // complement.
+  // Partitioned: a separator tile takes the contributions of every column
+  // outside its own node (interior columns, deeper separators) as update
+  // tasks of the source column's owner, never absorbed by its panel, so that
+  // the tile holds partial sums per rank until its node's exchange.
   auto plan_tile = [&](int32_t sl, int32_t P, int32_t* aoff, int32_t* an, int32_t town) {
     all.assign(cpool.begin() + cstart[sl], cpool.begin() + cfill[sl]);
     std::sort(all.begin(), all.end(), [](const Contrib& x, const Contrib& y) { return x.R < y.R; });
@@ -335,7 +345,7 @@ void schedule(int NT, const std::vector<std::vector<int32_t>>& adj, const std::v
     if (town < 0) {
       owners.clear();
       for (const Contrib& c : all)
-        if (c.own >= 0) owners.push_back(c.own);
+        if (c.own != town) owners.push_back(c.own);
       std::sort(owners.begin(), owners.end());
       owners.erase(std::unique(owners.begin(), owners.end()), owners.end());
       for (int32_t o : owners) {
@@ -346,7 +356,7 @@ void schedule(int NT, const std::vector<std::vector<int32_t>>& adj, const std::v
         emit_updates(mine, q, INT32_MAX, o);
       }
       for (const Contrib& c : all)
-        if (c.own < 0) cs.push_back(c);
+        if (c.own == town) cs.push_back(c);
     } else {
       cs = all;
     }
@@ -664,18 +674,18 @@ std::vector<int32_t> queue_order(const Plan& P, const std::vector<TileTask>& fta
   return order;
 }
 
-// keep the tasks whose owner is `who`, in schedule order, with their levels
+// keep the tasks q with keep(q), in schedule order, with their levels
 // renumbered densely (empty levels dropped)
-void filter_tasks(const std::vector<TileTask>& all, const std::vector<int32_t>& lev,
-                  const std::vector<int32_t>& owner, int32_t who, std::vector<TileTask>& ftask,
-                  std::vector<int32_t>& flevel, std::vector<int32_t>& fpanels) {
+template <class Keep>
+void filter_tasks(const std::vector<TileTask>& all, const std::vector<int32_t>& lev, Keep&& keep,
+                  std::vector<TileTask>& ftask, std::vector<int32_t>& flevel, std::vector<int32_t>& fpanels) {
   ftask.clear();
   flevel.assign(1, 0);
   fpanels.clear();
   for (size_t l = 0; l + 1 < lev.size(); ++l) {
     int np = 0;
     for (int32_t q = lev[l]; q < lev[l + 1]; ++q)
-      if (owner[q] == who) {
+      if (keep(q)) {
         ftask.push_back(all[q]);
         np += all[q].kind == 0;
       }
@@ -707,11 +717,12 @@ std::vector<int32_t> tile_maxnb(const Plan& P) {
 }  // namespace
 
 // the tile owners of nd_order_part's top splits (in natural tile order)
-bool partition_tile_owners(const Plan& P, int nranks, std::vector<int32_t>& owner) {
+bool partition_tile_owners(const Plan& P, int nranks, std::vector<int32_t>& owner, std::vector<SepNode>& nodes) {
   owner.assign(P.NT, 0);
+  nodes.clear();
   if (nranks <= 1) return true;
   std::vector<int32_t> out, own;
-  if (!nd_order_part(0, P.NT, 0, tile_maxnb(P), nranks, 0, out, own)) return false;
+  if (!nd_order_part(0, P.NT, 0, tile_maxnb(P), nranks, 0, out, own, nodes)) return false;
   for (size_t q = 0; q < out.size(); ++q) owner[out[q]] = own[q];
   return true;
 }
@@ -840,57 +851,116 @@ bool build_tile_schedule(Plan& P, bool own_threads) {
     P.row_start[t + 1] = static_cast<int32_t>(P.row_col.size());
   }
   // ---- partitioned: this rank's phase-0 tasks (its subtree, and its
-  // interior columns' updates of separator tiles), then the separator tasks
-  // every rank runs after the exchange
+  // interior columns' updates of separator tiles), then one phase per
+  // separator node on its path to the top, deepest first. A node's phase
+  // runs on every rank of its group: its panels and the updates among its
+  // own tiles; its updates of the separators above it run on the group's
+  // leader only (the others' copies of those tiles keep their own partial
+  // sums, so the next exchange counts each contribution once).
   P.tile_owner.assign(NT, 0);
   for (int cp = 0; cp < NT; ++cp) P.tile_owner[best.order[cp]] = best.owner[cp];
-  P.sep_slot_ranges.clear();
-  P.sep_tile_ranges.clear();
-  P.ftask1.clear();
-  P.flevel1.assign(1, 0);
-  P.fpanels1.clear();
-  P.fdep_start1.assign(1, 0);
-  P.fdep1.clear();
+  P.sep_nodes = best.nodes;
+  P.phases.clear();
+  P.rhs0_tile.clear();
+  P.rhs0_start.assign(1, 0);
+  P.rhs0_slot.clear();
   if (nr > 1) {
     const std::vector<TileTask> all = P.ftask;
     const std::vector<int32_t> lev = P.flevel;
-    filter_tasks(all, lev, best.task_owner, P.rank, P.ftask, P.flevel, P.fpanels);
-    filter_tasks(all, lev, best.task_owner, -1, P.ftask1, P.flevel1, P.fpanels1);
-    build_dataflow_deps(P, P.ftask1, P.flevel1, P.fdep_start1, P.fdep1);
-    P.fqueue1 = queue_order(P, P.ftask1, P.flevel1, P.fdep_start1, P.fdep1, queue_workers());
-    // backward: separator columns first (they are the top of the tree), then
-    // this rank's interior, in the global level order
+    // the owner of each slot's column
+    std::vector<int32_t> slot_own(best.n_slots);
+    for (int cp = 0; cp < NT; ++cp)
+      for (size_t x = 0; x < best.st[cp].size(); ++x) slot_own[best.slot_base[cp] + x] = best.owner[cp];
+    auto in_group = [&](int32_t node, int32_t r) {
+      const SepNode& nd = P.sep_nodes[node];
+      return r >= nd.r0 && r < nd.r0 + nd.nr;
+    };
+    filter_tasks(all, lev, [&](int32_t q) { return best.task_owner[q] == P.rank; }, P.ftask, P.flevel, P.fpanels);
+    // this rank's nodes, deepest first
+    std::vector<int32_t> path;
+    for (int32_t nd = 0; nd < static_cast<int32_t>(P.sep_nodes.size()); ++nd)
+      if (in_group(nd, P.rank)) path.push_back(nd);
+    std::stable_sort(path.begin(), path.end(),
+                     [&](int32_t a, int32_t b) { return P.sep_nodes[a].depth > P.sep_nodes[b].depth; });
+    // slot ranges of a node's columns (contiguous per column position)
+    auto node_slots = [&](int32_t depth, std::vector<int32_t>& xs, std::vector<int32_t>& xt) {
+      xs.clear();
+      xt.clear();
+      for (int cp = 0; cp < NT; ++cp) {
+        const int32_t o = best.owner[cp];
+        if (o >= 0 || P.sep_nodes[sep_node(o)].depth != depth) continue;
+        const int32_t b = best.slot_base[cp], e = b + static_cast<int32_t>(best.st[cp].size());
+        if (!xs.empty() && xs.back() == b) xs.back() = e;
+        else {
+          xs.push_back(b);
+          xs.push_back(e);
+        }
+      }
+      for (int t = 0; t < NT; ++t) {
+        const int32_t o = P.tile_owner[t];
+        if (o >= 0 || P.sep_nodes[sep_node(o)].depth != depth) continue;
+        if (!xt.empty() && xt.back() == t) xt.back() = t + 1;
+        else {
+          xt.push_back(t);
+          xt.push_back(t + 1);
+        }
+      }
+    };
+    // the contributions of columns owned by `src` to rows of other
+    // separators (k_sep_rhs lists)
+    auto rhs_lists = [&](int32_t src, std::vector<int32_t>& tl, std::vector<int32_t>& ts, std::vector<int32_t>& sl) {
+      tl.clear();
+      ts.assign(1, 0);
+      sl.clear();
+      for (int t = 0; t < NT; ++t) {
+        const int32_t o = P.tile_owner[t];
+        if (o >= 0 || o == src) continue;
+        const size_t n0 = sl.size();
+        for (int32_t e = P.row_start[t]; e < P.row_start[t + 1]; ++e)
+          if (P.tile_owner[P.row_col[e]] == src) sl.push_back(P.row_slot[e]);
+        if (sl.size() == n0) continue;
+        tl.push_back(t);
+        ts.push_back(static_cast<int32_t>(sl.size()));
+      }
+    };
+    rhs_lists(P.rank, P.rhs0_tile, P.rhs0_start, P.rhs0_slot);
+    P.phases.resize(path.size());
+    for (size_t ph = 0; ph < path.size(); ++ph) {
+      PartPhase& F = P.phases[ph];
+      const int32_t nd = path[ph], code = sep_code(nd);
+      F.node = nd;
+      F.leader = P.sep_nodes[nd].r0 == P.rank ? 1 : 0;
+      node_slots(P.sep_nodes[nd].depth, F.xslot, F.xtile);
+      filter_tasks(all, lev,
+                   [&](int32_t q) {
+                     if (best.task_owner[q] != code) return false;
+                     // updates of another node's tiles: the leader only
+                     return all[q].kind == 0 || slot_own[all[q].dst] == code || F.leader;
+                   },
+                   F.ftask, F.flevel, F.fpanels);
+      build_dataflow_deps(P, F.ftask, F.flevel, F.fdep_start, F.fdep);
+      F.fqueue = queue_order(P, F.ftask, F.flevel, F.fdep_start, F.fdep, queue_workers());
+      rhs_lists(code, F.rhs_tile, F.rhs_start, F.rhs_slot);
+    }
+    // backward: this rank's separator columns first (the top of the tree),
+    // then its interior, in the global level order
+    std::vector<int32_t> mine_codes;
+    for (int32_t nd : path) mine_codes.push_back(sep_code(nd));
     std::vector<BackPart> keep;
     std::vector<int32_t> klev(1, 0);
     for (int pass = 0; pass < 2; ++pass) {
-      const int32_t who = pass == 0 ? -1 : P.rank;
       for (size_t l = 0; l + 1 < P.bplevel.size(); ++l) {
-        for (int32_t q = P.bplevel[l]; q < P.bplevel[l + 1]; ++q)
-          if (P.tile_owner[P.bpart[q].k] == who) keep.push_back(P.bpart[q]);
+        for (int32_t q = P.bplevel[l]; q < P.bplevel[l + 1]; ++q) {
+          const int32_t o = P.tile_owner[P.bpart[q].k];
+          const bool take = pass == 0 ? std::find(mine_codes.begin(), mine_codes.end(), o) != mine_codes.end()
+                                      : o == P.rank;
+          if (take) keep.push_back(P.bpart[q]);
+        }
         if (static_cast<int32_t>(keep.size()) != klev.back()) klev.push_back(static_cast<int32_t>(keep.size()));
       }
     }
     P.bpart = std::move(keep);
     P.bplevel = std::move(klev);
-    // exchanged data: every stored tile of the separator columns (contiguous
-    // slots per column position), and the separator rows of the RHS
-    for (int cp = 0; cp < NT; ++cp) {
-      if (best.owner[cp] >= 0) continue;
-      const int32_t b = best.slot_base[cp], e = b + static_cast<int32_t>(best.st[cp].size());
-      if (!P.sep_slot_ranges.empty() && P.sep_slot_ranges.back() == b) P.sep_slot_ranges.back() = e;
-      else {
-        P.sep_slot_ranges.push_back(b);
-        P.sep_slot_ranges.push_back(e);
-      }
-    }
-    for (int t = 0; t < NT; ++t) {
-      if (P.tile_owner[t] >= 0) continue;
-      if (!P.sep_tile_ranges.empty() && P.sep_tile_ranges.back() == t) P.sep_tile_ranges.back() = t + 1;
-      else {
-        P.sep_tile_ranges.push_back(t);
-        P.sep_tile_ranges.push_back(t + 1);
-      }
-    }
   }
   bmark("rows, partition");
   build_dataflow_deps(P, P.ftask, P.flevel, P.fdep_start, P.fdep);

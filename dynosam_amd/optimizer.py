@@ -210,8 +210,9 @@ def plan_schedule(graph, values):
 
 def plan_export(graph, values, name, nranks=1, rank=0):
     """Host-only: one named int32 array of the (partitioned) plan of `rank`
-    (dynohip_plan_export). Structs come back flattened: ftask / ftask1 10
-    ints per task, bpart 8 ints per part."""
+    (dynohip_plan_export). Structs come back flattened: ftask and the
+    separator phases' "phase<p>_ftask" 10 ints per task, bpart 8 ints per
+    part."""
     lib = _native.load("libdynohip.so")
     gv = graph.view()
     keys = np.ascontiguousarray(values.keys, dtype=np.uint64)
@@ -226,7 +227,7 @@ def plan_export(graph, values, name, nranks=1, rank=0):
     rc = lib.dynohip_plan_export(C.byref(gv), kp, kk, keys.shape[0], int(nranks), int(rank), name.encode(),
                                  out.ctypes.data_as(C.POINTER(C.c_int32)), n.value, C.byref(n))
     _check(lib, None, rc)
-    if name in ("ftask", "ftask1"):
+    if name == "ftask" or (name.startswith("phase") and name.endswith("_ftask")):
         return out.reshape(-1, 10)
     if name == "bpart":
         return out.reshape(-1, 8)

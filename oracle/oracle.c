@@ -510,6 +510,10 @@ struct oracle_problem {
      factors and eliminates the point components in reverse order, which
      changes only the rounding of the reduced system */
   int reverse_sums;
+  /* control (oracle_set_solve_ld): every damped solve of the LM in x87
+     extended precision (solve_schur_ld): the exact-step trajectory that
+     the deep-convergence free runs are compared with */
+  int solve_ld;
   char err[256];
   /* structure for the Schur solve */
   int* comp_of;        /* per variable: component id (points) or -1 */
@@ -554,6 +558,7 @@ static void set_err(oracle_problem* p, const char* fmt, ...) {
 const char* oracle_last_error(const oracle_problem* p) { return p ? p->err : "null"; }
 void oracle_set_dense(oracle_problem* p, int dense) { p->dense = dense; }
 void oracle_set_reverse_sums(oracle_problem* p, int reverse) { p->reverse_sums = reverse; }
+void oracle_set_solve_ld(oracle_problem* p, int on) { p->solve_ld = on; }
 
 static int cmp_keyidx(const void* a, const void* b) {
   const keyidx_t* x = (const keyidx_t*)a;
@@ -1222,7 +1227,9 @@ static size_t make_doff(const oracle_problem* p, size_t* doff) {
 }
 
 static int solve_schur_mt(oracle_problem* p, double lambda, double* delta, const size_t* doff);
+static int solve_schur_ld(oracle_problem* p, double lambda, double* delta, const size_t* doff);
 static int solve_system(oracle_problem* p, double lambda, double* delta, const size_t* doff, size_t N) {
+  if (p->solve_ld) return solve_schur_ld(p, lambda, delta, doff);
   if (p->dense) return solve_dense(p, lambda, delta, doff, N);
   if (p->nthreads > 1 && !p->reverse_sums) return solve_schur_mt(p, lambda, delta, doff);
   return solve_schur(p, lambda, delta, doff);

@@ -51,6 +51,8 @@ void oracle_set_dense(oracle_problem* p, int dense);
 /* rounding control: the Schur solve sums factors and point components in
    reverse order (serial solve); the same mathematics, other rounding */
 void oracle_set_reverse_sums(oracle_problem* p, int reverse);
+/* every LM solve in x87 extended precision (test reference, serial) */
+void oracle_set_solve_ld(oracle_problem* p, int on);
 /* threads of the Schur + skyline LM (default 1); the trajectory is
    bit-identical for every thread count (the all-cores CPU baseline) */
 int oracle_set_threads(oracle_problem* p, int nthreads);

@@ -34,6 +34,8 @@ def lib(libm=False):
         L.oracle_set_dense.argtypes = [vp, C.c_int]
         L.oracle_set_reverse_sums.argtypes = [vp, C.c_int]
         L.oracle_set_reverse_sums.restype = None
+        L.oracle_set_solve_ld.argtypes = [vp, C.c_int]
+        L.oracle_set_solve_ld.restype = None
         L.oracle_set_threads.argtypes = [vp, C.c_int]
         L.oracle_set_threads.restype = C.c_int
         L.oracle_error.argtypes = [vp]
@@ -76,7 +78,7 @@ def dptr(a):
 class Oracle:
     """CPU restatement of LevenbergMarquardtOptimizer(graph, values).optimize()."""
 
-    def __init__(self, graph, values, dense=False, threads=1, reverse_sums=False, libm=False):
+    def __init__(self, graph, values, dense=False, threads=1, reverse_sums=False, libm=False, solve_ld=False):
         L = self.L = lib(libm)
         self.graph = graph
         self.values = values
@@ -97,6 +99,8 @@ class Oracle:
             L.oracle_set_reverse_sums(self.h, 1)
         if threads > 1:
             L.oracle_set_threads(self.h, int(threads))
+        if solve_ld:   # every LM step solved in extended precision: the exact-step trajectory
+            L.oracle_set_solve_ld(self.h, 1)
         self.ndata = data.shape[0]
 
     def __del__(self):

@@ -2,20 +2,24 @@
 
 The plan of every rank (dynohip_plan_export with nranks > 1) is replayed in
 numpy with the semantics of the kernels it drives (k_tasks / k_back in
-csrc/tilechol.hip, k_sep_rhs in csrc/kernels.hip, the separator all-reduce
-of solver.cpp):
+csrc/tilechol.hip, k_sep_rhs in csrc/kernels.hip, the per-depth separator
+all-reduces of solver.cpp):
   * each rank gets a share of a random SPD matrix and right-hand side whose
     support lies in its interior tiles and the separators (separator-only
-    entries split at random between the ranks, as factors touching only
-    separators may sit on any rank);
+    entries split at random between all ranks: every exchange sums over the
+    whole world, so any rank's share of a separator is counted);
   * phase 0: the rank's own tasks, then its interior contributions leave
     the separator RHS rows;
-  * the separator tiles and rows are summed over ranks (the all-reduce);
-  * phase 1 and the backward substitution on every rank;
-and the rows every rank owns (its interior and the separators) must match
-numpy.linalg.solve of the whole matrix. Also checks the factor ownership:
-every factor and landmark chain lands on exactly one rank, and the ranks'
-factor counts add up to the graph.
+  * per separator depth, deepest first: that depth's separator tiles and
+    rows are summed over ranks (the all-reduce), every rank runs its node's
+    tasks (the group's leader also its updates of the separators above), and
+    the node's contributions leave the RHS rows above (leader) or are
+    dropped (the other members);
+  * the backward substitution on every rank;
+and the rows every rank solves (its interior and its separator nodes) must
+match numpy.linalg.solve of the whole matrix. Also checks the factor
+ownership: every factor and landmark chain lands on exactly one rank, and
+the ranks' factor counts add up to the graph.
 """
 import numpy as np
 import pytest
@@ -25,12 +29,25 @@ from dynosam_amd.optimizer import plan_export, plan_schedule
 
 T = 64
 NAMES = ("info", "tile_pos", "tile_owner", "row_start", "row_col", "row_slot", "pairs", "ftask", "flevel",
-         "ftask1", "flevel1", "bpart", "bplevel", "bent", "sep_slot_ranges", "sep_tile_ranges", "value_owner",
-         "damp_row")
+         "bpart", "bplevel", "bent", "value_owner", "damp_row", "phases", "sep_nodes", "rhs0_tile", "rhs0_start",
+         "rhs0_slot")
+PHASE_NAMES = ("ftask", "flevel", "xslot", "xtile", "rhs_tile", "rhs_start", "rhs_slot")
 
 
 def export_all(graph, values, nranks, rank):
-    return {k: plan_export(graph, values, k, nranks, rank) for k in NAMES}
+    p = {k: plan_export(graph, values, k, nranks, rank) for k in NAMES}
+    p["phase"] = [{k: plan_export(graph, values, f"phase{ph}_{k}", nranks, rank) for k in PHASE_NAMES}
+                  for ph in range(len(p["phases"]) // 2)]
+    return p
+
+
+def sep_nodes(plan):
+    """(r0, nr, depth, t0, t1) per separator node"""
+    return plan["sep_nodes"].reshape(-1, 5)
+
+
+def sep_code(node):
+    return -1 - node
 
 
 def random_spd(n_pose, NT, red_a, red_b, rng):
@@ -163,16 +180,15 @@ class RankState:
                     slots[dst] = L
                     self.contrib[dst] = L @ yk
 
-    def sep_rhs(self, rank):
-        p = self.p
-        owner = p["tile_owner"]
-        for b, e in p["sep_tile_ranges"].reshape(-1, 2):
-            for s in range(b, e):
-                for q in range(p["row_start"][s], p["row_start"][s + 1]):
-                    if owner[p["row_col"][q]] == rank:
-                        sl = p["row_slot"][q]
-                        self.r[s] -= self.contrib[sl]
-                        self.contrib[sl] = 0.0
+    def sep_rhs(self, tiles, start, slots, apply):
+        """k_sep_rhs: the listed contributions leave row tile tiles[q]
+        (subtracted when `apply`) and are cleared"""
+        for q, s in enumerate(tiles):
+            for e in range(start[q], start[q + 1]):
+                sl = slots[e]
+                if apply:
+                    self.r[s] -= self.contrib[sl]
+                self.contrib[sl] = 0.0
 
     def backward(self):
         bp, bl, be = self.p["bpart"], self.p["bplevel"], self.p["bent"].reshape(-1, 2)
@@ -195,7 +211,7 @@ def replay_partitioned(name, nranks, seed=5, **kw):
     owner = plans[0]["tile_owner"]
     for p in plans[1:]:
         assert np.array_equal(p["tile_owner"], owner)
-        assert np.array_equal(p["ftask1"], plans[0]["ftask1"])
+        assert np.array_equal(p["sep_nodes"], plans[0]["sep_nodes"])
     rng = np.random.default_rng(seed)
     M = random_spd(glob["n_pose"], glob["n_tiles"], glob["red_a"], glob["red_b"], rng)
     rhs = rng.standard_normal(M.shape[0])
@@ -203,22 +219,37 @@ def replay_partitioned(name, nranks, seed=5, **kw):
     states = [RankState(plans[r], Ms[r], rs[r]) for r in range(nranks)]
     for r, st in enumerate(states):
         st.forward(st.p["ftask"], st.p["flevel"])
-        st.sep_rhs(r)
-    # the all-reduce of the separator tiles and right-hand side rows
-    ssr, str_ = plans[0]["sep_slot_ranges"].reshape(-1, 2), plans[0]["sep_tile_ranges"].reshape(-1, 2)
-    for b, e in ssr:
-        tot = sum(st.slots[b:e] for st in states)
-        for st in states:
-            st.slots[b:e] = tot
-    for b, e in str_:
-        tot = sum(st.r[b:e] for st in states)
-        for st in states:
-            st.r[b:e] = tot
+        st.sep_rhs(st.p["rhs0_tile"], st.p["rhs0_start"], st.p["rhs0_slot"], True)
+    nodes = sep_nodes(plans[0])
+    nph = len(plans[0]["phase"])
+    assert all(len(p["phase"]) == nph for p in plans)
+    for ph in range(nph):
+        # the all-reduce of this depth's separator tiles and right-hand side rows
+        px = plans[0]["phase"][ph]
+        for p in plans[1:]:
+            assert np.array_equal(p["phase"][ph]["xslot"], px["xslot"])
+            assert np.array_equal(p["phase"][ph]["xtile"], px["xtile"])
+        for b, e in px["xslot"].reshape(-1, 2):
+            tot = sum(st.slots[b:e] for st in states)
+            for st in states:
+                st.slots[b:e] = tot
+        for b, e in px["xtile"].reshape(-1, 2):
+            tot = sum(st.r[b:e] for st in states)
+            for st in states:
+                st.r[b:e] = tot
+        for r, st in enumerate(states):
+            node, leader = (int(v) for v in st.p["phases"][2 * ph:2 * ph + 2])
+            r0, nr, depth = nodes[node][:3]
+            assert r0 <= r < r0 + nr and leader == (r == r0)
+            assert depth == nph - ph
+            F = st.p["phase"][ph]
+            st.forward(F["ftask"], F["flevel"])
+            st.sep_rhs(F["rhs_tile"], F["rhs_start"], F["rhs_slot"], bool(leader))
     ref = np.linalg.solve(M, rhs).reshape(-1, T)
     for r, st in enumerate(states):
-        st.forward(st.p["ftask1"], st.p["flevel1"])
         st.backward()
-        mine = [t for t in range(st.NT) if owner[t] in (-1, r)]
+        path = {sep_code(int(st.p["phases"][2 * ph])) for ph in range(nph)}
+        mine = [t for t in range(st.NT) if owner[t] == r or owner[t] in path]
         assert np.allclose(st.x[mine], ref[mine], rtol=1e-9, atol=1e-10), f"rank {r}"
     return plans, graph, values
 
@@ -252,9 +283,8 @@ def test_partition_ownership():
     assert total == int(infos[0][6])
     vo = plan_export(graph, values, "value_owner", nranks, 0)
     kinds = np.asarray(values.kinds)
-    # every landmark has exactly one owning rank, poses are owned or replicated
-    assert (vo[kinds == 1] >= 0).all() and (vo[kinds == 1] < nranks).all()
-    assert (vo >= -1).all()
+    # every value has exactly one owning rank (a separator pose: its node's leader)
+    assert (vo >= 0).all() and (vo < nranks).all()
     # ranks hold disjoint landmark sets that cover the graph
     n_pts = [int(plan_export(graph, values, "info", nranks, r)[4]) for r in range(nranks)]
     assert sum(n_pts) == int((kinds == 1).sum())

@@ -231,10 +231,12 @@ def test_dataflow_queue_order_is_topological(name):
 def test_partitioned_queue_orders_are_topological():
     from dynosam_amd.optimizer import plan_export
     g, v, _ = synth.generate("C2")
-    for rank in range(2):
-        for sfx in ("", "1"):
-            ft = plan_export(g, v, "ftask" + sfx, nranks=2, rank=rank).reshape(-1, 10)
-            fs = plan_export(g, v, "fdep_start" + sfx, nranks=2, rank=rank)
-            fd = plan_export(g, v, "fdep" + sfx, nranks=2, rank=rank).reshape(-1, 2)
-            qu = plan_export(g, v, "fqueue" + sfx, nranks=2, rank=rank)
-            queue_is_topological(ft, fs, fd, qu)
+    for nranks in (2, 4):
+        for rank in range(nranks):
+            nph = len(plan_export(g, v, "phases", nranks=nranks, rank=rank)) // 2
+            for pre in [""] + [f"phase{k}_" for k in range(nph)]:
+                ft = plan_export(g, v, pre + "ftask", nranks=nranks, rank=rank).reshape(-1, 10)
+                fs = plan_export(g, v, pre + "fdep_start", nranks=nranks, rank=rank)
+                fd = plan_export(g, v, pre + "fdep", nranks=nranks, rank=rank).reshape(-1, 2)
+                qu = plan_export(g, v, pre + "fqueue", nranks=nranks, rank=rank)
+                queue_is_topological(ft, fs, fd, qu)
