@@ -1028,9 +1028,35 @@ void compute_base_stats(dynohip_solver* s) {
   if (fused_lone(s))
     for (const LoneGroup& G : P.lgroup) impl += 8.0 * 42.0 * G.m;
   st.lin_bytes_impl = impl;
+  // the reduced assembly: every entry descriptor (16 B), every distinct
+  // operand block once (a block feeding several targets is counted once: the
+  // re-reads are L2 hits, not algorithmic bytes) and every output written
   double asmb = 0.0;
-  for (const GEntry& e : P.gRed.ent) asmb += 16.0 + 8.0 * e.k * 12.0;
-  for (const GEntry& e : P.gGred.ent) asmb += 16.0 + 8.0 * e.k * 7.0;
+  {
+    std::vector<uint64_t> blk;   // (arena offset << 8) | doubles
+    blk.reserve(2 * (P.gRed.ent.size() + P.gGred.ent.size()));
+    auto add = [&](uint32_t off, int nd) { blk.push_back((static_cast<uint64_t>(off) << 8) | static_cast<uint64_t>(nd)); };
+    for (const GEntry& e : P.gRed.ent) {
+      if (e.sign == kAddBlock) {
+        add(e.b, 36);
+      } else {
+        add(e.a, 6 * e.k);
+        add(e.b, 6 * e.k);
+      }
+    }
+    for (const GEntry& e : P.gGred.ent) {
+      if (e.sign == kAddBlock) {
+        add(e.b, 6);
+      } else {
+        add(e.a, 6 * e.k);
+        add(e.b, e.k);
+      }
+    }
+    std::sort(blk.begin(), blk.end());
+    blk.erase(std::unique(blk.begin(), blk.end()), blk.end());
+    for (uint64_t x : blk) asmb += 8.0 * static_cast<double>(x & 0xffu);
+    asmb += 16.0 * static_cast<double>(P.gRed.ent.size() + P.gGred.ent.size());
+  }
   asmb += 36.0 * 8.0 * P.gRed.ntargets() + 6.0 * 8.0 * P.n_pose;
   st.assembly_bytes = asmb;
   // envelope Cholesky flop count of the reduced system

@@ -245,8 +245,11 @@ typedef struct {
                                 H_lc per point-pose edge, m-m block per
                                 chain link, H_cc + g per pose, 6x6 per
                                 pose-pose pair)                              */
-  double assembly_bytes;     /* algorithmic bytes of one reduced assembly
-                                (gather lists + blocks read, band written)  */
+  double assembly_bytes;     /* algorithmic bytes of one reduced assembly:
+                                gather-list entries, every distinct operand
+                                block once, the band and gradient written
+                                (since ABI v3 the operand blocks are counted
+                                once, not per entry that reads them)        */
   double chol_flops;         /* algorithmic flops of one envelope Cholesky  */
   double chol_tile_flops;    /* flops actually issued by the tile algorithm */
   /* accumulated device time (ms, HIP events) and counts since lm_reset.
