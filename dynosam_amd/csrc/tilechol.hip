@@ -446,7 +446,38 @@ struct TaskLds {
   double vv[T];        // r_k minus the contributions of eliminated columns
   double yv[T];        // y_k = L_kk^-1 vv
   double tv[4][16];    // forward substitution scratch, per block
+  // own panels: per block step KB, "U row KB published" flags holding the
+  // task's sequence number (flagA: W_KB and U[KB][KB+1], flagB: the whole
+  // row), and "y_KB out" (factor_own_w)
+  int flagA[4], flagB[4], yflag[4];
 };
+
+// Hand-offs between the waves of one workgroup through LDS: the producer
+// drains its LDS writes (lgkmcnt(0)) and then stores the flag; a consumer
+// polls the flag and only then issues its loads (LDS operations of one wave
+// complete in order, so a consumer that sees the flag sees the data).
+__device__ __forceinline__ void lds_flag_set(int* f, int v) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if ((threadIdx.x & 63) == 0) __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  asm volatile("" ::: "memory");
+}
+// The poll is one opaque loop of five instructions (the compiler would
+// otherwise duplicate the code around every inlined spin loop).
+__device__ __forceinline__ void lds_flag_wait(const int* f, int v) {
+  const unsigned a = static_cast<unsigned>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const int*)f));
+  int t;
+  int st;
+  asm volatile(
+      "1:\n\t"
+      "ds_read_b32 %0, %2\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "v_readfirstlane_b32 %1, %0\n\t"
+      "s_cmp_lg_u32 %1, %3\n\t"
+      "s_cbranch_scc1 1b"
+      : "=&v"(t), "=&s"(st)
+      : "v"(a), "s"(v)
+      : "memory", "scc");
+}
 
 // Launch-invariant inputs of a panel task: operand slots, the entries of
 // tile row k and r_k. They are fetched before the dependency wait, so that
@@ -564,12 +595,13 @@ __device__ __forceinline__ double sum_groups(double v) {
 
 template <int w, class DiagPend, class Chunk>
 __device__ bool factor_own_w(v4d (&accA)[4], v4d (&XT)[4], int l, TaskLds& S, DiagPend&& diagpend, Chunk&& chunk,
-                             int q) {
+                             int q, int seq) {
   bool ok = true;
   const int li = l & 15, g = l >> 4;
   double* const U = S.Ust;
   auto Ublk = [&](int c, int tj) { return U + (c * 4 + tj) * 256; };
   auto subst = [&](int c) {
+    lds_flag_wait(&S.flagB[c], seq);   // W_c and every U[c'][c], c' < c
     v4d Tm;   // A(w, c)^T: element (j = g + 4r, i = li) = A[16w + i][16c + j]
 #pragma unroll
     for (int r = 0; r < 4; ++r) Tm[r] = S.As[(16 * w + li) * LD + 16 * c + g + 4 * r];
@@ -584,6 +616,8 @@ __device__ bool factor_own_w(v4d (&accA)[4], v4d (&XT)[4], int l, TaskLds& S, Di
     XT[c] = mfma_tn(ld_blk(Ublk(c, c), l), Tm, v4d{0.0, 0.0, 0.0, 0.0}, false);
   };
   auto ystep = [&](int c) {   // y_c = W_c^T (vv_c - sum_{c' < c} U[c'][c]^T y_c')
+    lds_flag_wait(&S.flagB[c], seq);
+    if (c > 0) lds_flag_wait(&S.yflag[c - 1], seq);
     double part = 0.0;
 #pragma unroll
     for (int cp = 0; cp < 3; ++cp)
@@ -600,6 +634,7 @@ __device__ bool factor_own_w(v4d (&accA)[4], v4d (&XT)[4], int l, TaskLds& S, Di
     for (int r = 0; r < 4; ++r) yp += Wc[r] * S.tv[c][g + 4 * r];
     yp = sum_groups(yp);
     if (g == 0) S.yv[16 * c + li] = yp;
+    lds_flag_set(&S.yflag[c], seq);
   };
   auto act = [&](int slot) {
 #pragma unroll
@@ -610,6 +645,19 @@ __device__ bool factor_own_w(v4d (&accA)[4], v4d (&XT)[4], int l, TaskLds& S, Di
       else if (x >= 0x10) chunk(x - 0x10);
     }
   };
+  // step KB's trailing update of this wave's blocks TJ in [t0, t1)
+  auto trailing = [&](int KB, int t0, int t1) {
+    const v4d Uv = ld_blk(Ublk(KB, w), l);
+#pragma unroll
+    for (int TJ = 0; TJ < 4; ++TJ)
+      if (TJ >= t0 && TJ < t1) accA[TJ] = mfma_tn(Uv, ld_blk(Ublk(KB, TJ), l), accA[TJ], true);
+  };
+  // No barrier per block step: the waves hand the U rows over through LDS
+  // flags, so a wave waits only for the data it reads, not for the other
+  // waves' chunk and substitution work. The wave that factors next takes
+  // step KB's update of its diagonal block as soon as W_KB and U[KB][KB+1]
+  // are out (flagA), factors, and only then applies step KB's update to its
+  // other blocks (flagB): each block still receives its updates in step order.
 #pragma unroll
   for (int KB = 0; KB < 4; ++KB) {
     if (w != KB) {
@@ -622,22 +670,33 @@ __device__ bool factor_own_w(v4d (&accA)[4], v4d (&XT)[4], int l, TaskLds& S, Di
       TCLKW(16 + 4 * KB, q);
       factor16(accA[KB], Wm, l, ok, &S.rpart[w][0]);
       TCLKW(17 + 4 * KB, q);
+      if (KB >= 1 && KB + 1 < 4) {
+        // the rest of step KB-1's update of this wave's blocks, off the
+        // diagonal block's path but before this row's U blocks use them
+        lds_flag_wait(&S.flagB[KB - 1], seq);
+        trailing(KB - 1, KB + 1, 4);
+      }
       st_blk(Ublk(KB, KB), Wm, l);
+      if (KB + 1 < 4) {
+        accA[KB + 1] = mfma_tn(Wm, accA[KB + 1], v4d{0.0, 0.0, 0.0, 0.0}, false);
+        st_blk(Ublk(KB, KB + 1), accA[KB + 1], l);
+      }
+      lds_flag_set(&S.flagA[KB], seq);
 #pragma unroll
-      for (int TJ = KB + 1; TJ < 4; ++TJ) {
+      for (int TJ = KB + 2; TJ < 4; ++TJ) {
         accA[TJ] = mfma_tn(Wm, accA[TJ], v4d{0.0, 0.0, 0.0, 0.0}, false);
         st_blk(Ublk(KB, TJ), accA[TJ], l);
       }
+      lds_flag_set(&S.flagB[KB], seq);
       TCLKW(18 + 4 * KB, q);
     }
-    __syncthreads();
-    TCLK(12 + KB, q, rtc());
     if (w == KB) TCLKW(19 + 4 * KB, q);
-    if (w > KB) {
-      const v4d Uv = ld_blk(Ublk(KB, w), l);
-#pragma unroll
-      for (int TJ = 0; TJ < 4; ++TJ)
-        if (TJ >= w) accA[TJ] = mfma_tn(Uv, ld_blk(Ublk(KB, TJ), l), accA[TJ], true);
+    if (w == KB + 1) {
+      lds_flag_wait(&S.flagA[KB], seq);
+      trailing(KB, w, w + 1);   // the next diagonal block: the critical path
+    } else if (w > KB + 1) {
+      lds_flag_wait(&S.flagB[KB], seq);
+      trailing(KB, w, 4);
     }
     act(2 * KB + 1);
   }
@@ -646,12 +705,12 @@ __device__ bool factor_own_w(v4d (&accA)[4], v4d (&XT)[4], int l, TaskLds& S, Di
 
 template <class DiagPend, class Chunk>
 __device__ __forceinline__ bool factor_own(v4d (&accA)[4], v4d (&XT)[4], int w, int l, TaskLds& S,
-                                           DiagPend&& diagpend, Chunk&& chunk, int q) {
+                                           DiagPend&& diagpend, Chunk&& chunk, int q, int seq) {
   switch (__builtin_amdgcn_readfirstlane(w)) {
-    case 0: return factor_own_w<0>(accA, XT, l, S, diagpend, chunk, q);
-    case 1: return factor_own_w<1>(accA, XT, l, S, diagpend, chunk, q);
-    case 2: return factor_own_w<2>(accA, XT, l, S, diagpend, chunk, q);
-    default: return factor_own_w<3>(accA, XT, l, S, diagpend, chunk, q);
+    case 0: return factor_own_w<0>(accA, XT, l, S, diagpend, chunk, q, seq);
+    case 1: return factor_own_w<1>(accA, XT, l, S, diagpend, chunk, q, seq);
+    case 2: return factor_own_w<2>(accA, XT, l, S, diagpend, chunk, q, seq);
+    default: return factor_own_w<3>(accA, XT, l, S, diagpend, chunk, q, seq);
   }
 }
 
@@ -659,7 +718,7 @@ template <bool SC1, class LateWait = NoWait>
 __device__ __forceinline__ void panel_task(const TileDev& b, const TileTask& tk, const int32_t* __restrict__ pairs,
                                            const PanelPre& p, double* __restrict__ Linv, double* __restrict__ contrib,
                                            double* __restrict__ y, int* fail, TaskLds& S, int q = 0,
-                                           LateWait&& late = LateWait()) {
+                                           LateWait&& late = LateWait(), int seq = 1) {
   double* const Ps = S.Ps;
   double* const Qs = S.Qs;
   double* const As = S.As;
@@ -813,7 +872,7 @@ __device__ __forceinline__ void panel_task(const TileDev& b, const TileTask& tk,
       for (int rr = 0; rr < 4; ++rr) As[ACC_ROW(w, l, rr) * LD + ACC_COL(c, l)] -= tot[rr];
     };
     v4d XT[4];
-    factor_own(accA, XT, w, l, S, diagpend, chunk, q);
+    factor_own(accA, XT, w, l, S, diagpend, chunk, q, seq);
     __syncthreads();   // y_3 (wave 1, after the last barrier)
     TCLK(3, q, rtc());
     TCLK(8, q, rtc());
@@ -886,6 +945,7 @@ __global__ __launch_bounds__(256) void k_tasks(TileDev b, const TileTask* __rest
   __shared__ TaskLds S;
   const TileTask tk = tasks[blockIdx.x];
   const int tid = threadIdx.x;
+  if (tid < 4) S.flagA[tid] = S.flagB[tid] = S.yflag[tid] = 0;   // seen after panel_task's first barrier
   if (tk.kind == 1) {
     run_update<false>(b, tk, pairs, S.Qs, S.Ps, tid, tid >> 6, tid & 63);
     return;
@@ -930,6 +990,7 @@ __global__ __launch_bounds__(256) void k_factor_persist(TileDev b, const TileTas
   __shared__ int s_q;
   const int tid = threadIdx.x;
   const int w = tid >> 6, l = tid & 63;
+  if (tid < 4) S.flagA[tid] = S.flagB[tid] = S.yflag[tid] = 0;   // tasks flag with qpos + 1
   for (;;) {
     if (tid == 0) s_q = static_cast<int>(__hip_atomic_fetch_add(queue, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     __syncthreads();
@@ -990,7 +1051,7 @@ __global__ __launch_bounds__(256) void k_factor_persist(TileDev b, const TileTas
       }
     };
     if (tk.kind == 1) run_update<true>(b, tk, pairs, S.Qs, S.Ps, tid, w, l, upa, upb, late);
-    else panel_task<true>(b, tk, pairs, p, Linv, contrib, y, fail, S, q, late);
+    else panel_task<true>(b, tk, pairs, p, Linv, contrib, y, fail, S, q, late, qpos + 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     TCLK(4, q, rtc());

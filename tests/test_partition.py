@@ -383,14 +383,17 @@ def _run_partition_check(tmp_path, config, nranks, extra=(), timeout=240):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nranks", [2, 4])
+@pytest.mark.parametrize("nranks", [2, 4, 8])
 def test_partitioned_lm_matches_single_gpu(tmp_path, nranks):
     """The partitioned solve on `nranks` processes sharing the GPU (gloo
     exchange) against the single-handle solve of the same C2 graph
     (tools/partition_check.py): conditioned on the single handle's values
     and lambda, every outer iteration lands within the north-star 1e-6
     relative Frobenius with the same inner-iteration count; free-running,
-    the iteration counts and accept sequence are identical."""
+    the iteration counts and accept sequence are identical. At 4 and 8
+    ranks the separators of the deeper splits are factored by groups of 2
+    (and 4) ranks, the group's other ranks dropping the contributions their
+    leader passes up."""
     res, r = _run_partition_check(tmp_path, "C2", nranks)
     assert r.returncode == 0 and res["ok"], r.stdout[-2000:] + r.stderr[-2000:]
     assert res["ranks"] == nranks
