@@ -415,6 +415,9 @@ struct dynohip_solver {
   GraphCopy graph;
   bool has_graph = false;
   bool has_plan = false;
+  // the plan's factor records (measurements, 1/sigma, Huber k) predate the
+  // current graph, whose structure (factor keys per type) is the plan's
+  bool records_stale = false;
   bool has_values = false;
   std::vector<uint64_t> value_keys;
   Plan plan;
@@ -1355,11 +1358,19 @@ int dynohip_set_graph(dynohip_solver* s, const dynohip_graph_view* g) {
       return set_err(s, DYNOHIP_EINVAL, "factor type %d: null keys/sigmas/measured", t);
   // copied into the handle's arrays (their capacity is reused across graphs)
   GraphCopy& gc = s->graph;
+  // A graph with the current plan's structure (the same factor keys per
+  // type, in order) keeps the plan: ordering, schedule and gather lists are
+  // functions of the keys alone, and set_values then only refreshes the
+  // factor records. Compared exactly (no hash to collide).
+  bool same_structure = s->has_graph && s->has_plan && s->nranks == 1;
+  for (int t = 0; t < kNTypes && same_structure; ++t)
+    same_structure = gc.n[t] == b[t]->n &&
+                     std::equal(gc.keys[t].begin(), gc.keys[t].end(), b[t]->keys);
   s->has_graph = false;
   for (int t = 0; t < kNTypes; ++t) {
     const size_t n = b[t]->n;
     gc.n[t] = n;
-    gc.keys[t].assign(b[t]->keys, b[t]->keys + n * kNKeys[t]);
+    if (!same_structure) gc.keys[t].assign(b[t]->keys, b[t]->keys + n * kNKeys[t]);
     if (kMeasDim[t] && n) gc.meas[t].assign(b[t]->measured, b[t]->measured + n * kMeasDim[t]);
     else gc.meas[t].clear();
     gc.sig[t].assign(b[t]->sigmas, b[t]->sigmas + n * kDim[t]);
@@ -1368,7 +1379,8 @@ int dynohip_set_graph(dynohip_solver* s, const dynohip_graph_view* g) {
   }
   s->has_graph = true;
   s->lin_valid = false;
-  s->has_plan = false;
+  s->has_plan = same_structure;
+  s->records_stale = same_structure;
   s->has_values = false;
   s->error_fresh = false;
   return DYNOHIP_OK;
@@ -1407,6 +1419,41 @@ struct EarlyUpload : PlanHook {
   hipError_t err = hipSuccess;
   bool done = false;
 };
+
+// The factor records of a kept plan, from the current graph: the same
+// checks and the same layout as build_plan's (plan.cpp, factor types).
+int refresh_records(dynohip_solver* s) {
+  Plan& P = s->plan;
+  const GraphCopy& gc = s->graph;
+  Uploads up;
+  for (int t = 0; t < kNTypes; ++t) {
+    TypePlan& tp = P.types[t];
+    const size_t n = gc.n[t];
+    const std::vector<double>& sig = gc.sig[t];
+    const std::vector<double>& meas = gc.meas[t];
+    for (size_t i = 0; i < n * kDim[t]; ++i)
+      if (!(sig[i] > 0.0 && std::isfinite(sig[i]))) return set_err(s, DYNOHIP_EINVAL, "non-positive sigma");
+    for (size_t i = 0; i < n * kMeasDim[t]; ++i)
+      if (!std::isfinite(meas[i])) return set_err(s, DYNOHIP_ENONFINITE, "non-finite measurement");
+    tp.meas.assign(meas.begin(), meas.end());
+    tp.isig.resize(sig.size());
+    for (size_t i = 0; i < sig.size(); ++i) tp.isig[i] = 1.0 / sig[i];
+    tp.hk.assign(gc.hub[t].begin(), gc.hub[t].end());
+    hipError_t e;
+    if ((e = up.add(s->tb[t].meas, tp.meas)) != hipSuccess || (e = up.add(s->tb[t].isig, tp.isig)) != hipSuccess ||
+        (e = up.add(s->tb[t].hk, tp.hk)) != hipSuccess)
+      return set_err(s, DYNOHIP_EHIP, "HIP error %d (%s) in the factor record upload", static_cast<int>(e),
+                     hipGetErrorString(e));
+  }
+  const hipError_t e = up.run(s->stage[0], s->stage_cap[0], s->dstage[0], s->stream, false);
+  if (e != hipSuccess)
+    return set_err(s, DYNOHIP_EHIP, "HIP error %d (%s) in the factor record upload", static_cast<int>(e),
+                   hipGetErrorString(e));
+  HIPCHK(s, hipStreamSynchronize(s->stream));   // the staging buffer is reused
+  s->records_stale = false;
+  s->base_stats_valid = false;
+  return DYNOHIP_OK;
+}
 
 int dynohip_set_values(dynohip_solver* s, const uint64_t* keys, const uint8_t* kind, const double* data, size_t n) {
   if (!s || (n && (!keys || !kind || !data))) return DYNOHIP_EINVAL;
@@ -1460,8 +1507,16 @@ int dynohip_set_values(dynohip_solver* s, const uint64_t* keys, const uint8_t* k
     s->value_keys.assign(keys, keys + n);
     s->value_kind.assign(kind, kind + n);
     s->has_plan = true;
+    s->records_stale = false;
     ++s->plan_gen;   // a snapshot of the previous graph's values no longer applies
     s->base_stats_valid = false;
+  } else if (s->records_stale) {
+    // the plan kept by set_graph: the speculative linearisation of the last
+    // try may still read the records being replaced
+    HIPCHK(s, hipStreamSynchronize(s->stream));
+    const int rc = refresh_records(s);
+    if (rc) return rc;
+    ++s->plan_gen;
   }
   s->lin_valid = false;
   static const bool vtiming = std::getenv("DYNOHIP_PLAN_TIMING") != nullptr;

@@ -172,7 +172,11 @@ int dynohip_pool_trim(void);
 const char* dynohip_last_error(const dynohip_solver* s);
 
 /* Upload the graph (structure + measurements). Builds all index structures
-   (point chains, frame-ordered reduced pose system, gather lists). */
+   (point chains, frame-ordered reduced pose system, gather lists). A graph
+   whose factor keys per type (in order) equal the current plan's, on a
+   single-GPU handle, keeps that plan: the next dynohip_set_values with the
+   same value keys only refreshes the factor records (measurements, sigmas,
+   Huber k), with the same checks. Results are identical to a fresh plan's. */
 int dynohip_set_graph(dynohip_solver* s, const dynohip_graph_view* g);
 
 /* Upload values (gtsam::Values): n entries, kind[i] in {POSE3, POINT3};
