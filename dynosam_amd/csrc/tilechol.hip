@@ -465,6 +465,7 @@ __device__ __forceinline__ void lds_flag_set(int* f, int v) {
 // otherwise duplicate the code around every inlined spin loop).
 __device__ __forceinline__ void lds_flag_wait(const int* f, int v) {
   const unsigned a = static_cast<unsigned>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const int*)f));
+  const int vs = __builtin_amdgcn_readfirstlane(v);   // (wave-uniform; an SGPR operand)
   int t;
   int st;
   asm volatile(
@@ -475,7 +476,7 @@ __device__ __forceinline__ void lds_flag_wait(const int* f, int v) {
       "s_cmp_lg_u32 %1, %3\n\t"
       "s_cbranch_scc1 1b"
       : "=&v"(t), "=&s"(st)
-      : "v"(a), "s"(v)
+      : "v"(a), "s"(vs)
       : "memory", "scc");
 }
 

@@ -198,3 +198,56 @@ extern "C" int probe_run(int variant, const double* Bh, double* Wh, unsigned lon
   (void)hipFree(c);
   return 0;
 }
+
+// f64 MFMA rate: cycles per v_mfma_f64_16x16x4f64 on one wave, (0) four
+// independent accumulator chains fed from registers, (1) the same with the
+// operands read from an LDS tile of row stride 68 doubles (as pend_block),
+// (2) one dependent chain from registers
+template <int V>
+__global__ __launch_bounds__(64) void k_mfma_rate(const double* __restrict__ in, double* __restrict__ out,
+                                                  unsigned long long* __restrict__ cyc, int reps) {
+  __shared__ double P[64 * 68];
+  const int l = threadIdx.x, li = l & 15, lk = l >> 4;
+  for (int i = l; i < 64 * 68; i += 64) P[i] = in[i % 256];
+  __syncthreads();
+  v4d c[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) c[s] = v4d{0.0, 0.0, 0.0, 0.0};
+  double a = in[l], b = in[64 + l];
+  unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  for (int it = 0; it < reps; ++it) {
+#pragma unroll
+    for (int K = 0; K < 4; ++K)
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        if constexpr (V == 1) {
+          a = -P[li * 68 + 16 * K + 4 * s4 + lk];
+          b = P[(16 + li) * 68 + 16 * K + 4 * s4 + lk];
+        }
+        if constexpr (V == 2) c[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c[0], 0, 0, 0);
+        else c[s4] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c[s4], 0, 0, 0);
+      }
+    asm volatile("" : "+v"(a), "+v"(b));
+  }
+  v4d tot = (c[0] + c[1]) + (c[2] + c[3]);
+  unsigned long long t1 = __builtin_amdgcn_s_memtime();
+#pragma unroll
+  for (int r = 0; r < 4; ++r) out[r * 64 + l] = tot[r];
+  if (l == 0) cyc[0] = t1 - t0;
+}
+
+extern "C" int probe_mfma(int variant, const double* inh, unsigned long long* cyc, int reps) {
+  double *in, *out;
+  unsigned long long* c;
+  if (hipMalloc(&in, 256 * 8) || hipMalloc(&out, 256 * 8) || hipMalloc(&c, 16)) return -1;
+  (void)hipMemcpy(in, inh, 256 * 8, hipMemcpyHostToDevice);
+  if (variant == 0) k_mfma_rate<0><<<1, 64>>>(in, out, c, reps);
+  else if (variant == 1) k_mfma_rate<1><<<1, 64>>>(in, out, c, reps);
+  else k_mfma_rate<2><<<1, 64>>>(in, out, c, reps);
+  if (hipDeviceSynchronize() != hipSuccess) return -2;
+  (void)hipMemcpy(cyc, c, 8, hipMemcpyDeviceToHost);
+  (void)hipFree(in);
+  (void)hipFree(out);
+  (void)hipFree(c);
+  return 0;
+}

@@ -1,5 +1,7 @@
 """Cycles per pivot of the in-wave 16x16 factorisation (f16wave.h) on the
-GPU, and the accuracy of W = U^-1 against numpy: tools/pivot_probe.hip.
+GPU, and the accuracy of W = U^-1 against numpy; and the issue rate of
+v_mfma_f64_16x16x4f64 on one wave (registers / LDS operands, four chains /
+one): tools/pivot_probe.hip.
 Usage: python tools/pivot_probe.py [reps]"""
 import ctypes as C
 import os
@@ -35,6 +37,12 @@ def main():
     ex = 1.0 / x
     ulp = np.abs(y - ex) / np.spacing(ex)
     print(f"v_rcp_f64: max {ulp.max():.3g} ulp, mean {ulp.mean():.3g}, exact {np.mean(y == ex) * 100:.1f} %")
+    L.probe_mfma.argtypes = [C.c_int, P, C.POINTER(C.c_ulonglong), C.c_int]
+    xin = rng.normal(size=256)
+    for v, what in ((0, "4 chains, registers"), (1, "4 chains, LDS operands (stride 68)"), (2, "1 chain, registers")):
+        cyc = (C.c_ulonglong * 1)()
+        assert L.probe_mfma(v, xin.ctypes.data_as(P), cyc, 200) == 0
+        print(f"v_mfma_f64_16x16x4f64 {what}: {cyc[0] / (200 * 16):.1f} cycles each")
     for cond in (1e2, 1e8, 1e14):
         Q, _ = np.linalg.qr(rng.normal(size=(16, 16)))
         B = (Q * np.logspace(0, -np.log10(cond), 16)) @ Q.T

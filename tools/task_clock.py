@@ -103,7 +103,13 @@ def main():
     dchain.reverse()
     out["dep_chain"] = [{"q": int(q), "kind": int(kind[q]), "k": int(kk[q]), "i": int(ii[q]),
                          "pick": float(t[0, q]), "ready": float(ready[q]), "deps_met": float(t[1, q]),
-                         "end": float(t[4, q])} for q in dchain]
+                         "end": float(t[4, q]),
+                         # a panel on the chain, from its predecessor's end: operands
+                         # and right-hand side in (late wait included), tiles in LDS,
+                         # pending diagonal block, factorisation, TRSM + stores
+                         **({"to_loaded": float(sub[0, q] - ready[q]), "to_lds": float(sub[1, q] - sub[0, q]),
+                             "pend": float(t[2, q] - sub[1, q]), "fac": float(t[3, q] - t[2, q]),
+                             "post": float(t[4, q] - t[3, q])} if kind[q] == 0 else {})} for q in dchain]
     # chain ending last
     chain = []
     cur = int(np.argmax(t[4]))
