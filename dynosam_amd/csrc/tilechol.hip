@@ -54,18 +54,36 @@ __device__ __forceinline__ void zero_acc(v4d acc[2][2]) {
 }
 
 // acc += A B^T
+// The k order of the 64-deep LDS-operand products: in k-block K (16 wide)
+// the s-th MFMA of lane group lk = l >> 4 takes k = 16K + 4 lk + s, so a
+// lane's four operands of a k-block are contiguous and come in two 16-byte
+// reads (ds_read_b128) instead of four 8-byte ones; both operands of a
+// product use the same order. (tools/pivot_probe: 98 instead of 123 cycles
+// per f64 MFMA fed from LDS.)
+typedef double d2v __attribute__((ext_vector_type(2)));
+struct Kq {
+  d2v lo, hi;
+  __device__ __forceinline__ double operator[](int s) const { return s < 2 ? lo[s] : hi[s - 2]; }
+};
+__device__ __forceinline__ Kq ld_kq(const double* row, int K, int lk) {
+  const d2v* p = reinterpret_cast<const d2v*>(row + 16 * K + 4 * lk);
+  return Kq{p[0], p[1]};
+}
+
 __device__ __forceinline__ void mfma_abt_acc(const double* As, const double* Bs, int wave, int lane, v4d acc[2][2]) {
   const int i0 = 32 * (wave >> 1), j0 = 32 * (wave & 1);
   const int li = lane & 15, lk = lane >> 4;
-#pragma unroll 4
-  for (int k0 = 0; k0 < T; k0 += 4) {
-    const int k = k0 + lk;
-    const double a0 = As[(i0 + li) * LD + k], a1 = As[(i0 + 16 + li) * LD + k];
-    const double b0 = Bs[(j0 + li) * LD + k], b1 = Bs[(j0 + 16 + li) * LD + k];
-    acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
-    acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
-    acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
-    acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+#pragma unroll
+  for (int K = 0; K < 4; ++K) {
+    const Kq a0 = ld_kq(As + (i0 + li) * LD, K, lk), a1 = ld_kq(As + (i0 + 16 + li) * LD, K, lk);
+    const Kq b0 = ld_kq(Bs + (j0 + li) * LD, K, lk), b1 = ld_kq(Bs + (j0 + 16 + li) * LD, K, lk);
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[s4], b0[s4], acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[s4], b1[s4], acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[s4], b0[s4], acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[s4], b1[s4], acc[1][1], 0, 0, 0);
+    }
   }
 }
 
@@ -253,7 +271,6 @@ __device__ __forceinline__ bool factor_tile_blk(v4d (&accA)[4], v4d (&accX)[4], 
 // slot's write counter is bumped, and every load of such data is an sc1 load
 // (16-byte buffer loads for whole tiles, 8-byte atomic loads otherwise), so
 // no acquire fence is needed.
-typedef double d2v __attribute__((ext_vector_type(2)));
 
 template <bool SC1>
 __device__ __forceinline__ double gld(const double* p) {
@@ -425,12 +442,17 @@ __device__ __forceinline__ void run_update(const TileDev& b, const TileTask& tk,
 // A_kk -= L(k,c) L(k,c)^T on this wave's upper blocks (w, TJ >= w), K = 64
 __device__ __forceinline__ void diag_pending(v4d (&accA)[4], const double* Ps, int w, int l) {
   const int li = l & 15, lk = l >> 4;
-#pragma unroll 4
-  for (int k0 = 0; k0 < T; k0 += 4) {
-    const double a = -Ps[(16 * w + li) * LD + k0 + lk];
+#pragma unroll
+  for (int K = 0; K < 4; ++K) {
+    const Kq a = ld_kq(Ps + (16 * w + li) * LD, K, lk);
 #pragma unroll
     for (int TJ = 0; TJ < 4; ++TJ)
-      if (TJ >= w) accA[TJ] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Ps[(16 * TJ + li) * LD + k0 + lk], accA[TJ], 0, 0, 0);
+      if (TJ >= w) {
+        const Kq bq = ld_kq(Ps + (16 * TJ + li) * LD, K, lk);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+          accA[TJ] = __builtin_amdgcn_mfma_f64_16x16x4f64(-a[s4], bq[s4], accA[TJ], 0, 0, 0);
+      }
   }
 }
 
@@ -527,11 +549,11 @@ __device__ __forceinline__ v4d pend_block(v4d acc, const double* Ps, int bi, int
 #pragma unroll
   for (int s4 = 0; s4 < 4; ++s4) c[s4] = v4d{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-  for (int k0 = 0; k0 < T; k0 += 16)
+  for (int K = 0; K < 4; ++K) {
+    const Kq a = ld_kq(Ps + (16 * bi + li) * LD, K, lk), bq = ld_kq(Ps + (16 * bj + li) * LD, K, lk);
 #pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4)
-      c[s4] = __builtin_amdgcn_mfma_f64_16x16x4f64(-Ps[(16 * bi + li) * LD + k0 + 4 * s4 + lk],
-                                                   Ps[(16 * bj + li) * LD + k0 + 4 * s4 + lk], c[s4], 0, 0, 0);
+    for (int s4 = 0; s4 < 4; ++s4) c[s4] = __builtin_amdgcn_mfma_f64_16x16x4f64(-a[s4], bq[s4], c[s4], 0, 0, 0);
+  }
   return acc + ((c[0] + c[1]) + (c[2] + c[3]));
 }
 
@@ -863,11 +885,11 @@ __device__ __forceinline__ void panel_task(const TileDev& b, const TileTask& tk,
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4) ao[s4] = v4d{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int k0 = 0; k0 < T; k0 += 16)
+      for (int K = 0; K < 4; ++K) {
+        const Kq a = ld_kq(Qs + (16 * w + li) * LD, K, lk), bq = ld_kq(Rop + (16 * c + li) * LD, K, lk);
 #pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4)
-          ao[s4] = __builtin_amdgcn_mfma_f64_16x16x4f64(Qs[(16 * w + li) * LD + k0 + 4 * s4 + lk],
-                                                        Rop[(16 * c + li) * LD + k0 + 4 * s4 + lk], ao[s4], 0, 0, 0);
+        for (int s4 = 0; s4 < 4; ++s4) ao[s4] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s4], bq[s4], ao[s4], 0, 0, 0);
+      }
       const v4d tot = (ao[0] + ao[1]) + (ao[2] + ao[3]);
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) As[ACC_ROW(w, l, rr) * LD + ACC_COL(c, l)] -= tot[rr];

@@ -199,10 +199,13 @@ extern "C" int probe_run(int variant, const double* Bh, double* Wh, unsigned lon
   return 0;
 }
 
+typedef double d2v __attribute__((ext_vector_type(2)));
+
 // f64 MFMA rate: cycles per v_mfma_f64_16x16x4f64 on one wave, (0) four
 // independent accumulator chains fed from registers, (1) the same with the
 // operands read from an LDS tile of row stride 68 doubles (as pend_block),
-// (2) one dependent chain from registers
+// (2) one dependent chain from registers, (3) as (1) with each lane's four
+// k-steps of a 16-wide k-block consecutive (two 16-byte reads per operand)
 template <int V>
 __global__ __launch_bounds__(64) void k_mfma_rate(const double* __restrict__ in, double* __restrict__ out,
                                                   unsigned long long* __restrict__ cyc, int reps) {
@@ -214,6 +217,7 @@ __global__ __launch_bounds__(64) void k_mfma_rate(const double* __restrict__ in,
 #pragma unroll
   for (int s = 0; s < 4; ++s) c[s] = v4d{0.0, 0.0, 0.0, 0.0};
   double a = in[l], b = in[64 + l];
+  d2v qa0, qa1, qb0, qb1;
   unsigned long long t0 = __builtin_amdgcn_s_memtime();
   for (int it = 0; it < reps; ++it) {
 #pragma unroll
@@ -223,6 +227,15 @@ __global__ __launch_bounds__(64) void k_mfma_rate(const double* __restrict__ in,
         if constexpr (V == 1) {
           a = -P[li * 68 + 16 * K + 4 * s4 + lk];
           b = P[(16 + li) * 68 + 16 * K + 4 * s4 + lk];
+        }
+        if constexpr (V == 3) {   // lane lk takes the four consecutive k of its quarter: 16-byte reads
+          if (s4 == 0) {
+            const d2v* pa = reinterpret_cast<const d2v*>(P + li * 68 + 16 * K + 4 * lk);
+            const d2v* pb = reinterpret_cast<const d2v*>(P + (16 + li) * 68 + 16 * K + 4 * lk);
+            qa0 = pa[0]; qa1 = pa[1]; qb0 = pb[0]; qb1 = pb[1];
+          }
+          a = -(s4 < 2 ? qa0[s4] : qa1[s4 - 2]);
+          b = s4 < 2 ? qb0[s4] : qb1[s4 - 2];
         }
         if constexpr (V == 2) c[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c[0], 0, 0, 0);
         else c[s4] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c[s4], 0, 0, 0);
@@ -243,7 +256,8 @@ extern "C" int probe_mfma(int variant, const double* inh, unsigned long long* cy
   (void)hipMemcpy(in, inh, 256 * 8, hipMemcpyHostToDevice);
   if (variant == 0) k_mfma_rate<0><<<1, 64>>>(in, out, c, reps);
   else if (variant == 1) k_mfma_rate<1><<<1, 64>>>(in, out, c, reps);
-  else k_mfma_rate<2><<<1, 64>>>(in, out, c, reps);
+  else if (variant == 2) k_mfma_rate<2><<<1, 64>>>(in, out, c, reps);
+  else k_mfma_rate<3><<<1, 64>>>(in, out, c, reps);
   if (hipDeviceSynchronize() != hipSuccess) return -2;
   (void)hipMemcpy(cyc, c, 8, hipMemcpyDeviceToHost);
   (void)hipFree(in);
