@@ -77,13 +77,16 @@ __device__ __forceinline__ void mfma_abt_acc(const double* As, const double* Bs,
   for (int K = 0; K < 4; ++K) {
     const Kq a0 = ld_kq(As + (i0 + li) * LD, K, lk), a1 = ld_kq(As + (i0 + 16 + li) * LD, K, lk);
     const Kq b0 = ld_kq(Bs + (j0 + li) * LD, K, lk), b1 = ld_kq(Bs + (j0 + 16 + li) * LD, K, lk);
+    // (each accumulator's four k-steps back to back: consecutive f64 MFMAs
+    // on one accumulator issue faster than rotating over four)
 #pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4) {
-      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[s4], b0[s4], acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[s4], b1[s4], acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[s4], b0[s4], acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[s4], b1[s4], acc[1][1], 0, 0, 0);
-    }
+    for (int s4 = 0; s4 < 4; ++s4) acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[s4], b0[s4], acc[0][0], 0, 0, 0);
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[s4], b1[s4], acc[0][1], 0, 0, 0);
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[s4], b0[s4], acc[1][0], 0, 0, 0);
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[s4], b1[s4], acc[1][1], 0, 0, 0);
   }
 }
 
@@ -540,21 +543,18 @@ __device__ __forceinline__ PanelPre panel_prefetch(const TileDev& b, const TileT
 
 // acc += -P_bi P_bj^T for 16x16 blocks (bi, bj) of a 64x64 LDS operand P,
 // in accumulator layout (the pending update of diagonal block (bi, bj)).
-// Four independent accumulator chains (k-steps s mod 4) keep the MFMA pipe
-// busy instead of waiting on one dependent chain of 16; summed in a fixed
-// order.
 __device__ __forceinline__ v4d pend_block(v4d acc, const double* Ps, int bi, int bj, int l) {
   const int li = l & 15, lk = l >> 4;
-  v4d c[4];
-#pragma unroll
-  for (int s4 = 0; s4 < 4; ++s4) c[s4] = v4d{0.0, 0.0, 0.0, 0.0};
+  // one accumulator chain (tools/pivot_probe: 86 cycles per LDS-fed f64
+  // MFMA against 99 rotating over four)
+  v4d c = v4d{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
   for (int K = 0; K < 4; ++K) {
     const Kq a = ld_kq(Ps + (16 * bi + li) * LD, K, lk), bq = ld_kq(Ps + (16 * bj + li) * LD, K, lk);
 #pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4) c[s4] = __builtin_amdgcn_mfma_f64_16x16x4f64(-a[s4], bq[s4], c[s4], 0, 0, 0);
+    for (int s4 = 0; s4 < 4; ++s4) c = __builtin_amdgcn_mfma_f64_16x16x4f64(-a[s4], bq[s4], c, 0, 0, 0);
   }
-  return acc + ((c[0] + c[1]) + (c[2] + c[3]));
+  return acc + c;
 }
 
 // sum over the 16 lanes of a row group (lanes with equal l >> 4), with DPP
@@ -881,16 +881,13 @@ __device__ __forceinline__ void panel_task(const TileDev& b, const TileTask& tk,
     const double* Rop = p.rb == p.qa ? Qs : Ps;
     auto chunk = [&](int c) {   // As(w, c) -= Q(w, :) R(c, :)^T, all 64 k in order
       if (!op) return;
-      v4d ao[4];   // four independent chains (k-steps s mod 4), summed in order
-#pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) ao[s4] = v4d{0.0, 0.0, 0.0, 0.0};
+      v4d tot = v4d{0.0, 0.0, 0.0, 0.0};   // one accumulator chain (as pend_block)
 #pragma unroll
       for (int K = 0; K < 4; ++K) {
         const Kq a = ld_kq(Qs + (16 * w + li) * LD, K, lk), bq = ld_kq(Rop + (16 * c + li) * LD, K, lk);
 #pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) ao[s4] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s4], bq[s4], ao[s4], 0, 0, 0);
+        for (int s4 = 0; s4 < 4; ++s4) tot = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s4], bq[s4], tot, 0, 0, 0);
       }
-      const v4d tot = (ao[0] + ao[1]) + (ao[2] + ao[3]);
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) As[ACC_ROW(w, l, rr) * LD + ACC_COL(c, l)] -= tot[rr];
     };

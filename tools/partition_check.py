@@ -25,7 +25,9 @@ graph on rank 0:
   that drift for a pure reordering.
 
 Prints one JSON line (rank 0); exit code 1 when the conditioned comparison
-misses --tol or the free run changes iteration counts / accept sequence.
+misses --tol or the free run leaves the single handle's iteration counts /
+accept sequence for ones the control's reordering does not produce either
+(or its final error leaves that spread).
 """
 import argparse
 import json
@@ -129,8 +131,18 @@ def main():
                             for a, b in zip(a_tr[:n], b_tr[:n]) if np.isfinite(b["new_error"]) and b["accepted"]),
                            default=0.0)
 
-            same_acc = [a["accepted"] for a in trace] == [b["accepted"] for b in rtrace]
-            ok_free = sp.iterations == sr.iterations and sp.inner_iterations == sr.inner_iterations and same_acc
+            acc_p = [a["accepted"] for a in trace]
+            same_acc = acc_p == [b["accepted"] for b in rtrace]
+            # the partitioned run takes the single handle's counts and accept
+            # sequence, or the control's: on an ill-conditioned graph a pure
+            # reordering of the same arithmetic moves them too (C5: 31 / 32
+            # iterations), and then its final error lies within that spread
+            counts = (sp.iterations, sp.inner_iterations)
+            counts_ok = counts in ((sr.iterations, sr.inner_iterations), (sc.iterations, sc.inner_iterations))
+            acc_ok = same_acc or acc_p == [c["accepted"] for c in ctrace]
+            err_ok = abs(sp.final_error - sr.final_error) <= max(1e-6 * abs(sr.final_error),
+                                                                 2.0 * abs(sc.final_error - sr.final_error))
+            ok_free = counts_ok and acc_ok and err_ok
             res["free"] = {
                 "iterations": [sp.iterations, sr.iterations, sc.iterations],
                 "inner": [sp.inner_iterations, sr.inner_iterations, sc.inner_iterations],

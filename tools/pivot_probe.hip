@@ -205,7 +205,8 @@ typedef double d2v __attribute__((ext_vector_type(2)));
 // independent accumulator chains fed from registers, (1) the same with the
 // operands read from an LDS tile of row stride 68 doubles (as pend_block),
 // (2) one dependent chain from registers, (3) as (1) with each lane's four
-// k-steps of a 16-wide k-block consecutive (two 16-byte reads per operand)
+// k-steps of a 16-wide k-block consecutive (two 16-byte reads per operand),
+// (4) / (5) as (3) with one / two accumulator chains
 template <int V>
 __global__ __launch_bounds__(64) void k_mfma_rate(const double* __restrict__ in, double* __restrict__ out,
                                                   unsigned long long* __restrict__ cyc, int reps) {
@@ -228,7 +229,7 @@ __global__ __launch_bounds__(64) void k_mfma_rate(const double* __restrict__ in,
           a = -P[li * 68 + 16 * K + 4 * s4 + lk];
           b = P[(16 + li) * 68 + 16 * K + 4 * s4 + lk];
         }
-        if constexpr (V == 3) {   // lane lk takes the four consecutive k of its quarter: 16-byte reads
+        if constexpr (V >= 3) {   // lane lk takes the four consecutive k of its quarter: 16-byte reads
           if (s4 == 0) {
             const d2v* pa = reinterpret_cast<const d2v*>(P + li * 68 + 16 * K + 4 * lk);
             const d2v* pb = reinterpret_cast<const d2v*>(P + (16 + li) * 68 + 16 * K + 4 * lk);
@@ -237,7 +238,8 @@ __global__ __launch_bounds__(64) void k_mfma_rate(const double* __restrict__ in,
           a = -(s4 < 2 ? qa0[s4] : qa1[s4 - 2]);
           b = s4 < 2 ? qb0[s4] : qb1[s4 - 2];
         }
-        if constexpr (V == 2) c[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c[0], 0, 0, 0);
+        if constexpr (V == 2 || V == 4) c[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c[0], 0, 0, 0);
+        else if constexpr (V == 5) c[s4 & 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c[s4 & 1], 0, 0, 0);
         else c[s4] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c[s4], 0, 0, 0);
       }
     asm volatile("" : "+v"(a), "+v"(b));
@@ -257,7 +259,9 @@ extern "C" int probe_mfma(int variant, const double* inh, unsigned long long* cy
   if (variant == 0) k_mfma_rate<0><<<1, 64>>>(in, out, c, reps);
   else if (variant == 1) k_mfma_rate<1><<<1, 64>>>(in, out, c, reps);
   else if (variant == 2) k_mfma_rate<2><<<1, 64>>>(in, out, c, reps);
-  else k_mfma_rate<3><<<1, 64>>>(in, out, c, reps);
+  else if (variant == 3) k_mfma_rate<3><<<1, 64>>>(in, out, c, reps);
+  else if (variant == 4) k_mfma_rate<4><<<1, 64>>>(in, out, c, reps);
+  else k_mfma_rate<5><<<1, 64>>>(in, out, c, reps);
   if (hipDeviceSynchronize() != hipSuccess) return -2;
   (void)hipMemcpy(cyc, c, 8, hipMemcpyDeviceToHost);
   (void)hipFree(in);

@@ -40,7 +40,8 @@ def main():
     L.probe_mfma.argtypes = [C.c_int, P, C.POINTER(C.c_ulonglong), C.c_int]
     xin = rng.normal(size=256)
     for v, what in ((0, "4 chains, registers"), (1, "4 chains, LDS operands (stride 68)"), (2, "1 chain, registers"),
-                      (3, "4 chains, LDS operands, 16-byte reads")):
+                      (3, "4 chains, LDS operands, 16-byte reads"), (4, "1 chain, LDS operands, 16-byte reads"),
+                      (5, "2 chains, LDS operands, 16-byte reads")):
         cyc = (C.c_ulonglong * 1)()
         assert L.probe_mfma(v, xin.ctypes.data_as(P), cyc, 200) == 0
         print(f"v_mfma_f64_16x16x4f64 {what}: {cyc[0] / (200 * 16):.1f} cycles each")
