@@ -258,7 +258,14 @@ void launch_tile_forward(const TileDev& b, const TileSchedDev& sd, const std::ve
 // the whole reduced solve of a system of <= kSmallNT tiles in one workgroup
 // (x = A^-1 r in natural tile order; tilechol.hip k_small_solve)
 constexpr int kSmallNT = 4;
-void launch_small_solve(const TileDev& b, const double* r, double* x, int* fail, hipStream_t s);
+// the small solve's view of the tiles: the tile at each elimination position
+// and the slot of position block (p, q), p <= q (-1: no stored tile); filled
+// on the host from the plan, so the kernel starts with no index round trips
+struct SmallMap {
+  int32_t ord[kSmallNT];
+  int32_t slot[kSmallNT][kSmallNT];
+};
+void launch_small_solve(const TileDev& b, const SmallMap& m, const double* r, double* x, int* fail, hipStream_t s);
 // sentinel_filled: x and sd.partials hold kBackSentinel for this solve (the
 // hand-off form k_back_poll needs it; without it the flag form runs)
 void launch_tile_backward(const TileDev& b, const TileSchedDev& sd, const std::vector<int32_t>& blevel,

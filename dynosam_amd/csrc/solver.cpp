@@ -443,9 +443,10 @@ struct dynohip_solver {
   LoneSchurDev ld;
   DevBuf<double> slots, gred, xy, dpt, linv, contrib;
   DevBuf<int32_t> tile_pos, row_start, row_col, row_slot, bent, pairs;
+  SmallMap smap{};  // the small solve's tile map (plans of <= kSmallNT tiles)
   DevBuf<TileTask> ftask;
   DevBuf<BackPart> bpart;
-  bool small_solve = false; // DYNOHIP_SMALL_SOLVE=1: systems of <= kSmallNT tiles in one workgroup (slower)
+  bool small_solve = false; // DYNOHIP_SMALL_SOLVE=1: systems of <= kSmallNT tiles in one workgroup (at par with the DAG)
   DevBuf<double> bpartials;
   DevBuf<int> arrive;
   DevBuf<int32_t> fdep_start, fdep, fqueue;
@@ -696,6 +697,18 @@ int upload_plan(dynohip_solver* s, bool types_done = false) {
   b.row_start = s->row_start.p;
   b.row_col = s->row_col.p;
   b.row_slot = s->row_slot.p;
+  if (P.NT >= 1 && P.NT <= kSmallNT) {
+    SmallMap& m = s->smap;
+    for (int t = 0; t < P.NT; ++t) m.ord[P.tile_pos[t]] = t;
+    for (int p = 0; p < P.NT; ++p)
+      for (int q = 0; q < P.NT; ++q) {
+        int32_t sl = -1;
+        if (p <= q)
+          for (int e = P.row_start[m.ord[q]]; e < P.row_start[m.ord[q] + 1]; ++e)
+            if (P.row_col[e] == m.ord[p]) sl = P.row_slot[e];
+        m.slot[p][q] = sl;
+      }
+  }
   s->sd.ftask = s->ftask.p;
   s->sd.pairs = s->pairs.p;
   s->sd.bpart = s->bpart.p;
@@ -935,7 +948,7 @@ int enqueue_try(dynohip_solver* s, double lambda) {
   } else if (s->small_solve && P.NT >= 1 && P.NT <= kSmallNT) {
     // a window-sized system: factorisation and both substitutions in one
     // workgroup (k_small_solve; ms_cholesky spans all of it)
-    launch_small_solve(s->bd, s->gred.p, x, s->failp, st);
+    launch_small_solve(s->bd, s->smap, s->gred.p, x, s->failp, st);
     if (timed) (void)hipEventRecord(s->ev[5], st);
   } else {
     launch_tile_forward(s->bd, s->sd, P.flevel, P.fpanels, s->linv.p, s->gred.p, s->contrib.p, y, s->failp, st,

@@ -1413,230 +1413,402 @@ __global__ __launch_bounds__(kBackThreads) void k_back_poll(TileDev b, const Bac
   if (tid == 0 && bad) atomicOr(fail, 2);
 }
 
-// ---- small reduced systems (<= kSmallNT tiles): one workgroup ------------
+// ---- small reduced systems (<= kSmallNT tiles): one workgroup, dataflow ---
 // The sliding-window solves (backend.flags: 10-frame windows) have reduced
-// systems of at most four tiles, where the tile DAG is a chain of four
-// dependent panels with a global-memory hand-off between each, and the
-// backward substitution four more. k_small_solve does the whole solve in
-// one workgroup of 8 waves instead, the matrix resident in registers:
-//   * the position-ordered matrix as 16x16 blocks in MFMA accumulator
-//     layout (upper triangle, A = U^T U): wave w holds diagonal blocks
-//     w and w + 8 and 15 off-diagonal blocks (enumerated by row, last row
-//     first, dealt round-robin, so every block step leaves each wave a
-//     similar share of the trailing update);
-//   * block step K: the owner of block (K,K) factors it in-wave
-//     (factor16_wave: U_KK and W = U_KK^-1) and forms y_K = W^T r_K; after a
-//     barrier the owners of row K form U[K][J] = W^T A[K][J] into LDS; after
-//     a second barrier every wave applies A[I][J] -= U[K][I]^T U[K][J] and
-//     r_I -= U[K][I]^T y_K to its blocks. The owner of block K+1 updates it
-//     first and factors it at once, ahead of its other updates (lookahead);
-//   * backward, x_K = W_K (y_K - sum_{J>K} U[K][J] x_J): each product
-//     U[K][J] x_J is formed by the block's owner as soon as x_J is out, and
-//     the owner of block K adds them in J order.
-// The forward substitution is the factorisation's extra right-hand-side
-// column; no L^-1 is stored and the backward substitution needs no other
-// launch. Results match the tile DAG's to rounding (another summation
-// order). Measured on the 10-frame windows (4 tiles): 105 us against the
-// DAG's 61 + 11 us, so it is opt-in (DYNOHIP_SMALL_SOLVE=1): the wave that
-// factors the next block also owns a full share of the trailing update,
-// which sits on every step's critical path.
+// systems of at most four tiles (16 blocks of 16), where the tile DAG is a
+// chain of four dependent panels with a global-memory hand-off between each,
+// and the backward substitution four more. k_small_solve does the whole solve
+// in one workgroup of 16 waves, the position-ordered matrix (upper triangle,
+// A = U^T U) resident in registers as 16x16 blocks in MFMA accumulator layout,
+// the waves handing blocks to each other through LDS flags (no barriers after
+// the first):
+//   * wave 0 factors the diagonal blocks one after the other (factor16: U_KK
+//     and W_K = U_KK^-1), publishes W_K and y_K = W_K^T r_K, then forms the
+//     superdiagonal block U[K][K+1] = W_K^T A[K][K+1] itself and with it the
+//     next diagonal block D(K+1) - U^T U and r_{K+1} - U^T y_K, so the chain
+//     of diagonal blocks never leaves the wave;
+//   * wave J (1..15) keeps D(J), A[J-1][J] and r_J up to date with the steps
+//     before J-1 and hands them to wave 0 after step J-2 (before wave 0 needs
+//     them, while it factors D(J-1));
+//   * the other 105 blocks (I, J >= I+2) are dealt over waves 1..15, seven
+//     each (eight spill registers to scratch); at step K the owners of row K form
+//     U[K][J] = W_K^T A[K][J] into an LDS ring of two rows, and every owner of
+//     a block below takes A[I][J] -= U[K][I]^T U[K][J] as the operands come
+//     out. A ring row is rewritten only once every wave is done with the step
+//     that read it (per-wave progress counters).
+// The forward substitution rides along (r_I updated with the blocks), and the
+// backward substitution x_K = W_K (y_K - sum_{J>K} U[K][J] x_J) uses the U
+// blocks where they were formed: each owner adds U[K][J] x_J to an LDS slot
+// as soon as x_J is out (its blocks in descending J, the order in which the
+// x_J come), and wave 0 sums the slots of row K in J order. Results match the
+// tile DAG's up to the summation order.
+// Measured on the C2 stream's 10-frame windows (four tiles, 95 % of the
+// 16x16 blocks nonzero after fill): 72 us per solve (HIP events) against the
+// DAG's 57 + 13 us, so it stays opt-in (DYNOHIP_SMALL_SOLVE=1). The bound is
+// the one CU's f64 MFMA rate: ~3200 MFMAs at ~100 cycles each per SIMD
+// (unchanged with half the LDS operand reads), the early steps throughput-
+// bound while wave 0 waits for its hand-overs, and the factoring wave slowed
+// from 3.0k to 5-7k cycles per block while the waves on its SIMD issue
+// MFMAs; the backward chain ~1.8k cycles per block (tools/small_clock.py).
 constexpr int kSmallNB = 4 * kSmallNT;   // 16x16 blocks per dimension
-#ifndef DYNOHIP_SMALL_WAVES
-#define DYNOHIP_SMALL_WAVES 8
-#endif
-constexpr int kSmallWaves = DYNOHIP_SMALL_WAVES;
-constexpr int kSmallNOff = kSmallNB * (kSmallNB - 1) / 2;
-constexpr int kSmallOff = (kSmallNOff + kSmallWaves - 1) / kSmallWaves;   // off-diagonal blocks per wave
-constexpr int kSmallD = (kSmallNB + kSmallWaves - 1) / kSmallWaves;        // diagonal blocks per wave
-static_assert(kSmallOff * kSmallWaves >= kSmallNOff && kSmallD <= 2, "the small solve's block deal");
+constexpr int kSW = 16;                  // waves
+constexpr int kSReg = 7;                 // off-band blocks per wave (at most)
+constexpr int kSRing = 2;                // rows of U in flight
+constexpr int kSRow = kSmallNB - 2;      // off-band blocks of a U row (J >= K + 2)
+constexpr int kSStage = 16 * 18;         // a wave's staging rows at the start (in the ring)
+static_assert(kSmallNB == 16, "the small solve's block deal is for 16 blocks");
 
-// off-diagonal block k of the enumeration by row I from the last, then J
-__device__ __forceinline__ void small_off_block(int k, int& I, int& J) {
-  int i = kSmallNB - 2, base = 0;
-  while (k >= base + (kSmallNB - 1 - i)) {
-    base += kSmallNB - 1 - i;
-    --i;
-  }
-  I = i;
-  J = i + 1 + (k - base);
+struct SmallDeal {
+  int8_t I[kSW][kSReg], J[kSW][kSReg];
+};
+// off-band blocks (I, J >= I + 2) by rows, round-robin over the waves (those
+// on wave 0's SIMD, 4, 8 and 12, last in the cycle); each wave's blocks in
+// descending J (then I) order
+constexpr SmallDeal small_deal() {
+  SmallDeal d{};
+  for (int w = 0; w < kSW; ++w)
+    for (int s = 0; s < kSReg; ++s) d.I[w][s] = d.J[w][s] = -1;
+  const int order[15] = {1, 2, 3, 5, 6, 7, 9, 10, 11, 13, 14, 15, 4, 8, 12};
+  int cap[kSW] = {}, cnt[kSW] = {};
+  for (int w = 1; w < kSW; ++w) cap[w] = kSReg;
+  int c = 0;
+  for (int I = 0; I < kSmallNB; ++I)
+    for (int J = I + 2; J < kSmallNB; ++J) {
+      while (cnt[order[c]] >= cap[order[c]]) c = (c + 1) % 15;
+      const int w = order[c];
+      d.I[w][cnt[w]] = static_cast<int8_t>(I);
+      d.J[w][cnt[w]] = static_cast<int8_t>(J);
+      ++cnt[w];
+      c = (c + 1) % 15;
+    }
+  for (int w = 1; w < kSW; ++w)
+    for (int a = 1; a < cnt[w]; ++a)
+      for (int b = a; b > 0; --b) {
+        const bool later = d.J[w][b] > d.J[w][b - 1] || (d.J[w][b] == d.J[w][b - 1] && d.I[w][b] > d.I[w][b - 1]);
+        if (!later) break;
+        const int8_t ti = d.I[w][b], tj = d.J[w][b];
+        d.I[w][b] = d.I[w][b - 1];
+        d.J[w][b] = d.J[w][b - 1];
+        d.I[w][b - 1] = ti;
+        d.J[w][b - 1] = tj;
+      }
+  return d;
+}
+__constant__ SmallDeal kSmallDeal = small_deal();
+
+// a 16x16 block in LDS: every lane's (v0, v1) pair, then every lane's (v2,
+// v3) pair: two conflict-free 16-byte accesses per lane
+typedef double d2s __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void st_b2(double* p, const v4d& v, int l) {
+  reinterpret_cast<d2s*>(p)[l] = d2s{v[0], v[1]};
+  reinterpret_cast<d2s*>(p + 128)[l] = d2s{v[2], v[3]};
+}
+__device__ __forceinline__ v4d ld_b2(const double* p, int l) {
+  const d2s a = reinterpret_cast<const d2s*>(p)[l], b = reinterpret_cast<const d2s*>(p + 128)[l];
+  return v4d{a[0], a[1], b[0], b[1]};
 }
 
-template <int D>
-using small_ic = std::integral_constant<int, D>;
+struct SmallLds {
+  double Ws[kSmallNB][256];            // W_K
+  double Usd[kSmallNB - 1][256];       // U[K][K+1]
+  double ring[kSRing][kSRow][256];     // U[K][J], J >= K + 2, at [K % kSRing][J - K - 2]
+  double hb[2][2][256];                // D(J), A[J-1][J] handed to wave 0 (buffer J & 1)
+  double hr[2][16];                    // r_J handed over
+  double rs[kSmallNB][16];             // r_K (wave 0's, for the column form)
+  double ys[kSmallNB][16];             // y_K
+  double xs[kSmallNB][16];             // x_K
+  double pb[kSmallNB * (kSmallNB - 1) / 2][16];   // U[K][J] x_J, J > K (upper-triangle index)
+  double dscr[16];
+  int wf[kSmallNB], yf[kSmallNB], sf[kSmallNB], xf[kSmallNB], prc[kSmallNB];
+  int uf[kSRing][kSmallNB];
+  int hf[2];
+  int urc[kSRing];                     // blocks published into each ring row (cumulative)
+  int prog[kSW];
+  int abort;
+};
+static_assert(sizeof(SmallLds) <= 160 * 1024, "the small solve's LDS");
+static_assert(kSW * kSStage <= kSRing * kSRow * 256, "the staging rows fit in the ring");
 
-__global__ __launch_bounds__(kSmallWaves * 64) void k_small_solve(TileDev b, const double* __restrict__ r,
-                                                                  double* __restrict__ x, int* fail) {
-  __shared__ double Ws[kSmallNB][256];             // W_K = U_KK^-1 of every block step
-  __shared__ double ys[kSmallNB * 16];             // y
-  __shared__ double Ur[2][kSmallNB + 1][256];      // row K of U (+ y_K at [kSmallNB])
-  __shared__ double dscr[kSmallWaves][16];
-  __shared__ double pb[kSmallNB][kSmallNB][16];    // U[I][J] x_J, I < J
-  __shared__ double xv[kSmallNB * 16];
-  __shared__ double tv[16];
-  __shared__ int ord[kSmallNT];
-  __shared__ int sslot[kSmallNT][kSmallNT];
+// upper-triangle index of (K, J), K < J
+__device__ __forceinline__ int small_ut(int K, int J) { return K * (2 * kSmallNB - K - 1) / 2 + (J - K - 1); }
+
+// The waits of the small solve are bounded: a wait that polls 2^22 times
+// (~0.3 s) without its value sets S.abort, every later wait returns at once,
+// and wave 0 reports the solve as failed (no hang on a broken hand-off).
+constexpr int kSmallPolls = 1 << 22;
+__device__ __forceinline__ int lds_ld(const int* p) {
+  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+__device__ __forceinline__ void small_wait(const int* f, int v, int* abort) {
+  for (int n = 0; n < kSmallPolls; ++n) {
+    if (lds_ld(f) == v) return;
+    __builtin_amdgcn_s_sleep(1);   // (the polls of 15 waves would crowd the LDS)
+    if ((n & 63) == 63 && lds_ld(abort)) return;
+  }
+  lds_flag_set(abort, 1);
+}
+// until each of the 16 waves' progress counters is >= v
+__device__ __forceinline__ void small_wait_prog(const int* prog, int v, int l, int* abort) {
+  for (int n = 0; n < kSmallPolls; ++n) {
+    const int p = __hip_atomic_load(prog + (l & 15), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (__all(p >= v)) return;
+    __builtin_amdgcn_s_sleep(1);
+    if ((n & 63) == 63 && lds_ld(abort)) return;
+  }
+  lds_flag_set(abort, 1);
+}
+// blocks published into ring row K % kSRing up to and including row K
+__device__ __forceinline__ int small_ring_count(int K, int nb) {
+  int c = 0;
+  for (int j = K & 1; j <= K; j += 2) c += max(0, nb - j - 2);
+  return c;
+}
+
+__global__ __launch_bounds__(kSW * 64) void k_small_solve(TileDev b, SmallMap m, const double* __restrict__ r,
+                                                          double* __restrict__ x, int* fail) {
+  __shared__ __attribute__((aligned(16))) SmallLds S;
   const int tid = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6), l = tid & 63;
   const int NT = b.NT, nb = 4 * NT;
   const int li = l & 15, g = l >> 4;
-  if (tid < NT) ord[b.pos[tid]] = tid;
-  __syncthreads();
-  if (tid < NT * NT) {
-    // the stored tile of position block (p, q), p <= q: (row tile ord[q], column tile ord[p])
-    const int p = tid / NT, q = tid % NT;
-    int sl = -1;
-    if (p <= q) {
-      const int tp = ord[p], tq = ord[q];
-      for (int e = b.row_start[tq]; e < b.row_start[tq + 1]; ++e)
-        if (b.row_col[e] == tp) sl = b.row_slot[e];
-    }
-    sslot[p][q] = sl;
+  if (tid < kSmallNB) {
+    S.wf[tid] = S.yf[tid] = S.sf[tid] = S.xf[tid] = S.prc[tid] = 0;
+    S.prog[tid] = tid == 0 ? 1 << 30 : 0;   // wave 0 reads no ring row
+    for (int q = 0; q < kSRing; ++q) S.uf[q][tid] = 0;
+    if (tid < kSRing) S.urc[tid] = 0;
+    if (tid < 2) S.hf[tid] = 0;
+    if (tid == 0) S.abort = 0;
   }
   __syncthreads();
-  // block (I, J), I <= J, of the position-ordered matrix
-  auto load_blk = [&](int I, int J) {
-    v4d v = v4d{0.0, 0.0, 0.0, 0.0};
-    const int p = I >> 2, q = J >> 2, sl = sslot[p][q];
-    if (sl < 0) return v;
-    const double* t = slot_ptr(b, sl);
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int a = 16 * (I & 3) + g + 4 * rr, c = 16 * (J & 3) + li;
-      v[rr] = p == q ? t[a * T + c] : t[c * T + a];
-    }
-    return v;
-  };
-  auto load_rhs = [&](int I) {
-    v4d v = v4d{0.0, 0.0, 0.0, 0.0};
-    if (li == 0) {
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) v[rr] = r[static_cast<int64_t>(ord[I >> 2]) * T + 16 * (I & 3) + g + 4 * rr];
-    }
-    return v;
-  };
   const v4d zero = v4d{0.0, 0.0, 0.0, 0.0};
-  v4d Dg[kSmallD], Rg[kSmallD], O[kSmallOff];
-  int oI[kSmallOff], oJ[kSmallOff];
-#pragma unroll
-  for (int s = 0; s < kSmallOff; ++s) {
-    oI[s] = oJ[s] = -1;
-    if (kSmallWaves * s + w < kSmallNOff) small_off_block(kSmallWaves * s + w, oI[s], oJ[s]);
-    if (oJ[s] >= nb) oI[s] = -1;   // outside this system
-    O[s] = oI[s] >= 0 ? load_blk(oI[s], oJ[s]) : zero;
-  }
-#pragma unroll
-  for (int d = 0; d < kSmallD; ++d) {
-    const int K = w + kSmallWaves * d;
-    Dg[d] = K < nb ? load_blk(K, K) : zero;
-    Rg[d] = K < nb ? load_rhs(K) : zero;
-  }
-  bool ok = true;
-  // the owner of diagonal block K = w + 8d: U_KK, W, y_K = W^T r_K (y_K
-  // also into buffer buf for the step's right-hand-side updates)
-  auto factor = [&](auto dc, int buf) {
-    constexpr int d = decltype(dc)::value;
-    const int K = w + kSmallWaves * d;
-    v4d Wm;
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) Wm[rr] = (g + 4 * rr == li) ? 1.0 : 0.0;
-    factor16(Dg[d], Wm, l, ok, &dscr[w][0]);
-    st_blk(&Ws[K][0], Wm, l);
-    const v4d Y = mfma_tn(Wm, Rg[d], zero, false);
-    st_blk(&Ur[buf][kSmallNB][0], Y, l);
-    if (li == 0) {
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) ys[16 * K + g + 4 * rr] = Y[rr];
-    }
+  // Block (I, J), I <= J, of the position-ordered matrix (zero where no tile
+  // is stored, or when !use): its 16x16 source region read row by row with
+  // coalesced 16-byte loads (raw_load; branch-free, so a wave's loads all go
+  // out together), then turned into accumulator layout through the wave's own
+  // LDS staging rows (unstage; transposed for a block of an off-diagonal
+  // tile, which stores A[I][J]^T). Direct accumulator-layout loads of the
+  // transposed blocks touch 16 rows per instruction and kept the last waves
+  // waiting ~10 us for their blocks.
+  struct RawBlk {
+    d2s h0, h1;
+    bool tr, present;
   };
-  // step K's update of diagonal block w + 8d and its right-hand side
-  auto diag_update = [&](auto dc, int K, int buf) {
-    constexpr int d = decltype(dc)::value;
-    const int Kd = w + kSmallWaves * d;
-    if (Kd > K && Kd < nb) {
-      const v4d Uk = ld_blk(&Ur[buf][Kd][0], l);
-      Dg[d] = mfma_tn(Uk, Uk, Dg[d], true);
-      Rg[d] = mfma_tn(Uk, ld_blk(&Ur[buf][kSmallNB][0], l), Rg[d], true);
-    }
+  auto raw_load = [&](int I, int J, bool use) {
+    const int Ic = use ? I : 0, Jc = use ? J : 0;
+    const int p = Ic >> 2, q = Jc >> 2, sl = m.slot[p][q];
+    RawBlk rb;
+    rb.present = use && sl >= 0;
+    rb.tr = p != q;
+    const double* t = slot_ptr(b, rb.present ? sl : 0);
+    const int br = rb.tr ? 16 * (Jc & 3) : 16 * (Ic & 3), bc = rb.tr ? 16 * (Ic & 3) : 16 * (Jc & 3);
+    const d2s* src = reinterpret_cast<const d2s*>(t + (br + (l >> 3)) * T + bc + 2 * (l & 7));
+    rb.h0 = src[0];
+    rb.h1 = src[4 * T];   // eight rows down
+    return rb;
   };
-  if (w == 0 && nb > 0) factor(small_ic<0>{}, 0);
-  for (int K = 0; K < nb; ++K) {
-    const int buf = K & 1;
-    __syncthreads();   // W_K, y_K out
-    const v4d Wc = ld_blk(&Ws[K][0], l);
+  double* stg = &S.ring[0][0][0] + w * kSStage;
+  auto unstage = [&](const RawBlk& rb) {
+    reinterpret_cast<d2s*>(stg + (l >> 3) * 18)[l & 7] = rb.h0;
+    reinterpret_cast<d2s*>(stg + ((l >> 3) + 8) * 18)[l & 7] = rb.h1;
+    v4d v;
 #pragma unroll
-    for (int s = 0; s < kSmallOff; ++s)
-      if (oI[s] == K) {
-        O[s] = mfma_tn(Wc, O[s], zero, false);
-        st_blk(&Ur[buf][oJ[s]][0], O[s], l);
-      }
-    __syncthreads();   // row K of U out
-    const int K1 = K + 1;
-    const bool next = K1 < nb && w == (K1 & (kSmallWaves - 1));
-    if (next) {
-      // lookahead: block K+1 updated and factored before this wave's other updates
-      if (K1 < kSmallWaves) {
-        diag_update(small_ic<0>{}, K, buf);
-        factor(small_ic<0>{}, buf ^ 1);
-        if constexpr (kSmallD > 1) diag_update(small_ic<1>{}, K, buf);
-      } else if constexpr (kSmallD > 1) {
-        diag_update(small_ic<1>{}, K, buf);
-        factor(small_ic<1>{}, buf ^ 1);
-        diag_update(small_ic<0>{}, K, buf);
-      }
-    } else {
-      diag_update(small_ic<0>{}, K, buf);
-      if constexpr (kSmallD > 1) diag_update(small_ic<1>{}, K, buf);
+    for (int rr = 0; rr < 4; ++rr) v[rr] = rb.tr ? stg[li * 18 + g + 4 * rr] : stg[(g + 4 * rr) * 18 + li];
+    return rb.present ? v : zero;
+  };
+  // r_I[li] (every row group)
+  auto load_r = [&](int I) { return r[static_cast<int64_t>(m.ord[I >> 2]) * T + 16 * (I & 3) + li]; };
+  // (Y^T v)[li] for a block Y and a vector v in LDS (v[g + 4rr] read here)
+  auto tmatvec = [&](const v4d& Y, const double* v) {
+    double p = 0.0;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) p = __builtin_fma(Y[rr], v[g + 4 * rr], p);
+    return sum_groups(p);
+  };
+
+  // ---- the matrix into registers: wave 0 D(0) and r_0; wave J its
+  // off-band blocks and its band D(J), A[J-1][J], r_J ----
+  int bI[kSReg], bJ[kSReg];
+  v4d A[kSReg];
+  const int J = w;
+  const bool band = w > 0 && J < nb;
+  v4d Dp, Ap;
+  double rp;
+  {
+    RawBlk rb[kSReg];
+#pragma unroll
+    for (int s = 0; s < kSReg; ++s) {
+      bI[s] = w > 0 ? kSmallDeal.I[w][s] : -1;
+      bJ[s] = w > 0 ? kSmallDeal.J[w][s] : -1;
+      if (bJ[s] >= nb) bI[s] = -1;   // outside this system (or no block)
+      rb[s] = raw_load(bI[s], bJ[s], bI[s] >= 0);
     }
+    const RawBlk rd = raw_load(J, J, w == 0 ? nb > 0 : band), ra = raw_load(J - 1, J, band);
+    rp = (w == 0 ? nb > 0 : band) ? load_r(J) : 0.0;
 #pragma unroll
-    for (int s = 0; s < kSmallOff; ++s)
-      if (oI[s] > K)
-        O[s] = mfma_tn(ld_blk(&Ur[buf][oI[s]][0], l), ld_blk(&Ur[buf][oJ[s]][0], l), O[s], true);
+    for (int s = 0; s < kSReg; ++s) A[s] = unstage(rb[s]);
+    Dp = unstage(rd);
+    Ap = unstage(ra);
   }
-  if (!ok && l == 0) *fail = 1;
-  // backward substitution
-  auto solve_x = [&](int K) {
-    if (li == 0) {
+  __syncthreads();   // the staging rows (ring) free
+  TCLKW(28, w);
+  if (w == 0) {
+    // ---- the chain of diagonal blocks ----
+    bool ok = true;
+    v4d D = Dp;
+    double rk = rp;
+    for (int K = 0; K < nb; ++K) {
+      TCLKW(20, K);
+      if (g == 0) S.rs[K][li] = rk;
+      v4d Wm;
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int row = g + 4 * rr;
-        double t = ys[16 * K + row];
-        for (int J = K + 1; J < nb; ++J) t -= pb[K][J][row];
-        tv[row] = t;
+      for (int rr = 0; rr < 4; ++rr) Wm[rr] = (g + 4 * rr == li) ? 1.0 : 0.0;
+      factor16(D, Wm, l, ok, &S.dscr[0]);
+      st_b2(&S.Ws[K][0], Wm, l);
+      lds_flag_set(&S.wf[K], 1);
+      TCLKW(21, K);
+      if (K + 1 < nb) {
+        const int hbuf = (K + 1) & 1;
+        small_wait(&S.hf[hbuf], K + 1, &S.abort);
+        TCLKW(22, K);
+        const v4d Dn = ld_b2(&S.hb[hbuf][0][0], l), An = ld_b2(&S.hb[hbuf][1][0], l);
+        const double rn = S.hr[hbuf][li];
+        const v4d U = mfma_tn(Wm, An, zero, false);
+        st_b2(&S.Usd[K][0], U, l);
+        lds_flag_set(&S.sf[K], 1);
+        D = mfma_tn(U, U, Dn, true);
+        const double yk = tmatvec(Wm, &S.rs[K][0]);
+        if (g == 0) S.ys[K][li] = yk;
+        lds_flag_set(&S.yf[K], 1);
+        rk = rn - tmatvec(U, &S.ys[K][0]);
+        TCLKW(23, K);
+      } else {
+        const double yk = tmatvec(Wm, &S.rs[K][0]);
+        if (g == 0) S.ys[K][li] = yk;
+        lds_flag_set(&S.yf[K], 1);
       }
     }
-    __builtin_amdgcn_wave_barrier();
-    const double tc = tv[li];
-    const v4d Wk = ld_blk(&Ws[K][0], l);
-    double xr[4];
+    // ---- backward: x_K = W_K (y_K - sum_{J > K} U[K][J] x_J) ----
+    for (int K = nb - 1; K >= 0; --K) {
+      const v4d Wk = ld_b2(&S.Ws[K][0], l);
+      const v4d Um = ld_b2(&S.Usd[K >= 1 ? K - 1 : 0][0], l);
+      const double yk = S.ys[K][li];
+      small_wait(&S.prc[K], max(0, nb - K - 2), &S.abort);
+      double t = yk;
+      for (int J = K + 1; J < nb; ++J) t -= S.pb[small_ut(K, J)][li];
+      double xr[4];
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) xr[rr] = sum16(Wk[rr] * tc);
-    if (li == 0) {
+      for (int rr = 0; rr < 4; ++rr) xr[rr] = sum16(Wk[rr] * t);
+      if (li == 0) {
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int row = g + 4 * rr;
-        xv[16 * K + row] = xr[rr];
-        x[static_cast<int64_t>(ord[K >> 2]) * T + 16 * (K & 3) + row] = xr[rr];
-      }
-    }
-  };
-  for (int K = nb - 1; K >= 0; --K) {
-    const int J = K + 1;
-    if (J < nb) {
-      const double xj = xv[16 * J + li];
-#pragma unroll
-      for (int s = 0; s < kSmallOff; ++s)
-        if (oJ[s] == J && oI[s] >= 0) {
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr) {
-            const double pr = sum16(O[s][rr] * xj);
-            if (li == 0) pb[oI[s]][J][g + 4 * rr] = pr;
-          }
+        for (int rr = 0; rr < 4; ++rr) {
+          S.xs[K][g + 4 * rr] = xr[rr];
+          x[static_cast<int64_t>(m.ord[K >> 2]) * T + 16 * (K & 3) + g + 4 * rr] = xr[rr];
         }
+      }
+      lds_flag_set(&S.xf[K], 1);
+      TCLKW(24, K);
+      if (K >= 1) {
+        // the superdiagonal product U[K-1][K] x_K, for row K-1
+        const double xk = S.xs[K][li];
+        double pr[4];
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) pr[rr] = sum16(Um[rr] * xk);
+        if (li == 0) {
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) S.pb[small_ut(K - 1, K)][g + 4 * rr] = pr[rr];
+        }
+      }
     }
-    __syncthreads();   // every U[K][J] x_J out
-    if (w == (K & (kSmallWaves - 1))) solve_x(K);
-    __syncthreads();   // x_K out
+    if ((!ok || lds_ld(&S.abort)) && l == 0) *fail = 1;
+    TCLKW(29, w);
+    return;
   }
+
+  // ---- waves 1..15 ----
+  // this wave's band: D(J), A[J-1][J], r_J for J = w, handed over after step J - 2
+  auto hand_over = [&]() {
+    const int hbuf = J & 1;
+    st_b2(&S.hb[hbuf][0][0], Dp, l);
+    st_b2(&S.hb[hbuf][1][0], Ap, l);
+    if (g == 0) S.hr[hbuf][li] = rp;
+    lds_flag_set(&S.hf[hbuf], J);
+    TCLKW(27, J);
+  };
+  if (band && J == 1) hand_over();
+  auto ring = [&](int K, int Jr) { return &S.ring[K % kSRing][Jr - K - 2][0]; };
+  for (int K = 0; K < nb; ++K) {
+    small_wait(&S.wf[K], 1, &S.abort);
+    TCLKW(26, 16 * w + K);
+    // (1) row K of U
+    bool first = true;
+#pragma unroll
+    for (int s = 0; s < kSReg; ++s)
+      if (bI[s] == K) {
+        if (first) small_wait_prog(S.prog, K - kSRing + 1, l, &S.abort);   // ring row K % kSRing free
+        first = false;
+        const v4d Wk = ld_b2(&S.Ws[K][0], l);
+        A[s] = mfma_tn(Wk, A[s], zero, false);
+        st_b2(ring(K, bJ[s]), A[s], l);
+        lds_flag_set(&S.uf[K % kSRing][bJ[s]], K + 1);
+        if (l == 0) __hip_atomic_fetch_add(&S.urc[K % kSRing], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    // (2) the band blocks, handed to wave 0 after step J - 2
+    if (band && K <= J - 2) {
+      small_wait(&S.uf[K % kSRing][J], K + 1, &S.abort);
+      const v4d Uj = ld_b2(ring(K, J), l);
+      v4d Uj1;
+      if (K == J - 2) {
+        small_wait(&S.sf[K], 1, &S.abort);
+        Uj1 = ld_b2(&S.Usd[K][0], l);
+      } else {
+        small_wait(&S.uf[K % kSRing][J - 1], K + 1, &S.abort);
+        Uj1 = ld_b2(ring(K, J - 1), l);
+      }
+      Dp = mfma_tn(Uj, Uj, Dp, true);
+      Ap = mfma_tn(Uj1, Uj, Ap, true);
+      small_wait(&S.yf[K], 1, &S.abort);
+      rp -= tmatvec(Uj, &S.ys[K][0]);
+      if (K == J - 2) hand_over();
+    }
+    // (3) the trailing update of this wave's blocks below row K, once the
+    // whole of row K is out
+    bool below = false;
+#pragma unroll
+    for (int s = 0; s < kSReg; ++s) below = below || bI[s] > K;
+    if (below) small_wait(&S.urc[K % kSRing], small_ring_count(K, nb), &S.abort);
+#pragma unroll
+    for (int s = 0; s < kSReg; ++s)
+      if (bI[s] > K) {
+        const int I = bI[s];
+        v4d U1;
+        if (I == K + 1) {
+          small_wait(&S.sf[K], 1, &S.abort);
+          U1 = ld_b2(&S.Usd[K][0], l);
+        } else {
+          U1 = ld_b2(ring(K, I), l);
+        }
+        A[s] = mfma_tn(U1, ld_b2(ring(K, bJ[s]), l), A[s], true);
+      }
+    lds_flag_set(&S.prog[w], K + 1);
+    TCLKW(25, 16 * w + K);
+  }
+  // backward: U[I][J] x_J of this wave's blocks, in descending J
+#pragma unroll
+  for (int s = 0; s < kSReg; ++s)
+    if (bI[s] >= 0) {
+      small_wait(&S.xf[bJ[s]], 1, &S.abort);
+      const double xj = S.xs[bJ[s]][li];
+      double pr[4];
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) pr[rr] = sum16(A[s][rr] * xj);
+      if (li == 0) {
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) S.pb[small_ut(bI[s], bJ[s])][g + 4 * rr] = pr[rr];
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (l == 0) __hip_atomic_fetch_add(&S.prc[bI[s]], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  TCLKW(29, w);
 }
 
 }  // namespace
@@ -1701,9 +1873,9 @@ void launch_tile_backward(const TileDev& b, const TileSchedDev& sd, const std::v
   }
 }
 
-void launch_small_solve(const TileDev& b, const double* r, double* x, int* fail, hipStream_t s) {
+void launch_small_solve(const TileDev& b, const SmallMap& m, const double* r, double* x, int* fail, hipStream_t s) {
   if (b.NT <= 0 || b.NT > kSmallNT) return;   // the host checks the size (solver.cpp)
-  k_small_solve<<<1, kSmallWaves * 64, 0, s>>>(b, r, x, fail);
+  k_small_solve<<<1, kSW * 64, 0, s>>>(b, m, r, x, fail);
 }
 
 }  // namespace dynohip
