@@ -142,6 +142,11 @@ struct Map {
     return frames.rbegin()->first;
   }
 
+  // the frame node of the previous add (a packet's measurements share one
+  // frame; map nodes never move or go away)
+  FrameNode* last_fn = nullptr;
+  uint64_t last_f = 0;
+
   // Map::addOrUpdateMapStructures (Map.hpp:376-444)
   void add(const dynob_measurement& m) {
     const bool is_static = m.object_id == kBackgroundLabel;
@@ -152,24 +157,35 @@ struct Map {
       n.object_id = m.object_id;
       lit = landmarks.emplace(m.tracklet_id, n).first;
     }
-    FrameNode& fn = frames[m.frame_id];
+    if (!last_fn || last_f != m.frame_id) {
+      last_fn = &frames[m.frame_id];
+      last_f = m.frame_id;
+    }
+    FrameNode& fn = *last_fn;
     fn.frame_id = m.frame_id;
     LandmarkNode& ln = lit->second;
     // "this might fail of a tracklet get associated with a different object"
     DB_CHECK(ln.object_id == m.object_id, DYNOHIP_EINVAL,
              "tracklet " + std::to_string(m.tracklet_id) + " changed object label");
-    // LandmarkNode::add (MapNodes-inl.hpp:163-176)
-    DB_CHECK(!ln.seen_at(m.frame_id), DYNOHIP_EINVAL,
+    // LandmarkNode::add (MapNodes-inl.hpp:163-176); frames mostly arrive in
+    // order, so the new entry usually goes at the end (hinted insert)
+    auto& ms = ln.measurements;
+    const bool at_end = ms.empty() || ms.rbegin()->first < m.frame_id;
+    DB_CHECK(at_end || !ln.seen_at(m.frame_id), DYNOHIP_EINVAL,
              "Unable to add new measurement to landmark node " + std::to_string(m.tracklet_id) + " at frame " +
                  std::to_string(m.frame_id) + " as a measurement already exists at this frame!");
-    ln.measurements[m.frame_id] = {m.landmark[0], m.landmark[1], m.landmark[2]};
+    const std::array<double, 3> xyz = {m.landmark[0], m.landmark[1], m.landmark[2]};
+    if (at_end)
+      ms.emplace_hint(ms.end(), m.frame_id, xyz);
+    else
+      ms[m.frame_id] = xyz;
     if (is_static) {
-      fn.static_landmarks.insert(m.tracklet_id);
+      fn.static_landmarks.emplace_hint(fn.static_landmarks.end(), m.tracklet_id);
     } else {
       ObjectNode& on = objects[m.object_id];
       on.object_id = m.object_id;
       on.dynamic_landmarks.insert(m.tracklet_id);
-      fn.dynamic_landmarks.insert(m.tracklet_id);
+      fn.dynamic_landmarks.emplace_hint(fn.dynamic_landmarks.end(), m.tracklet_id);
       fn.objects_seen.insert(m.object_id);
     }
   }
@@ -332,18 +348,22 @@ struct GraphExport {
   std::vector<uint64_t> keys[6];
   std::vector<double> meas[6], sig[6], hub[6];
   void build(const Graph& g) {
+    size_t n[6] = {};
+    for (const Factor& f : g.factors) ++n[f.type];
     for (int t = 0; t < 6; ++t) {
-      keys[t].clear();
-      meas[t].clear();
-      sig[t].clear();
-      hub[t].clear();
+      keys[t].resize(n[t] * kNKeys[t]);
+      meas[t].resize(n[t] * kMeas[t]);
+      sig[t].resize(n[t] * kDim[t]);
+      hub[t].resize(n[t]);
+      n[t] = 0;
     }
     for (const Factor& f : g.factors) {
       const int t = f.type;
-      keys[t].insert(keys[t].end(), f.keys, f.keys + kNKeys[t]);
-      meas[t].insert(meas[t].end(), f.meas, f.meas + kMeas[t]);
-      sig[t].insert(sig[t].end(), f.noise.sigmas, f.noise.sigmas + kDim[t]);
-      hub[t].push_back(f.noise.huber);
+      const size_t i = n[t]++;
+      std::copy(f.keys, f.keys + kNKeys[t], keys[t].data() + i * kNKeys[t]);
+      std::copy(f.meas, f.meas + kMeas[t], meas[t].data() + i * kMeas[t]);
+      std::copy(f.noise.sigmas, f.noise.sigmas + kDim[t], sig[t].data() + i * kDim[t]);
+      hub[t][i] = f.noise.huber;
     }
   }
   void view(dynohip_graph_view* g) const {
@@ -367,6 +387,9 @@ struct ValuesExport {
     keys.clear();
     kinds.clear();
     data.clear();
+    keys.reserve(v.size());
+    kinds.reserve(v.size());
+    data.reserve(12 * v.size());
     for (const auto& kv : v) {
       keys.push_back(kv.first);
       kinds.push_back(kv.second.kind);
@@ -386,7 +409,18 @@ struct NoiseModels {
 // UpdateObservationResult (Formulation.hpp:44-64)
 struct UpdateResult {
   std::map<int32_t, std::set<uint64_t>> objects_affected_per_frame;
-  void affected(uint64_t frame, int32_t obj) { objects_affected_per_frame[obj].insert(frame); }
+  // the two most recent (frame, object) pairs (a point's updates repeat them)
+  uint64_t seen_f[2] = {~0ull, ~0ull};
+  int32_t seen_o[2] = {0, 0};
+  void affected(uint64_t frame, int32_t obj) {
+    for (int i = 0; i < 2; ++i)
+      if (seen_f[i] == frame && seen_o[i] == obj) return;
+    objects_affected_per_frame[obj].insert(frame);
+    seen_f[1] = seen_f[0];
+    seen_o[1] = seen_o[0];
+    seen_f[0] = frame;
+    seen_o[0] = obj;
+  }
 };
 
 struct Formulation {
@@ -576,12 +610,10 @@ struct Formulation {
         internal.add(kPoseToPoint, {camera_pose_key(k), point_key}, ln.measurement(k), noise.static_point);
       } else {
         if (static_cast<int64_t>(ln.num_observations()) < params.min_static_observations) continue;
-        for (const auto& kv : ln.measurements) {  // seen frames, ascending
-          const uint64_t seen = kv.first;
-          if (seen > k) break;
-          if (!do_backtrack && seen < k) continue;
-          internal.add(kPoseToPoint, {camera_pose_key(seen), point_key}, kv.second.data(), noise.static_point);
-        }
+        // seen frames, ascending, up to k (only k itself without backtracking)
+        for (auto it = do_backtrack ? ln.measurements.begin() : ln.measurements.lower_bound(k);
+             it != ln.measurements.end() && it->first <= k; ++it)
+          internal.add(kPoseToPoint, {camera_pose_key(it->first), point_key}, it->second.data(), noise.static_point);
         double lmk_world[3];
         if (!static_landmark(t, lmk_world)) transform_from(T_world_camera_frontend, ln.measurement(k), lmk_world);
         values_insert(new_values, point_key, point_value(lmk_world));
@@ -603,7 +635,14 @@ struct Formulation {
   // WorldMotionFormulation::dynamicPointUpdateCallback
   // (WorldMotionEstimator.cc:155-238) and WorldPoseFormulation's
   // (WorldPoseEstimator.cc:84-165)
+  // (the caller's theta and new_values both take the point's values; they go
+  // into each directly, where the reference collects them in a local Values
+  // first: same contents, same exception on a key already in theta)
   void dynamic_point_update(const PointContext& c, UpdateResult& result, Values& new_values, Graph& nf) {
+    auto put = [&](uint64_t key, const Value& v) {
+      values_insert(theta, key, v);
+      values_insert(new_values, key, v);
+    };
     const LandmarkNode& ln = map->landmarks.at(c.tracklet);
     const uint64_t key_k_1 = dynamic_key(c.frame_k_1, c.tracklet);
     const uint64_t key_k = dynamic_key(c.frame_k, c.tracklet);
@@ -617,9 +656,9 @@ struct Formulation {
         std::memcpy(lmk, v->d, sizeof(lmk));
       else
         transform_from(c.X_k_1_measured, ln.measurement(c.frame_k_1), lmk);
-      values_insert(new_values, key_k_1, point_value(lmk));
+      put(key_k_1, point_value(lmk));
     }
-    DB_CHECK(new_values.count(key_k_1) || query(key_k_1), DYNOHIP_ESTATE,
+    DB_CHECK(query(key_k_1), DYNOHIP_ESTATE,
              "previous dynamic point of tracklet " + std::to_string(c.tracklet) + " at frame " +
                  std::to_string(c.frame_k_1) + " was never added");
     nf.add(kPoseToPoint, {camera_pose_key(c.frame_k), key_k}, ln.measurement(c.frame_k), noise.dynamic_point);
@@ -629,7 +668,7 @@ struct Formulation {
       std::memcpy(lmk, v->d, sizeof(lmk));
     else
       transform_from(c.X_k_measured, ln.measurement(c.frame_k), lmk);
-    values_insert(new_values, key_k, point_value(lmk));
+    put(key_k, point_value(lmk));
     if (motion_formulation()) {
       nf.add(kTernary, {key_k_1, key_k, motion_key(c.object, c.frame_k)}, nullptr, noise.landmark_motion);
     } else {
@@ -781,10 +820,7 @@ struct Formulation {
             c.X_k_measured = iol_pose(prev->first);
             c.X_k_1_measured = X_k_1;
             c.is_starting_motion_frame = (it == start_it);
-            Values local;
-            dynamic_point_update(c, result, local, internal);
-            values_insert(theta, local);
-            values_insert(new_values, local);
+            dynamic_point_update(c, result, new_values, internal);
           }
         } else {
           PointContext c;
@@ -795,10 +831,7 @@ struct Formulation {
           c.X_k_1_measured = iol_pose(k_1);
           c.X_k_measured = iol_pose(k);
           c.is_starting_motion_frame = false;
-          Values local;
-          dynamic_point_update(c, result, local, internal);
-          values_insert(theta, local);
-          values_insert(new_values, local);
+          dynamic_point_update(c, result, new_values, internal);
         }
       }
     }
