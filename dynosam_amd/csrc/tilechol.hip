@@ -90,11 +90,6 @@ __device__ __forceinline__ void mfma_abt_acc(const double* As, const double* Bs,
   }
 }
 
-__device__ __forceinline__ void mfma_abt(const double* As, const double* Bs, int wave, int lane, v4d acc[2][2]) {
-  zero_acc(acc);
-  mfma_abt_acc(As, Bs, wave, lane, acc);
-}
-
 // element (row, col) of the quadrant result held by this lane
 #define MFMA_ROW(wave, lane, ti, r) (32 * ((wave) >> 1) + 16 * (ti) + ((lane) >> 4) + 4 * (r))
 #define MFMA_COL(wave, lane, tj) (32 * ((wave) & 1) + 16 * (tj) + ((lane) & 15))
@@ -121,7 +116,9 @@ __device__ unsigned long long g_tclk[32][32768];
   do {                  \
   } while (0)
 #endif
+#ifdef DYNOHIP_TASK_CLOCK
 __device__ __forceinline__ unsigned long long rtc() { return __builtin_amdgcn_s_memrealtime(); }
+#endif
 
 __device__ __forceinline__ double* slot_ptr(const TileDev& b, int32_t slot) {
   return b.slots + static_cast<int64_t>(slot) * T * T;
