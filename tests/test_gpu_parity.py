@@ -515,6 +515,9 @@ def test_execution_paths_agree(gpu_available, name, monkeypatch):
 
 
 SMALL_GRAPHS = [("T1", {}), (None, dict(frames=8, objects=1, static_landmarks=80, dyn_slots=4)),
+                (None, dict(frames=10, objects=1, static_landmarks=80, dyn_slots=4)),    # 2 tiles
+                (None, dict(frames=12, objects=1, static_landmarks=80, dyn_slots=4)),    # 3 tiles
+                (None, dict(frames=20, objects=1, static_landmarks=100, dyn_slots=4)),   # 4 tiles, 9 of 10 stored
                 (None, dict(frames=10, objects=3, static_landmarks=150, dyn_slots=6))]
 
 
@@ -527,7 +530,7 @@ def test_small_solve_matches_tile_dag(gpu_available, name, kw, monkeypatch):
     each path against the exact step (the oracle's Schur solve in x87
     extended precision): the one-workgroup solve is as accurate as the DAG
     up to the summation order (within 10x its distance, observed <= 4x, or
-    1e-12); and the free-running LM takes the same tries, ending within the
+    1e-10 of the step); and the free-running LM takes the same tries, ending within the
     north-star 1e-6 of each other (the runs drift apart through their
     accumulated rounding: 2.6e-9 on T1)."""
     g, v, _ = synth.generate(name, **kw)
@@ -558,7 +561,10 @@ def test_small_solve_matches_tile_dag(gpu_available, name, kw, monkeypatch):
     for lam, x, y, e in zip(lams, da, db, exact):
         es, ed = rel(x, e), rel(y, e)
         print(name, kw, nt, f"lambda {lam:.0e}: small vs DAG {rel(x, y):.2e}, to the exact step: small {es:.2e}, DAG {ed:.2e}")
-        assert es <= max(1e-12, 10 * ed)
+        # (the floor: 1e-10 of the step is far inside double precision for
+        # a system conditioned ~1e6 at lambda 1e-5; the DAG's own distance
+        # ranges from 2e-12 to 5e-11 over these graphs)
+        assert es <= max(1e-10, 10 * ed)
     assert ta == tb
     assert (ra.iterations, ra.inner_iterations) == (rb.iterations, rb.inner_iterations)
     print(name, kw, nt, f"free run values rel {rel(va, vb):.2e}")
