@@ -1774,7 +1774,15 @@ __device__ unsigned long long g_lclk[8][8192];
   do {                                                                                            \
     if (threadIdx.x == 0 && blockIdx.x < 8192) g_lclk[i][blockIdx.x] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
+// (lane 0 of wave 2: its gradient rows done)
+#define LCLK2(i)                                                                                  \
+  do {                                                                                            \
+    if (threadIdx.x == 128 && blockIdx.x < 8192) g_lclk[i][blockIdx.x] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 #else
+#define LCLK2(i) \
+  do {           \
+  } while (0)
 #define LCLK(i) \
   do {          \
   } while (0)
@@ -1959,6 +1967,7 @@ __device__ void lone_schur_block(const LoneSchurDev& d, int gb, double* __restri
     }
     acc[j] += acc1;
   }
+  LCLK(5);
   const uint32_t out = static_cast<uint32_t>(hdr[2]);
   if (wave >= 2 && lane < n6) {
     const int a = lane / 6, r = lane - 6 * a;
@@ -1973,6 +1982,7 @@ __device__ void lone_schur_block(const LoneSchurDev& d, int gb, double* __restri
         }
         arena[out + 36 * np + lane] = sJb[lane] - zz;
       }
+      LCLK2(6);
     } else if (wave == 3) {
       double jj[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
       for (int p = 0; p < npt; ++p) {
@@ -2005,6 +2015,7 @@ __device__ void lone_schur_block(const LoneSchurDev& d, int gb, double* __restri
     }
   }
   __syncthreads();
+  LCLK(7);
   // lane (li, lk) of a tile holds rows lk + 4i, column li
 #pragma unroll
   for (int j = 0; j < kLoneWT; ++j) {

@@ -38,6 +38,10 @@ def main():
     for i, nm in enumerate(names):
         d = t[i + 1] - t[i]
         print(f"  {nm:14s} median {np.median(d):7.2f} p90 {np.percentile(d, 90):7.2f} max {d.max():7.2f} us")
+    x = (buf[5:8, :n].astype(np.int64) - buf[0, :n].astype(np.int64).min()) / 100.0
+    for nm, d in (("  MFMA tiles (wave 0)", x[0] - t[3]), ("  gradient (wave 2)", x[1] - t[3]),
+                  ("  barrier passed", x[2] - t[3]), ("  stores (wave 0)", t[4] - x[2])):
+        print(f"  {nm:20s} median {np.median(d):7.2f} p90 {np.percentile(d, 90):7.2f} max {d.max():7.2f} us")
     tot = t[4] - t[0]
     print(f"  {'total':14s} median {np.median(tot):7.2f} p90 {np.percentile(tot, 90):7.2f} max {tot.max():7.2f} us")
     st = np.sort(t[0])
