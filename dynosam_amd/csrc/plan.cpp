@@ -156,6 +156,10 @@ std::vector<int64_t> even_cuts(int64_t n) {
 
 }  // namespace
 
+// values + factors below which a plan runs its parallel sections on one
+// thread (a C2-stream window: ~1.5k values, ~4k factors; C2: 185k)
+constexpr size_t kSmallPlanItems = 20000;
+
 static double plan_now() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -245,6 +249,11 @@ void plan_recycle(Plan& P) {
 int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t* kind, size_t n, Plan& P,
                std::string& err, int nranks, int rank, bool with_schedule, bool structure_only, PlanHook* hook) {
   double tmark = plan_now();
+  // small graphs plan on this thread (and its schedule thread) alone
+  const size_t n_fac = g.pose_to_point.n + g.landmark_motion_ternary.n + g.between.n + g.prior.n +
+                       g.landmark_motion_pose.n + g.landmark_pose_smoothing.n;
+  const int pcap = n + n_fac < kSmallPlanItems ? 1 : 0;
+  PlanCap plan_cap(pcap);
   plan_recycle(P);
   P.nranks = nranks;
   P.rank = rank;
@@ -751,6 +760,7 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
     }
   } sched_join{sched};
   sched = std::thread([&] {
+    PlanCap sched_cap(pcap);
     structure();
     pairs_ready.set_value();
     if (with_schedule) sched_ok = build_tile_schedule(P, true);
@@ -1071,6 +1081,7 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
     };
     if (!structure_only) {
       std::thread grad([&] {
+        PlanCap grad_cap(pcap);
         // gradient gathers per pose: J_A^T b per factor, -W_A v per component,
         // the groups' partial gradients
         // (on a thread of its own, one range: it runs beside the pair lists)

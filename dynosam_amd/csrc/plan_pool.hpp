@@ -40,10 +40,16 @@ class PlanPool {
     }
     return *p;
   }
-  int workers() const { return nmax_; }
+  // (a PlanCap on the calling thread lowers both: a section sized by
+  // workers() never asks run() for more workers than it gets)
+  int workers() const { return cap() > 0 ? std::min(nmax_, cap()) : nmax_; }
+  static int& cap() {
+    static thread_local int c = 0;
+    return c;
+  }
   template <typename Body>
   void run(int nw, Body&& body) {
-    nw = std::max(1, std::min(nw, nmax_));
+    nw = std::max(1, std::min(nw, workers()));
     if (nw == 1) {
       body(0);
       return;
@@ -133,6 +139,20 @@ class PlanPool {
   std::exception_ptr err_;   // first exception of a helper in the current section
   std::atomic<int> pending_{0}, sleepers_{0};
   std::atomic<uint64_t> gen_{0};
+};
+
+// Caps the parallel sections of the calling thread at `c` workers (0: none)
+// for its lifetime. A sliding window's plan (a few thousand factors) is
+// faster on one thread than with the pool's wake-ups per section (set_values
+// 1.26-1.29 against 1.37-1.43 ms per C2-stream window in one A/B run,
+// profiles/r05/window/plan_cap_ab.log); the plan is the same either way
+// (tests/test_plan_digest.py).
+struct PlanCap {
+  int prev;
+  explicit PlanCap(int c) : prev(PlanPool::cap()) { PlanPool::cap() = c; }
+  ~PlanCap() { PlanPool::cap() = prev; }
+  PlanCap(const PlanCap&) = delete;
+  PlanCap& operator=(const PlanCap&) = delete;
 };
 
 // body(b, e) over [0, n) in contiguous ranges on the planner's workers
