@@ -869,6 +869,47 @@ def test_replan_on_reused_handles(gpu_available):
         h.close()
 
 
+_POOL_SCRIPT = r"""
+import sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+from dynosam_amd import synth
+from dynosam_amd.optimizer import Solver
+out = []
+for n, sd in (("C1", 42), ("T2", 43), ("C1", 42)):
+    g, v, _ = synth.generate(n, seed=sd)
+    h = Solver(0)
+    h.set_graph(g)
+    h.set_values(v)
+    h.optimize()
+    out.append(h.values_data())
+    h.close()
+np.savez(sys.argv[2], *out)
+"""
+
+
+def test_pool_cap_zero_same_values(gpu_available, tmp_path):
+    """DYNOHIP_POOL_MAX_MB=0 (read once per process, so in a child process):
+    the device pool keeps nothing between handles and every handle allocates
+    afresh; the values equal this process's pooled handles' bit for bit."""
+    import subprocess
+    import sys
+    f = tmp_path / "pool0.npz"
+    env = dict(os.environ, DYNOHIP_POOL_MAX_MB="0")
+    r = subprocess.run([sys.executable, "-c", _POOL_SCRIPT, os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                        str(f)], capture_output=True, text=True, env=env, timeout=100)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = np.load(f)
+    for i, (n, sd) in enumerate((("C1", 42), ("T2", 43), ("C1", 42))):
+        g, v, _ = synth.generate(n, seed=sd)
+        h = Solver(0)
+        h.set_graph(g)
+        h.set_values(v)
+        h.optimize()
+        assert np.array_equal(h.values_data(), got[f"arr_{i}"]), (n, sd)
+        h.close()
+
+
 def test_replan_two_threads_two_handles(gpu_available):
     """Two handles on two threads (two streams) re-plan back and forth
     between graphs of different sizes while the other solves: blocks that a

@@ -8,7 +8,8 @@ subprocess of its own (host-only planning, no GPU):
     still applied exactly once, queue topological;
   * DYNOHIP_BACK_PART_TILES=2: every backward task split into parts of at
     most two entries that cover its entries in order;
-  * DYNOHIP_PART_BALANCE=0: the partitioned plans' queues topological."""
+  * DYNOHIP_PART_BALANCE=0: the partitioned plans' queues topological;
+  * DYNOHIP_PLAN_TIMING, DYNOHIP_SCHED_TIMING: stage times on stderr, same plan."""
 import json
 import os
 import subprocess
@@ -121,3 +122,16 @@ def test_midpoint_partition_queues_are_topological():
     p = plan_with({"DYNOHIP_PART_BALANCE": "0"}, name="C1", nranks=2)
     for rank in range(2):
         topological(p, f"r{rank}_")
+
+
+def test_timing_knobs_print_and_keep_the_plan(base):
+    """DYNOHIP_PLAN_TIMING / DYNOHIP_SCHED_TIMING only add per-stage times on
+    stderr: the plan is the default one."""
+    e = dict(os.environ, DYNOHIP_PLAN_TIMING="1", DYNOHIP_SCHED_TIMING="1")
+    r = subprocess.run([sys.executable, "-c", _SCRIPT, ROOT, "C1", "1"], capture_output=True, text=True, env=e,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "[plan]" in r.stderr and "[tiles]" in r.stderr, r.stderr[-2000:]
+    p = {k: np.asarray(v, dtype=np.int64) for k, v in json.loads(r.stdout.strip().splitlines()[-1]).items()}
+    for k in base:
+        assert np.array_equal(p[k], base[k]), k
