@@ -2,8 +2,12 @@
 // (tilechol.hip factor16_wave) in isolation: one wave factors a 16x16 SPD
 // block `reps` times back to back, timed with s_memtime; W = U^-1 is written
 // out so the host can check it (W^T B W = I). Built and run by
-// tools/pivot_probe.py (hipcc, ctypes). Variant 0: the factorisation of the
-// kernels (tilechol.hip); variant 1: the candidate in tilechol_f16.h.
+// tools/pivot_probe.py (hipcc, ctypes). Variants: 0 factor16_wave (pivot by
+// pivot), 1 factor16_blk4 (the kernels' form), 2/3 the next pivot formed a
+// step ahead (cubic / bare reciprocal), 4/5 the DPP broadcast folded into
+// v_fmac_f64_dpp, 6 the sub-block's pivots from in-lane replicas
+// (profiles/r05/pivot/probe_inlane.log: 189.5 against 171.5 cycles per pivot,
+// bit-identical).
 #include <hip/hip_runtime.h>
 
 #include "../dynosam_amd/csrc/f16wave.h"
@@ -127,6 +131,59 @@ __device__ __forceinline__ void factor16_fold(v4d& B, v4d& Wv, int l, bool& ok, 
   ok = ok && __all((dj > 0.0) && (dj < 1e300));
 }
 
+// candidate: factor16_blk4 with each four-pivot sub-block's upper triangle
+// replicated in every lane (ten DPP broadcasts up front), so the pivots,
+// reciprocals and multipliers of the sub-block come from in-lane arithmetic
+// (no DPP on the pivot chain); every replicated value is the same operation
+// on the same operands as in the lane that owns its column, so W and the
+// factor are factor16_blk4's bit for bit
+__device__ __forceinline__ void factor16_inlane(v4d& B, v4d& W, int l, bool& ok, double* dscr) {
+  const int j = l & 15;
+  const bool g0 = (l >> 4) & 1, g1 = (l >> 5) & 1;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    double R[4], F[4], a[4][4];
+    groups4(B[s], R);
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int d = c; d < 4; ++d) a[c][d] = bcast_row_lane(R[c], 4 * s + d);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int p = 4 * s + c;
+      const double d = a[c][c];
+      const double rc = rcp_cubic(d);
+      const double f = R[c] * rc;
+      double fm;
+      switch (p) {
+#define KC(q) case q: fm = keep_cols_above<q>(f); break;
+        KC(0) KC(1) KC(2) KC(3) KC(4) KC(5) KC(6) KC(7) KC(8) KC(9) KC(10) KC(11) KC(12) KC(13) KC(14) default: fm = 0.0;
+#undef KC
+      }
+      dscr[p] = d;
+      F[c] = f;
+#pragma unroll
+      for (int k = c + 1; k < 4; ++k) {
+        const double m = a[c][k] * rc;
+        R[k] -= m * R[c];
+#pragma unroll
+        for (int e = k; e < 4; ++e) a[k][e] -= m * a[c][e];
+      }
+#pragma unroll
+      for (int r = 0; r <= s; ++r) W[r] -= bcast_row_lane(W[r], p) * fm;
+    }
+    if (s < 3)
+      B = __builtin_amdgcn_mfma_f64_16x16x4f64(-sel_group(F[0], F[1], F[2], F[3], g0, g1),
+                                               sel_group(R[0], R[1], R[2], R[3], g0, g1), B, 0, 0, 0);
+  }
+  asm volatile("" ::: "memory");
+  const double dj = dscr[j];
+  const double myrs = rsqrt_nr(dj);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) W[r] *= myrs;
+  ok = ok && __all((dj > 0.0) && (dj < 1e300));
+}
+
 template <int V>
 __global__ __launch_bounds__(64) void k_probe(const double* __restrict__ Bin, double* __restrict__ Wout,
                                               unsigned long long* __restrict__ cyc, int reps) {
@@ -149,7 +206,8 @@ __global__ __launch_bounds__(64) void k_probe(const double* __restrict__ Bin, do
     else if constexpr (V == 2) factor16_ahead<1>(B, W, l, ok, dscr);
     else if constexpr (V == 3) factor16_ahead<0>(B, W, l, ok, dscr);
     else if constexpr (V == 4) factor16_fold<1>(B, W, l, ok, dscr);
-    else factor16_fold<0>(B, W, l, ok, dscr);
+    else if constexpr (V == 5) factor16_fold<0>(B, W, l, ok, dscr);
+    else factor16_inlane(B, W, l, ok, dscr);
     asm volatile("" : "+v"(W));
   }
   t1 = __builtin_amdgcn_s_memtime();
@@ -189,7 +247,8 @@ extern "C" int probe_run(int variant, const double* Bh, double* Wh, unsigned lon
   else if (variant == 2) k_probe<2><<<1, 64>>>(B, W, c, reps);
   else if (variant == 3) k_probe<3><<<1, 64>>>(B, W, c, reps);
   else if (variant == 4) k_probe<4><<<1, 64>>>(B, W, c, reps);
-  else k_probe<5><<<1, 64>>>(B, W, c, reps);
+  else if (variant == 5) k_probe<5><<<1, 64>>>(B, W, c, reps);
+  else k_probe<6><<<1, 64>>>(B, W, c, reps);
   if (hipDeviceSynchronize() != hipSuccess) return -2;
   (void)hipMemcpy(Wh, W, 256 * 8, hipMemcpyDeviceToHost);
   (void)hipMemcpy(cyc, c, 16, hipMemcpyDeviceToHost);
