@@ -759,12 +759,16 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
       if (t.joinable()) t.join();
     }
   } sched_join{sched};
-  sched = std::thread([&] {
+  auto sched_body = [&] {
     PlanCap sched_cap(pcap);
     structure();
     pairs_ready.set_value();
     if (with_schedule) sched_ok = build_tile_schedule(P, true);
-  });
+  };
+  // a small graph's structure and schedule take less than starting and
+  // joining a thread for them: run them here, first
+  if (pcap == 1) sched_body();
+  else sched = std::thread(sched_body);
   auto tid = [&](int32_t A, int32_t B) -> int32_t {
     return dense ? id_dense[static_cast<size_t>(A) * span + (A - B)] : id_map.at(pkey(A, B));
   };
@@ -1080,7 +1084,8 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
       for (int64_t s = std::max(s0, nF + nC); s < s1; ++s) on_group(P.lgroup[s - nF - nC]);
     };
     if (!structure_only) {
-      std::thread grad([&] {
+      std::thread grad;
+      auto grad_body = [&] {
         PlanCap grad_cap(pcap);
         // gradient gathers per pose: J_A^T b per factor, -W_A v per component,
         // the groups' partial gradients
@@ -1115,7 +1120,9 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
                                   });
                           },
                           P.gGred);
-      });
+      };
+      if (pcap == 1) grad_body();
+      else grad = std::thread(grad_body);
       struct JoinGrad {
         std::thread& t;
         ~JoinGrad() {
@@ -1151,7 +1158,7 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
                                 });
                         },
                         P.gRed);
-      grad.join();
+      if (grad.joinable()) grad.join();
     }
   }
   plan_mark("reduced system targets", tmark);
