@@ -1407,7 +1407,7 @@ struct EarlyUpload : PlanHook {
   explicit EarlyUpload(dynohip_solver* h) : s(h) {}
   ~EarlyUpload() override { join(); }
   void types_ready(const Plan& P) override {
-    th = std::thread([this, &P] {
+    auto body = [this, &P] {
       (void)hipSetDevice(s->device);
       try {
         Uploads up;
@@ -1422,7 +1422,11 @@ struct EarlyUpload : PlanHook {
         err = hipErrorOutOfMemory;
       }
       done = err == hipSuccess;
-    });
+    };
+    // a small plan (PlanCap 1 on the planning thread) copies its few records
+    // here: a thread's start, join and first HIP call cost more
+    if (PlanPool::cap() == 1) body();
+    else th = std::thread(body);
   }
   void join() {
     if (th.joinable()) th.join();
