@@ -1485,6 +1485,10 @@ int dynohip_set_values(dynohip_solver* s, const uint64_t* keys, const uint8_t* k
     // process-wide pool: nothing of this handle may still run on them (the
     // speculative linearisation of the last try does)
     HIPCHK(s, hipStreamSynchronize(s->stream));
+    static const bool sync_timing = std::getenv("DYNOHIP_PLAN_TIMING") != nullptr;
+    if (sync_timing)
+      std::fprintf(stderr, "[plan] set_values stream sync      %8.2f ms\n",
+                   std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb0).count());
     s->has_plan = false;
     dynohip_graph_view g = s->graph.view();
     EarlyUpload early(s);
