@@ -563,9 +563,17 @@ struct Formulation {
 
   // ---- graph construction ----
   // Formulation::setInitialPose (Formulation-impl.hpp:83-89)
+  // (The reference ends these three updates with theta.insert_or_assign(
+  // new_values). Every other entry of new_values is in theta with the same
+  // value already: the callers start from an empty new_values, and the
+  // construction writes theta only here and through inserts that put the
+  // same value into both. So theta takes just the values the call added: a
+  // window's construction no longer re-assigns its growing new_values at
+  // every frame.)
   void set_initial_pose(uint64_t f, const P3& T, Values& new_values) {
-    values_insert(new_values, camera_pose_key(f), pose_value(T));
-    values_insert_or_assign(theta, new_values);
+    const Value v = pose_value(T);
+    values_insert(new_values, camera_pose_key(f), v);
+    theta.insert_or_assign(camera_pose_key(f), v);
   }
   // Formulation::setInitialPosePrior (Formulation-impl.hpp:91-104)
   void set_initial_pose_prior(uint64_t f, const P3& T, Graph& new_factors) {
@@ -578,8 +586,9 @@ struct Formulation {
   }
   // Formulation::addOdometry (Formulation-impl.hpp:128-161)
   void add_odometry(uint64_t f, const P3& T_world_camera, Values& new_values, Graph& new_factors) {
-    values_insert(new_values, camera_pose_key(f), pose_value(T_world_camera));
-    values_insert_or_assign(theta, new_values);
+    const Value v = pose_value(T_world_camera);
+    values_insert(new_values, camera_pose_key(f), v);
+    theta.insert_or_assign(camera_pose_key(f), v);
     DB_CHECK(f > map->first_frame_id(), DYNOHIP_ESTATE, "addOdometry at the first frame");
     P3 T_k_1;
     DB_CHECK(map->initial_sensor_pose(f - 1u, &T_k_1), DYNOHIP_ESTATE,
@@ -602,6 +611,7 @@ struct Formulation {
     DB_CHECK(fk != nullptr, DYNOHIP_ESTATE, "updateStaticObservations: frame not in map");
     P3 T_world_camera_frontend;
     DB_CHECK(map->initial_sensor_pose(k, &T_world_camera_frontend), DYNOHIP_ESTATE, "no frontend pose");
+    std::vector<std::pair<uint64_t, Value>> added;
     for (int64_t t : fk->static_landmarks) {
       const LandmarkNode& ln = map->landmarks.at(t);
       DB_CHECK(ln.is_static(), DYNOHIP_EINVAL, "Static estimate requested but landmark is dynamic!");
@@ -616,11 +626,13 @@ struct Formulation {
           internal.add(kPoseToPoint, {camera_pose_key(it->first), point_key}, it->second.data(), noise.static_point);
         double lmk_world[3];
         if (!static_landmark(t, lmk_world)) transform_from(T_world_camera_frontend, ln.measurement(k), lmk_world);
-        values_insert(new_values, point_key, point_value(lmk_world));
+        const Value v = point_value(lmk_world);
+        values_insert(new_values, point_key, v);
+        added.emplace_back(point_key, v);
         is_other_values_in_map.insert(point_key);
       }
     }
-    values_insert_or_assign(theta, new_values);
+    for (const auto& kv : added) theta.insert_or_assign(kv.first, kv.second);
     sink.commit();
   }
 
