@@ -58,8 +58,16 @@ def parse():
     ap.add_argument("--problems", type=int, default=4096, help="refine mode: (object, frame pair) problems per batch")
     ap.add_argument("--full-batch", action="store_true", help="stream mode: one full-batch solve at the last frame "
                                                              "instead of the sliding window (shipped flags)")
+    ap.add_argument("--windows-in-flight", type=int, default=3,
+                    help="stream mode, sliding window: deferred windows on K worker handles (0: the sequential "
+                         "module, each window solved inside its spin)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample (s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
+                    help="torch.distributed backend for N > 1 (nccl = RCCL; gloo: tests that run several ranks "
+                         "on one GPU)")
+    ap.add_argument("--no-phase-pass", action="store_true",
+                    help="skip the event-timed phase pass and the full-batch call timings (tests)")
     return ap.parse_args()
 
 
@@ -83,6 +91,36 @@ def host_cpu():
     except OSError:
         pass
     return n, granted, model
+
+
+class Dist:
+    """torch.distributed for the barrier and the max-over-ranks timing
+    (no data-path collective). Each rank drives GPU local_rank; with more
+    ranks than GPUs (the gloo test of N > 1 on a one-GPU box) ranks share
+    them round robin. Reductions go through CPU tensors under gloo."""
+
+    def __init__(self, backend, world, local_rank):
+        import torch
+        import torch.distributed as dist
+        self.dist = dist
+        ndev = torch.cuda.device_count()
+        self.device = local_rank if ndev >= world or ndev == 0 else local_rank % ndev
+        if ndev:
+            torch.cuda.set_device(self.device)
+        dist.init_process_group(backend=backend)
+        self.tdev = "cuda" if backend == "nccl" else "cpu"
+
+    def barrier(self):
+        self.dist.barrier()
+
+    def reduce(self, xs, op):
+        import torch
+        t = torch.tensor(xs, dtype=torch.float64, device=self.tdev)
+        self.dist.all_reduce(t, op=getattr(self.dist.ReduceOp, op))
+        return [float(x) for x in t.tolist()]
+
+    def close(self):
+        self.dist.destroy_process_group()
 
 
 def _oracle_rate(graph, values, seconds, threads):
@@ -182,7 +220,53 @@ def ns_leg(local_rank, seconds, steps=2):
             "cpu_baseline": cpu, "speedup_vs_cpu_all_cores": gpu / cpu["value"] if cpu["value"] > 0 else None}
 
 
-def stream_main(args, world, rank, local_rank, dist):
+def stream_cpu_baseline(packets, seconds):
+    """All granted cores (the baseline) and one thread (small windows factor
+    faster without the threads' hand-offs), half the sample each."""
+    nproc, cores, model = host_cpu()
+    out = _stream_cpu_sample(packets, seconds / 2, cores)
+    one = _stream_cpu_sample(packets, seconds / 2, 1)
+    out["single_thread"] = {k: one[k] for k in ("value", "unit", "cores", "sample")}
+    out["host"] = {"nproc": nproc, "cores_granted": cores, "cpu_model": model}
+    return out
+
+
+def _stream_cpu_sample(packets, seconds, cores):
+    """The stream's sliding windows solved by the oracle (CPU restatement of
+    GTSAM LM, oracle/; GTSAM itself cannot be built here)
+    on every granted core: the module replays the stream building graphs
+    only (optimize off: each triggered window's constructGraph output is
+    still exported), and each window's problem (graph + initial values: the
+    windows ignore the updater's theta, RGBDBackendModule.cc:288-300) is
+    optimised by the oracle from the same initial values. Bounded: windows
+    in stream order until `seconds` of construction + solve. Value = LM
+    iterations / (construction + oracle time)."""
+    from dynosam_amd import backend
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_binding import Oracle  # test infrastructure: the checker
+    m = backend.RGBDBackendModule(use_full_batch_opt=False, optimize=False, post_update=False)
+    iters = windows = 0
+    t_c = t_o = 0.0
+    for p in packets:
+        t0 = time.perf_counter()
+        r = m.spinOnce(p)
+        t_c += time.perf_counter() - t0
+        if r["window_end"] > r["window_start"]:
+            g, v, _ = m.lastProblem()
+            t0 = time.perf_counter()
+            iters += Oracle(g, v, threads=cores).optimize().iterations
+            t_o += time.perf_counter() - t0
+            windows += 1
+        if t_c + t_o > seconds:
+            break
+    dt = t_c + t_o
+    return {"value": iters / dt if dt > 0 else 0.0, "unit": "LM iterations/s", "cores": cores, "kind": "port",
+            "sample": f"the first {windows} sliding windows of the stream (module graph construction "
+                      f"{t_c:.2f} s + oracle LM {t_o:.2f} s on {cores} threads, {iters} LM iterations; CPU "
+                      f"restatement, oracle/, not GTSAM)"}
+
+
+def stream_main(args, world, rank, dev, D):
     """--mode stream: RGBDBackendModule (dynosam_amd.backend) replays a
     synthetic frontend stream of the config's shape — per frame Map update +
     Formulation update, and either the sliding window (shipped
@@ -191,7 +275,11 @@ def stream_main(args, world, rank, local_rank, dist):
     whole stream through a fresh module; value = LM iterations of all
     solves on all ranks / wall time (host graph construction, plan build and
     value upload are inside the timed region: this is the drop-in module's
-    end-to-end rate)."""
+    end-to-end rate). Sliding window with --windows-in-flight K > 0: the
+    module's deferred windows (offline replay: each window solved on one of
+    K worker handles while later frames are constructed; final state bit
+    for bit the sequential module's, tests/test_backend.py), the sequential
+    module (K = 0, per-spin outputs as the reference) timed beside it."""
     import torch
     from dynosam_amd import backend, stream, synth
 
@@ -200,45 +288,54 @@ def stream_main(args, world, rank, local_rank, dist):
                               dyn_slots=c["dyn_slots"], object_visible_frames=c.get("object_visible_frames", 0),
                               seed=42 + rank)
     packets, _ = stream.generate(cfg)
+    wif = 0 if args.full_batch else args.windows_in_flight
 
-    def replay():
+    def replay(k):
         m = backend.RGBDBackendModule(use_full_batch_opt=args.full_batch, full_batch_frame=len(packets),
-                                      optimize=True, device_id=local_rank, post_update=False)
+                                      optimize=True, device_id=dev, post_update=False, windows_in_flight=k)
         it = inner = solves = 0
         ms_c = ms_o = 0.0
-        for p in packets:
-            r = m.spinOnce(p)
+        rs = [m.spinOnce(p) for p in packets]
+        if k:
+            rs.append(m.flush())
+        for r in rs:
             ms_c += r["ms_construct"]
             if r["optimized"]:
                 it += r["iterations"]
                 inner += r["inner_iterations"]
-                solves += 1
+                solves += max(r["windows_merged"], 1)
                 ms_o += r["ms_optimize"]
         return it, inner, solves, ms_c, ms_o
 
     def barrier():
-        if dist is not None:
-            dist.barrier()
+        if D is not None:
+            D.barrier()
         torch.cuda.synchronize()
 
+    def timed(k, steps):
+        barrier()
+        t0 = time.perf_counter()
+        tot = [0, 0, 0, 0.0, 0.0]
+        for _ in range(steps):
+            tot = [a + b for a, b in zip(tot, replay(k))]
+        barrier()
+        dt = time.perf_counter() - t0
+        if D is not None:
+            dt = D.reduce([dt], "MAX")[0]
+            tot[:3] = [int(x) for x in D.reduce(tot[:3], "SUM")]
+        return dt, tot
+
     for _ in range(args.warmup):
-        replay()
-    barrier()
-    t0 = time.perf_counter()
-    iters = inner = solves = 0
-    ms_c = ms_o = 0.0
-    for _ in range(args.steps):
-        a, b, n, c1, c2 = replay()
-        iters, inner, solves, ms_c, ms_o = iters + a, inner + b, solves + n, ms_c + c1, ms_o + c2
-    barrier()
-    dt = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-        cnt = torch.tensor([iters, inner, solves], dtype=torch.float64, device="cuda")
-        dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
-        iters, inner, solves = (int(x) for x in cnt.tolist())
+        replay(wif)
+    dt, (iters, inner, solves, ms_c, ms_o) = timed(wif, args.steps)
+    seq = None
+    if wif:
+        replay(0)
+        sdt, (s_it, _, _, s_c, _) = timed(0, args.steps)
+        seq = {"value": s_it / sdt, "unit": "LM iterations/s", "ms_per_step": 1e3 * sdt / args.steps,
+               "ms_per_frame_construction": s_c / (args.steps * len(packets)),
+               "note": "the sequential module (windows_in_flight 0: each window solved and merged inside its "
+                       "spin, per-spin outputs as the reference), same stream, same protocol"}
     if rank == 0:
         out = {
             "metric": "LM iterations/sec + ms/iter, full-batch dynamic factor graph",
@@ -252,16 +349,21 @@ def stream_main(args, world, rank, local_rank, dist):
             "data": "synthetic frontend stream (dynosam_amd.stream, seed 42 + rank)",
             "config": {"workload": f"{args.config}-shaped stream through RGBDBackendModule, "
                                    + ("full batch at the last frame" if args.full_batch else
-                                      "sliding window 10 / overlap 4 (backend.flags)"),
-                       "frames": cfg.frames, "objects": cfg.objects,
+                                      "sliding window 10 / overlap 4 (backend.flags)"
+                                      + (f", deferred windows on {wif} worker handles" if wif else "")),
+                       "frames": cfg.frames, "objects": cfg.objects, "windows_in_flight": wif,
                        "parallelism": f"stream-sharded x{world} (one module per rank, no data-path collective)"},
         }
+        if seq is not None:
+            out["sequential"] = seq
+        if world == 1 and not args.no_cpu_baseline and not args.full_batch:
+            out["cpu_baseline"] = stream_cpu_baseline(packets, args.cpu_seconds)
         print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    if D is not None:
+        D.close()
 
 
-def refine_main(args, world, rank, local_rank, dist):
+def refine_main(args, world, rank, dev, D):
     """--mode refine: the batched frontend object-motion refinement
     (dynosam_amd.refine). One step = one batch of
     `--problems` MotionOnlyRefinementOptimizer problems (20-60 tracklets
@@ -273,14 +375,14 @@ def refine_main(args, world, rank, local_rank, dist):
     from dynosam_amd import refine
 
     batch = refine.synthetic_batch(args.problems, tracks=(20, 60), seed=42 + rank)
-    opt = refine.MotionOnlyRefinementOptimizer(device=local_rank)
+    opt = refine.MotionOnlyRefinementOptimizer(device=dev)
     opt.upload(batch)
     for _ in range(args.warmup):
         opt.solve()
 
     def barrier():
-        if dist is not None:
-            dist.barrier()
+        if D is not None:
+            D.barrier()
         torch.cuda.synchronize()
 
     barrier()
@@ -293,10 +395,8 @@ def refine_main(args, world, rank, local_rank, dist):
     H, flags, res = opt.download()
     iters = sum(r["iterations"] for r in res)
     inner = sum(r["inner_iterations"] for r in res)
-    if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    if D is not None:
+        dt = D.reduce([dt], "MAX")[0]
     n_total = args.problems * args.steps * world
     if rank == 0:
         out = {
@@ -327,8 +427,8 @@ def refine_main(args, world, rank, local_rank, dist):
                                    "sample": f"first {n} problems of the batch, numpy restatement (oracle/refine.py, "
                                              f"dense solve), {cdt:.1f} s"}
         print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    if D is not None:
+        D.close()
 
 
 def main():
@@ -341,15 +441,12 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
 
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group(backend="nccl")
+    D = Dist(args.backend, world, local_rank) if world > 1 else None
+    dev = D.device if D is not None else local_rank
     if args.mode == "stream":
-        return stream_main(args, world, rank, local_rank, dist)
+        return stream_main(args, world, rank, dev, D)
     if args.mode == "refine":
-        return refine_main(args, world, rank, local_rank, dist)
+        return refine_main(args, world, rank, dev, D)
     from dynosam_amd import synth
     from dynosam_amd.graph import NonlinearFactorGraph
     from dynosam_amd.optimizer import Solver
@@ -357,16 +454,16 @@ def main():
     graph, values, _ = synth.generate(args.config, seed=42 if parted else 42 + rank)
     if parted and world > 1:
         from dynosam_amd.partitioned import PartitionedSolver, TorchAllReduce
-        solver = PartitionedSolver(local_rank, world, rank, TorchAllReduce(local_rank))
+        solver = PartitionedSolver(dev, world, rank, TorchAllReduce(dev))
     else:
-        solver = Solver(local_rank)
+        solver = Solver(dev)
     solver.set_graph(graph)
     solver.set_values(values)
     solver.snapshot()
 
     def barrier():
-        if dist is not None:
-            dist.barrier()
+        if D is not None:
+            D.barrier()
         torch.cuda.synchronize()
 
     for _ in range(args.warmup):
@@ -384,15 +481,38 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
 
-    if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    if D is not None:
+        dt = D.reduce([dt], "MAX")[0]
         if not parted:  # partitioned: every rank ran the same LM iterations
-            c = torch.tensor([iters, inner], dtype=torch.float64, device="cuda")
-            dist.all_reduce(c, op=dist.ReduceOp.SUM)
-            iters, inner = int(c[0].item()), int(c[1].item())
+            iters, inner = (int(x) for x in D.reduce([iters, inner], "SUM"))
     nshare = 1 if parted else world   # ranks whose iterations make up `iters`
+    base = {
+        "metric": "LM iterations/sec + ms/iter, full-batch dynamic factor graph",
+        "value": iters / dt,
+        "unit": "LM iterations/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * dt / args.steps,
+        "ms_per_iter": 1e3 * dt * nshare / max(iters, 1),
+        "ms_per_inner_iter": 1e3 * dt * nshare / max(inner, 1),
+        "lm_iterations_per_step": iters / (args.steps * nshare),
+        "inner_iterations_per_step": inner / (args.steps * nshare),
+        "higher_is_better": True,
+        "scaling": "strong" if parted else "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (in-repo deterministic generator, SURVEY.md §8(d); seed "
+                + ("42, one graph split over the ranks)" if parted else "42 + rank)"),
+    }
+    if args.no_phase_pass:
+        if rank == 0:
+            base["config"] = {"workload": f"{args.config}: full-batch LM", "parallelism":
+                              f"{'partitioned' if parted else 'window-sharded'} x{world} ({args.backend})"}
+            print(json.dumps(base), flush=True)
+        if D is not None:
+            D.close()
+        return
 
     # phase breakdown (separate, event-timed pass; not part of the timed region)
     solver.restore()
@@ -402,8 +522,8 @@ def main():
     solver.set_timing(False)
 
     if rank != 0:
-        if dist is not None:
-            dist.destroy_process_group()
+        if D is not None:
+            D.close()
         return
 
     phases = {
@@ -475,13 +595,17 @@ def main():
     # persistent handle (device buffers reused across calls, as the drop-in
     # adapter keeps one handle per backend module); the same
     # with a fresh handle created and destroyed inside the call beside it
-    # (calls 2 and 3 on the persistent handle see the structure it planned
-    # and keep that plan, dynohip_set_graph); _replan alternates the graph
-    # with the same factors in reversed order per type, a different structure
-    # for the planner each call, so every call plans in full
+    # The reference constructs its optimiser once per full-batch run
+    # (RGBDBackendModule.cc:201-221) on a graph the handle has not planned,
+    # so the headline figure plans in full every call: the graph alternates
+    # with the same factors in reversed order per type, a different
+    # structure for the planner each call. _fresh_handle adds handle
+    # creation and destruction; _kept_plan (secondary) repeats one graph,
+    # whose plan the handle keeps (dynohip_set_graph), which the reference's
+    # call pattern never does.
     t_fb, t_fb_fresh, t_fb_replan = [], [], []
     if not (parted and world > 1):
-        fb = Solver(local_rank)
+        fb = Solver(dev)
         for _ in range(3):
             t0 = time.perf_counter()
             fb.set_graph(graph)
@@ -501,7 +625,7 @@ def main():
         fb.close()
         for _ in range(2):
             t0 = time.perf_counter()
-            fb = Solver(local_rank)
+            fb = Solver(dev)
             fb.set_graph(graph)
             fb.set_values(values)
             fb.optimize()
@@ -509,24 +633,8 @@ def main():
             fb.close()
             t_fb_fresh.append(time.perf_counter() - t0)
 
-    out = {
-        "metric": "LM iterations/sec + ms/iter, full-batch dynamic factor graph",
-        "value": iters / dt,
-        "unit": "LM iterations/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": 1e3 * dt / args.steps,
-        "ms_per_iter": 1e3 * dt * nshare / max(iters, 1),
-        "ms_per_inner_iter": 1e3 * dt * nshare / max(inner, 1),
-        "lm_iterations_per_step": iters / (args.steps * nshare),
-        "inner_iterations_per_step": inner / (args.steps * nshare),
-        "higher_is_better": True,
-        "scaling": "strong" if parted else "weak",
-        "vs_baseline": None,
-        "dtype": "f64",
-        "data": "synthetic (in-repo deterministic generator, SURVEY.md §8(d); seed "
-                + ("42, one graph split over the ranks)" if parted else "42 + rank)"),
+    out = dict(base)
+    out.update({
         "config": {
             "workload": f"{args.config}: full-batch LM, WorldMotion formulation, backend.flags noise; "
                         f"{st['n_pose']} poses, {int((values.kinds == 1).sum())} points, {graph.size()} factors",
@@ -537,26 +645,26 @@ def main():
                             f"the separator system per solve)" if parted else
                             f"window-sharded x{world} (independent graphs, no data-path collective)"),
         },
-        "ms_full_batch_opt": 1e3 * min(t_fb) if t_fb else None,
+        "ms_full_batch_opt": 1e3 * min(t_fb_replan) if t_fb_replan else None,
         "ms_full_batch_opt_fresh_handle": 1e3 * min(t_fb_fresh) if t_fb_fresh else None,
-        "ms_full_batch_opt_replan": 1e3 * min(t_fb_replan) if t_fb_replan else None,
+        "ms_full_batch_opt_kept_plan": 1e3 * min(t_fb) if t_fb else None,
         "ms_full_batch_opt_note": "one LevenbergMarquardtOptimizer(graph, values).optimize() call as the reference "
                                   "times it (construction = host planning + upload, optimize, values read back) on "
-                                  "the backend's persistent handle, best of 3, outside the timed region (the graph "
-                                  "repeats, so the handle keeps its plan and refreshes the factor records); "
-                                  "_replan: the same with a full re-plan every call (graph structure alternated); "
-                                  "_fresh_handle adds handle creation and destruction (full plan)",
+                                  "the backend's persistent handle, a graph structure it has not planned (a full "
+                                  "plan every call, as the reference's one call per run), best of 4, outside the "
+                                  "timed region; _fresh_handle adds handle creation and destruction; _kept_plan "
+                                  "(secondary): the same graph again, whose plan the handle keeps",
         "phases_ms_per_optimize": {k: round(v, 4) for k, v in phases.items()},
         "roofline": roof,
         "phase_rooflines": phase_rooflines,
-    }
+    })
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(graph, values, args.cpu_seconds)
         if args.config == "C2" and not parted:
-            out["north_star"] = ns_leg(local_rank, args.cpu_seconds)
+            out["north_star"] = ns_leg(dev, args.cpu_seconds)
     print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    if D is not None:
+        D.close()
 
 
 if __name__ == "__main__":

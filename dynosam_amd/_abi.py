@@ -231,7 +231,7 @@ class ModuleParams(C.Structure):
         ("optimize", C.c_int),
         ("device_id", C.c_int),
         ("post_update", C.c_int),
-        ("reserved", C.c_int),
+        ("windows_in_flight", C.c_int),
         ("lm", LMParams),
     ]
 
@@ -241,7 +241,7 @@ class SpinResult(C.Structure):
         ("optimized", C.c_int),
         ("iterations", C.c_int),
         ("inner_iterations", C.c_int),
-        ("reserved", C.c_int),
+        ("windows_merged", C.c_int),
         ("window_start", C.c_uint64),
         ("window_end", C.c_uint64),
         ("error_before", C.c_double),

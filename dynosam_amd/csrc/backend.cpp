@@ -11,6 +11,8 @@
 #include <algorithm>
 #include <array>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
 #include <fstream>
 #include <sstream>
 #include <iterator>
@@ -18,11 +20,13 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <set>
 #include <unordered_map>
 #include <unordered_set>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/dynobackend.h"
@@ -84,6 +88,12 @@ struct LandmarkNode {
   std::map<uint64_t, std::array<double, 3>> measurements;
   bool is_static() const { return object_id == kBackgroundLabel; }
   size_t num_observations() const { return measurements.size(); }
+  // the observations a spin at frame `horizon` saw (frames arrive in order,
+  // so a map read later holds the later frames' measurements too)
+  size_t num_observations_upto(uint64_t horizon) const {
+    if (measurements.empty() || measurements.rbegin()->first <= horizon) return measurements.size();
+    return static_cast<size_t>(std::distance(measurements.begin(), measurements.upper_bound(horizon)));
+  }
   bool seen_at(uint64_t f) const { return measurements.count(f) != 0; }
   const double* measurement(uint64_t f) const {
     auto it = measurements.find(f);
@@ -461,6 +471,16 @@ struct Formulation {
 
   bool motion_formulation() const { return params.formulation == DYNOB_MOTION_IN_WORLD; }
 
+  // The last frame the map holds for this formulation's reads: the module's
+  // deferred-window mode runs a frame's construction (and post-update) after
+  // later frames have entered the map, and reads it as of that frame; a
+  // construction at spin time (every other caller) sees no later frame, so
+  // there the horizon is the whole map.
+  uint64_t horizon = ~0ull;
+  size_t observations(const LandmarkNode& ln) const {
+    return horizon == ~0ull ? ln.num_observations() : ln.num_observations_upto(horizon);
+  }
+
   // ---- accessor (Accessor-impl.hpp, WorldPoseEstimator.cc:31-81,
   //      WorldMotionEstimator.cc:32-66) ----
   const Value* query(uint64_t key) const {
@@ -619,7 +639,7 @@ struct Formulation {
       if (is_other_values_in_map.count(point_key)) {
         internal.add(kPoseToPoint, {camera_pose_key(k), point_key}, ln.measurement(k), noise.static_point);
       } else {
-        if (static_cast<int64_t>(ln.num_observations()) < params.min_static_observations) continue;
+        if (static_cast<int64_t>(observations(ln)) < params.min_static_observations) continue;
         // seen frames, ascending, up to k (only k itself without backtracking)
         for (auto it = do_backtrack ? ln.measurements.begin() : ln.measurements.lower_bound(k);
              it != ln.measurements.end() && it->first <= k; ++it)
@@ -799,7 +819,7 @@ struct Formulation {
       if (seen_k.size() < kMinNumberPoints || map->object_landmarks_at(obj, k_1).size() < kMinNumberPoints) continue;
       for (int64_t t : seen_k) {
         const LandmarkNode& ln = map->landmarks.at(t);
-        if (static_cast<int64_t>(ln.num_observations()) < params.min_dynamic_observations) continue;
+        if (static_cast<int64_t>(observations(ln)) < params.min_dynamic_observations) continue;
         if (!is_dynamic_tracklet_in_map.count(t)) {
           const uint64_t first = ln.measurements.begin()->first;
           uint64_t start;
@@ -814,6 +834,9 @@ struct Formulation {
                    "Starting motion frame is " + std::to_string(start) + " but first frame is " +
                        std::to_string(first));
           for (auto it = start_it; it != ln.measurements.end(); ++it) {
+            // (a frame the spin at `horizon` had not seen yet: stop before
+            // its consecutiveness check, as that spin would have)
+            if (horizon != ~0ull && it->first > horizon) break;
             auto prev = std::prev(it);
             DB_CHECK(it->first == prev->first + 1u, DYNOHIP_ESTATE,
                      "tracklet " + std::to_string(t) + " is not seen in consecutive frames");
@@ -905,7 +928,7 @@ struct Formulation {
   void post_update() {
     if (!motion_formulation()) return;  // WorldPoseAccessor has no cache
     std::map<int32_t, std::map<uint64_t, P3>> object_poses;
-    if (map->frames.size() < 2) {
+    if (map->frames.size() < 2 || std::next(map->frames.begin())->first > horizon) {
       object_pose_cache = object_poses;
       return;
     }
@@ -914,7 +937,7 @@ struct Formulation {
     // changes the estimates), and a frame without motions needs neither
     std::map<int32_t, std::array<double, 3>> c_prev;
     bool have_prev = false;
-    for (; it != map->frames.end(); ++it) {
+    for (; it != map->frames.end() && it->first <= horizon; ++it) {
       const uint64_t k = it->first, k_1 = std::prev(it)->first;
       DB_CHECK(k_1 + 1 == k, DYNOHIP_ESTATE, "map frames are not consecutive");
       // getObjectMotions(k): objects seen at k with a motion estimate
@@ -1043,6 +1066,135 @@ struct dynob_map {
 struct dynob_formulation {
   std::unique_ptr<Formulation> f;
 };
+namespace dynob {
+
+// ---- deferred sliding windows (dynob_module_params.windows_in_flight > 0) ----
+//
+// A window's graph and initial values come from the map alone
+// (constructGraph builds a fresh updater over [start, end],
+// RGBDBackendModule.cc:246-296), so its LM solve can run while later frames
+// arrive. What must keep the reference's order is the persistent updater's
+// theta: every spin inserts the frame's new values, a window's solve is
+// merged with insert_or_assign (RGBDBackendModule.cc:241,
+// Formulation-impl.hpp:53-60), and a later frame's construction reads the
+// merged camera poses (getInitialOrLinearizedSensorPose). So the module
+// queues the updater's work as operations (the frame's construction, the
+// window's merge, the post-update) in spin order and runs them in that
+// order, a merge only once its window's solve is done, each frame's reads of
+// the map taken as of that frame (Formulation::horizon). The updater then
+// performs the same sequence of operations on the same inputs as the
+// sequential module, and ends with the same theta bit for bit; only the time
+// at which each operation runs (and so each spin's output) lags.
+
+struct WindowJob {
+  uint64_t start = 0, end = 0;
+  GraphExport graph;          // the window's getGraph() / getTheta() copies
+  ValuesExport values;
+  std::vector<double> optimised;
+  dynohip_lm_summary summary{};
+  int rc = DYNOHIP_OK;
+  std::string err;
+  double ms_solve = 0.0;      // set_graph .. get_values on the worker
+  double ms_construct = 0.0;  // the window's construction on the spin's thread
+  std::mutex mu;
+  std::condition_variable cv;
+  bool done = false;
+  void wait() {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return done; });
+  }
+  bool ready() {
+    std::lock_guard<std::mutex> lk(mu);
+    return done;
+  }
+};
+
+// Worker threads, each with its own solver handle (own HIP stream and device
+// buffers), taking window jobs in submission order: several windows' LM runs
+// are in flight on the device at once (one 10-frame window's kernels occupy a
+// handful of CUs).
+class WindowWorkers {
+ public:
+  WindowWorkers(int n, int device, const dynohip_lm_params& lm) : device_(device), lm_(lm) {
+    for (int i = 0; i < n; ++i) threads_.emplace_back([this] { loop(); });
+  }
+  ~WindowWorkers() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : threads_) t.join();
+  }
+  void submit(std::shared_ptr<WindowJob> j) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      q_.push_back(std::move(j));
+    }
+    cv_.notify_one();
+  }
+
+ private:
+  void loop() {
+    dynohip_solver* solver = nullptr;
+    for (;;) {
+      std::shared_ptr<WindowJob> j;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+        if (q_.empty()) break;   // stopping, nothing left
+        j = std::move(q_.front());
+        q_.pop_front();
+      }
+      run(j.get(), solver);
+      {
+        std::lock_guard<std::mutex> lk(j->mu);
+        j->done = true;
+      }
+      j->cv.notify_all();
+    }
+    if (solver) dynohip_destroy(solver);
+  }
+  void run(WindowJob* j, dynohip_solver*& solver) {
+    const auto t0 = std::chrono::steady_clock::now();
+    int rc = DYNOHIP_OK;
+    if (!solver) rc = dynohip_create(device_, &solver);
+    if (rc != DYNOHIP_OK) {
+      j->rc = rc;
+      j->err = "dynohip_create failed";
+      return;
+    }
+    dynohip_graph_view gv;
+    j->graph.view(&gv);
+    rc = dynohip_set_graph(solver, &gv);
+    if (rc == DYNOHIP_OK)
+      rc = dynohip_set_values(solver, j->values.keys.data(), j->values.kinds.data(), j->values.data.data(),
+                              j->values.keys.size());
+    if (rc == DYNOHIP_OK) rc = dynohip_optimize(solver, &lm_, &j->summary);
+    j->optimised.assign(j->values.data.size(), 0.0);
+    if (rc == DYNOHIP_OK) rc = dynohip_get_values(solver, j->optimised.data(), j->optimised.size());
+    if (rc != DYNOHIP_OK) j->err = std::string("LM solve failed: ") + dynohip_last_error(solver);
+    j->rc = rc;
+    j->ms_solve = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+  std::vector<std::thread> threads_;
+  std::deque<std::shared_ptr<WindowJob>> q_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  bool stop_ = false;
+  int device_;
+  dynohip_lm_params lm_;
+};
+
+// One queued operation of the persistent updater (deferred-window mode)
+struct ModuleOp {
+  enum Kind { kBootstrap, kFrame, kMerge, kPostUpdate } kind;
+  uint64_t k = 0;                    // the spin's frame
+  std::shared_ptr<WindowJob> job;    // kMerge
+};
+
+}  // namespace dynob
+
 struct dynob_module {
   dynob_params params;
   dynob_module_params mp;
@@ -1052,6 +1204,11 @@ struct dynob_module {
   bool bootstrapped = false;
   dynohip_solver* solver = nullptr;
   std::string err;
+  // deferred-window mode: the updater's pending operations in spin order,
+  // the windows being solved, and the workers (created on the first window)
+  std::deque<ModuleOp> ops;
+  size_t windows_pending = 0;
+  std::unique_ptr<WindowWorkers> workers;
   // last solved problem
   GraphExport last_graph;
   ValuesExport last_values;
@@ -1128,6 +1285,23 @@ void export_problem(dynob_module* m, const Formulation& problem) {
   m->last_optimised = m->last_values.data;
 }
 
+// Formulation::updateTheta (Formulation-impl.hpp:53-60): insert_or_assign of
+// a solved problem's values
+void update_theta(Formulation& up, const ValuesExport& vals, const std::vector<double>& optimised) {
+  Values opt;
+  size_t off = 0;
+  for (size_t i = 0; i < vals.keys.size(); ++i) {
+    Value v;
+    std::memset(&v, 0, sizeof(v));
+    v.kind = vals.kinds[i];
+    const size_t len = v.kind == DYNOHIP_POSE3 ? 12 : 3;
+    std::memcpy(v.d, optimised.data() + off, len * sizeof(double));
+    off += len;
+    opt[vals.keys[i]] = v;
+  }
+  values_insert_or_assign(up.theta, opt);
+}
+
 // LM on the exported problem (export_problem first), then updateTheta
 int solve(dynob_module* m, dynob_spin_result* r) {
   if (!m->mp.optimize) return DYNOHIP_OK;
@@ -1159,20 +1333,157 @@ int solve(dynob_module* m, dynob_spin_result* r) {
   r->error_before = s.initial_error;
   r->error_after = s.final_error;
   r->ms_optimize = now_ms() - t0;
-  // Formulation::updateTheta (Formulation-impl.hpp:53-60): insert_or_assign
-  Values opt;
-  size_t off = 0;
-  for (size_t i = 0; i < m->last_values.keys.size(); ++i) {
-    Value v;
-    std::memset(&v, 0, sizeof(v));
-    v.kind = m->last_values.kinds[i];
-    const size_t len = v.kind == DYNOHIP_POSE3 ? 12 : 3;
-    std::memcpy(v.d, m->last_optimised.data() + off, len * sizeof(double));
-    off += len;
-    opt[m->last_values.keys[i]] = v;
-  }
-  values_insert_or_assign(m->updater.f->theta, opt);
+  update_theta(*m->updater.f, m->last_values, m->last_optimised);
   return DYNOHIP_OK;
+}
+
+// TimingStatsCollector's samples for an interval measured elsewhere (a window
+// solved on a worker thread): whole milliseconds and the nanosecond twin
+void record_interval(Statistics& st, const std::string& tag, double ms) {
+  st.samples[tag + " [ms]"].push_back(std::floor(ms));
+  st.ns[tag + " [ns]"].push_back(std::floor(ms * 1e6));
+}
+
+// RGBDBackendModule::nominalSpinImpl's graph construction for frame k
+// (RGBDBackendModule.cc:154-199): odometry, static and dynamic observations
+void construct_frame(dynob_module* m, uint64_t k, const P3& T_k) {
+  Formulation& up = *m->updater.f;
+  Values nv;
+  Graph nf;
+  nf.discard = true;   // the spin's new factors are only kept in the updater's factors_
+  up.add_odometry(k, T_k, nv, nf);
+  {
+    TimingStatsCollector timer(m->stats, "backend.update_static_obs");
+    up.update_static(k, nv, nf, false);
+  }
+  {
+    TimingStatsCollector timer(m->stats, "backend.update_dynamic_obs");
+    up.update_dynamic(k, nv, nf, false);
+  }
+}
+
+// deferred-window mode: the merge of a solved window into the persistent
+// updater, as the sequential spin's solve() ends (updateTheta), with its
+// statistics; the spin result sums the windows merged during the spin
+void merge_window(dynob_module* m, WindowJob& j, dynob_spin_result* r) {
+  DB_CHECK(j.rc == DYNOHIP_OK, j.rc, j.err);
+  const double t0 = now_ms();
+  update_theta(*m->updater.f, j.values, j.optimised);
+  record_interval(m->stats, m->name() + ".sliding_window_optimise", j.ms_solve + (now_ms() - t0));
+  r->optimized = 1;
+  r->windows_merged += 1;
+  r->iterations += static_cast<int>(j.summary.iterations);
+  r->inner_iterations += static_cast<int>(j.summary.inner_iterations);
+  r->window_start = j.start;
+  r->window_end = j.end;
+  r->error_before = j.summary.initial_error;
+  r->error_after = j.summary.final_error;
+  r->ms_optimize += j.ms_solve;
+  // the last solved problem is this window's
+  m->last_graph = std::move(j.graph);
+  m->last_values = std::move(j.values);
+  m->last_optimised = std::move(j.optimised);
+}
+
+// one queued updater operation, its map reads as of its spin's frame
+void run_op(dynob_module* m, ModuleOp& op, dynob_spin_result* r) {
+  Formulation& up = *m->updater.f;
+  struct Horizon {
+    Formulation& f;
+    ~Horizon() { f.horizon = ~0ull; }
+  } reset{up};
+  up.horizon = op.k;
+  const FrameNode* fn = m->map.map.frame(op.k);
+  switch (op.kind) {
+    case ModuleOp::kBootstrap: {
+      Values nv;
+      Graph nf;
+      nf.discard = true;
+      up.set_initial_pose(op.k, fn->X_world, nv);
+      up.set_initial_pose_prior(op.k, fn->X_world, nf);
+      break;
+    }
+    case ModuleOp::kFrame: {
+      const double t0 = now_ms();
+      construct_frame(m, op.k, fn->X_world);
+      r->ms_construct += now_ms() - t0;
+      break;
+    }
+    case ModuleOp::kMerge:
+      merge_window(m, *op.job, r);
+      break;
+    case ModuleOp::kPostUpdate: {
+      TimingStatsCollector post_timer(m->stats, m->name() + ".post_update");
+      up.post_update();
+      break;
+    }
+  }
+}
+
+// runs the queued operations in order; a merge whose window is still being
+// solved stops the run unless more than `max_pending` windows are
+// outstanding, in which case it waits for that window
+void drain(dynob_module* m, dynob_spin_result* r, size_t max_pending) {
+  while (!m->ops.empty()) {
+    ModuleOp& head = m->ops.front();
+    if (head.kind == ModuleOp::kMerge && !head.job->ready()) {
+      if (m->windows_pending <= max_pending) break;
+      head.job->wait();
+    }
+    ModuleOp op = std::move(head);
+    m->ops.pop_front();
+    if (op.kind == ModuleOp::kMerge) --m->windows_pending;
+    run_op(m, op, r);
+  }
+}
+
+bool deferred(const dynob_module* m) {
+  return m->mp.windows_in_flight > 0 && !m->mp.use_full_batch_opt && m->mp.optimize;
+}
+
+// windows allowed to wait for their merge before a spin blocks on the oldest
+size_t max_pending(const dynob_module* m) { return 4 * static_cast<size_t>(m->mp.windows_in_flight); }
+
+// The deferred-window spin after the map update (see WindowJob): the frame's
+// updater work is queued, a triggered window is constructed from the map now
+// and solved on a worker, and the queue runs as far as the solved windows
+// allow.
+void spin_deferred(dynob_module* m, uint64_t k, dynob_spin_result* r) {
+  if (!m->bootstrapped) {
+    uint64_t s, e;
+    DB_CHECK(dynohip_sliding_window_check(&m->window, k, &s, &e) == 0, DYNOHIP_ESTATE,
+             "sliding window triggered on the first frame");
+    m->ops.push_back({ModuleOp::kBootstrap, k, nullptr});
+    m->bootstrapped = true;
+    drain(m, r, max_pending(m));
+    return;
+  }
+  m->ops.push_back({ModuleOp::kFrame, k, nullptr});
+  uint64_t s = 0, e = 0;
+  const int wc = dynohip_sliding_window_check(&m->window, k, &s, &e);
+  DB_CHECK(wc >= 0, DYNOHIP_EINVAL, "SlidingWindow::check: window starts before the first frame");
+  if (wc == 1) {
+    const std::string name = m->name();
+    auto job = std::make_shared<WindowJob>();
+    job->start = s;
+    job->end = e;
+    const double tc = now_ms();
+    {
+      TimingStatsCollector timer(m->stats, name + ".sliding_window_construction");
+      std::unique_ptr<Formulation> window = construct_graph(&m->map.map, m->params, s, e, true);
+      job->graph.build(window->factors);
+      job->values.build(window->theta);
+      m->stats.add(name + ".sliding_window_optimise_num_vars_all", static_cast<double>(window->theta.size()));
+    }
+    job->ms_construct = now_ms() - tc;
+    r->ms_construct += job->ms_construct;
+    if (!m->workers) m->workers = std::make_unique<WindowWorkers>(m->mp.windows_in_flight, m->mp.device_id, m->mp.lm);
+    m->workers->submit(job);
+    m->ops.push_back({ModuleOp::kMerge, k, job});
+    ++m->windows_pending;
+  }
+  if (m->mp.post_update) m->ops.push_back({ModuleOp::kPostUpdate, k, nullptr});
+  drain(m, r, max_pending(m));
 }
 
 }  // namespace
@@ -1728,6 +2039,7 @@ void dynob_module_params_default(dynob_module_params* p) {
 int dynob_module_create(const dynob_params* p, const dynob_module_params* mp, dynob_module** out) {
   if (!out || !mp || !params_valid(p)) return DYNOHIP_EINVAL;
   if (!mp->use_full_batch_opt && (mp->opt_window_size <= 0 || mp->opt_window_overlap < 0)) return DYNOHIP_EINVAL;
+  if (mp->windows_in_flight < 0 || mp->windows_in_flight > 16) return DYNOHIP_EINVAL;
   auto* m = new dynob_module();
   m->params = *p;
   m->mp = *mp;
@@ -1768,6 +2080,7 @@ int dynob_module_spin(dynob_module* m, const dynob_input_packet* in, dynob_spin_
     for (size_t i = 0; i < in->n_motions; ++i) fn.motions_world[in->motion_object_ids[i]] = pose_from(in->motions12 + 12 * i);
     map_timer.stop();
     const P3 T_k = fn.X_world;
+    if (deferred(m)) return spin_deferred(m, k, r);
     Values nv;
     Graph nf;
     nf.discard = true;   // the spin's new factors are only kept in the updater's factors_
@@ -1782,15 +2095,7 @@ int dynob_module_spin(dynob_module* m, const dynob_input_packet* in, dynob_spin_
       return;
     }
     // nominalSpinImpl (RGBDBackendModule.cc:154-262)
-    up.add_odometry(k, T_k, nv, nf);
-    {
-      TimingStatsCollector timer(m->stats, "backend.update_static_obs");
-      up.update_static(k, nv, nf, false);
-    }
-    {
-      TimingStatsCollector timer(m->stats, "backend.update_dynamic_obs");
-      up.update_dynamic(k, nv, nf, false);
-    }
+    construct_frame(m, k, T_k);
     r->ms_construct = now_ms() - t0;
     const std::string name = m->name();
     if (m->mp.use_full_batch_opt) {
@@ -1834,6 +2139,18 @@ int dynob_module_spin(dynob_module* m, const dynob_input_packet* in, dynob_spin_
     TimingStatsCollector post_timer(m->stats, name + ".post_update");
     if (m->mp.post_update) up.post_update();
   });
+}
+
+int dynob_module_flush(dynob_module* m, dynob_spin_result* r) {
+  if (!m) return DYNOHIP_EINVAL;
+  dynob_spin_result local;
+  if (!r) r = &local;
+  std::memset(r, 0, sizeof(*r));
+  return guard(m->err, [&] { drain(m, r, 0); });
+}
+
+int dynob_module_pending(const dynob_module* m) {
+  return m ? static_cast<int>(m->ops.size()) : DYNOHIP_EINVAL;
 }
 
 // Statistics::WriteAllSamplesToCsvFile (Statistics.cc:352-381) through

@@ -53,10 +53,14 @@ namespace {
 
 // owner merge over the tiles a factor or chain touches: a rank (its
 // interior) wins over a separator node (one of the rank's ancestors: a
-// separator is adjacent only to the subtrees it splits); two ranks, or two
-// separator nodes, conflict
+// separator is adjacent only to the subtrees it splits); of two separator
+// nodes on one root path the deeper one wins (a left subtree's reach is
+// clipped at its end, so a depth-2 separator's tiles can neighbour the top
+// separator's: the deeper node's leader is a member of every ancestor's
+// group, and the ancestor's slots are exchanged at their own, later depth);
+// two ranks, or two separator nodes on different paths, conflict
 constexpr int32_t kOwnNone = INT32_MIN, kOwnConflict = INT32_MIN + 1;
-int32_t merge_owner(int32_t a, int32_t b) {
+int32_t merge_owner(int32_t a, int32_t b, const std::vector<SepNode>& nodes) {
   if (a == kOwnNone) return b;
   if (b == kOwnNone) return a;
   if (a == kOwnConflict || b == kOwnConflict) return kOwnConflict;
@@ -64,6 +68,13 @@ int32_t merge_owner(int32_t a, int32_t b) {
   if (a >= 0 && b >= 0) return kOwnConflict;
   if (a >= 0) return a;
   if (b >= 0) return b;
+  const SepNode& na = nodes[sep_node(a)];
+  const SepNode& nb = nodes[sep_node(b)];
+  auto within = [](const SepNode& in, const SepNode& out) {
+    return in.r0 >= out.r0 && in.r0 + in.nr <= out.r0 + out.nr;
+  };
+  if (within(na, nb)) return a;   // a is the deeper node of the path
+  if (within(nb, na)) return b;
   return kOwnConflict;
 }
 
@@ -111,7 +122,7 @@ int build_partitioned_plan(const dynohip_graph_view& g, const uint64_t* keys, co
   part.rank = rank;
   auto pose_owner = [&](int32_t p) {
     int32_t o = kOwnNone;
-    for (int t = (6 * p) / kTile; t <= (6 * p + 5) / kTile; ++t) o = merge_owner(o, towner[t]);
+    for (int t = (6 * p) / kTile; t <= (6 * p + 5) / kTile; ++t) o = merge_owner(o, towner[t], nodes);
     return o;
   };
   // a separator node's factors and chains go to its group's leader
@@ -133,7 +144,7 @@ int build_partitioned_plan(const dynohip_graph_view& g, const uint64_t* keys, co
       for (int64_t i = i0; i < i1; ++i) {
         int32_t o = kOwnNone;
         for (int sl = 0; sl < nk; ++sl)
-          if (kSlotKind[t][sl] == 0) o = merge_owner(o, pose_owner(tp.idx[i * nk + sl]));
+          if (kSlotKind[t][sl] == 0) o = merge_owner(o, pose_owner(tp.idx[i * nk + sl]), nodes);
         fown[t][i] = o;
       }
     });
@@ -141,7 +152,7 @@ int build_partitioned_plan(const dynohip_graph_view& g, const uint64_t* keys, co
       for (int sl = 0; sl < nk; ++sl)
         if (kSlotKind[t][sl] == 1) {
           const int c = comp_of[tp.idx[i * nk + sl]];
-          comp_own[c] = merge_owner(comp_own[c], fown[t][i]);
+          comp_own[c] = merge_owner(comp_own[c], fown[t][i], nodes);
         }
   }
   for (int c = 0; c < G.n_comp; ++c) {
@@ -169,7 +180,7 @@ int build_partitioned_plan(const dynohip_graph_view& g, const uint64_t* keys, co
       for (int64_t i = nt * w / nw; i < nt * (w + 1) / nw; ++i) {
         int32_t o = fown[t][i];
         for (int sl = 0; sl < nk; ++sl)
-          if (kSlotKind[t][sl] == 1) o = merge_owner(o, comp_own[comp_of[tp.idx[i * nk + sl]]]);
+          if (kSlotKind[t][sl] == 1) o = merge_owner(o, comp_own[comp_of[tp.idx[i * nk + sl]]], nodes);
         if (o == kOwnConflict) bad[w] = 1;
         o = to_rank(o);
         fown[t][i] = o;

@@ -157,8 +157,16 @@ std::vector<int64_t> even_cuts(int64_t n) {
 }  // namespace
 
 // values + factors below which a plan runs its parallel sections on one
-// thread (a C2-stream window: ~1.5k values, ~4k factors; C2: 185k)
-constexpr size_t kSmallPlanItems = 20000;
+// thread (a C2-stream window: ~1.5k values, ~4k factors; C2: 185k).
+// DYNOHIP_SMALL_PLAN_ITEMS overrides it (0: no small-plan cap), so the tests
+// can compare a capped plan with the threaded one (tests/test_plan_digest.py)
+static size_t small_plan_items() {
+  static const size_t v = [] {
+    const char* e = std::getenv("DYNOHIP_SMALL_PLAN_ITEMS");
+    return e ? static_cast<size_t>(std::strtoull(e, nullptr, 10)) : size_t{20000};
+  }();
+  return v;
+}
 
 static double plan_now() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -252,7 +260,7 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
   // small graphs plan on this thread (and its schedule thread) alone
   const size_t n_fac = g.pose_to_point.n + g.landmark_motion_ternary.n + g.between.n + g.prior.n +
                        g.landmark_motion_pose.n + g.landmark_pose_smoothing.n;
-  const int pcap = n + n_fac < kSmallPlanItems ? 1 : 0;
+  const int pcap = n + n_fac < small_plan_items() ? 1 : 0;
   PlanCap plan_cap(pcap);
   plan_recycle(P);
   P.nranks = nranks;

@@ -345,7 +345,7 @@ int build_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t*
 // Partitioned full-batch solve: what one rank holds (partition.cpp).
 struct Partition {
   int nranks = 1, rank = 0;
-  std::vector<int32_t> value_owner;     // per global value: owning rank; a pose of a separator: sep_code(node)
+  std::vector<int32_t> value_owner;     // per global value: owning rank (a separator pose: its node's leader, nodes[].r0)
   std::vector<int32_t> local_of;        // per global value: index in the local value list, -1 = not held
   std::vector<uint64_t> keys;           // local value list (all poses + this rank's points)
   std::vector<uint8_t> kind;

@@ -146,7 +146,8 @@ class PlanPool {
 // faster on one thread than with the pool's wake-ups per section (set_values
 // 1.26-1.29 against 1.37-1.43 ms per C2-stream window in one A/B run,
 // profiles/r05/window/plan_cap_ab.log); the plan is the same either way
-// (tests/test_plan_digest.py).
+// (tests/test_plan_digest.py compares the capped small plans with the same
+// plans built threaded, DYNOHIP_SMALL_PLAN_ITEMS=0).
 struct PlanCap {
   int prev;
   explicit PlanCap(int c) : prev(PlanPool::cap()) { PlanPool::cap() = c; }

@@ -252,8 +252,10 @@ typedef struct {
   double assembly_bytes;     /* algorithmic bytes of one reduced assembly:
                                 gather-list entries, every distinct operand
                                 block once, the band and gradient written
-                                (since ABI v3 the operand blocks are counted
-                                once, not per entry that reads them)        */
+                                (the operand blocks are counted once, not
+                                per entry that reads them, since the round-5
+                                build of ABI 3: earlier ABI-3 builds counted
+                                them per entry, so their figures are higher) */
   double chol_flops;         /* algorithmic flops of one envelope Cholesky  */
   double chol_tile_flops;    /* flops actually issued by the tile algorithm */
   /* accumulated device time (ms, HIP events) and counts since lm_reset.
@@ -328,24 +330,31 @@ typedef int (*dynohip_allreduce_fn)(void* ctx, double* buf, size_t n, int on_dev
    then passes the same GLOBAL graph and values. The reduced pose system is
    split along its nested dissection into nranks time-contiguous subtrees:
    a rank linearises and Schur-eliminates only the factors and landmark
-   chains touching its subtree, then the ranks sum the separator system (one
-   all-reduce of its tiles and right-hand side per linear solve, plus one of
-   8 scalars per LM inner iteration) and every rank factors it. LM decisions
+   chains touching its subtree (factors and chains touching only separator
+   tiles: the leader, lowest rank, of the deepest separator node they touch).
+   Then, per separator depth from the deepest up, the ranks sum that depth's
+   separator tiles and right-hand side rows (one all-reduce per depth per
+   linear solve, plus one of 8 scalars per LM inner iteration); each
+   separator node is factored by the group of ranks whose subtrees it splits,
+   its leader passing the node's contributions to the separators above. LM decisions
    are identical on all ranks. All ranks must make the same calls in the
    same order (set_values, optimize, iterate, graph_error are collective).
    Replaces the single-process solve of RGBDBackendModule.cc:207-231. */
 int dynohip_set_partition(dynohip_solver* s, int nranks, int rank, dynohip_allreduce_fn allreduce, void* ctx);
 
 /* After set_values on a partitioned handle: per global value, the rank
-   whose dynohip_get_values output is authoritative for it (-1: every rank
-   holds it identically). get_values fills only the values this rank holds
+   whose dynohip_get_values output is authoritative for it: its subtree's
+   rank, or for a separator pose the leader of its separator node (every
+   value has exactly one owner, 0 <= owner < nranks). get_values fills only the values this rank holds
    and leaves the others untouched in `data_out`. `exchange_doubles` (may be
    null) receives the size of the per-solve separator all-reduce. */
 int dynohip_value_owner(dynohip_solver* s, int32_t* owner_out, size_t n, int64_t* exchange_doubles);
 
 /* Host-only introspection: one named int32 array of rank `rank`'s plan
-   (nranks = 1: the ordinary plan), e.g. "ftask", "ftask1", "bpart",
-   "tile_owner", "sep_slot_ranges", "value_owner". *n_out = its length;
+   (nranks = 1: the ordinary plan), e.g. "ftask", "bpart", "tile_owner",
+   "sep_nodes" (r0, nr, depth, t0, t1 per separator node), "phases" (node,
+   leader per separator phase), "phase<p>_ftask", "value_owner". Unknown
+   names return DYNOHIP_EINVAL. *n_out = its length;
    at most `cap` entries are copied to `out` (may be null). */
 int dynohip_plan_export(const dynohip_graph_view* g, const uint64_t* keys, const uint8_t* kind, size_t n,
                         int nranks, int rank, const char* name, int32_t* out, size_t cap, size_t* n_out);

@@ -585,3 +585,69 @@ def test_module_statistics_keys_and_csv(tmp_path, full_batch):
     for label, samples in rows.items():
         np.testing.assert_allclose(samples, m.statistics(label), rtol=1e-5)
     assert set(_read_statistics_csv(ns_path)) == {l for l in labels if l.endswith(" [ns]")}
+
+
+def _module_run(packets, formulation, windows_in_flight, post_update=True):
+    m = backend.RGBDBackendModule(backend.backend_params(formulation=formulation), use_full_batch_opt=False,
+                                  optimize=True, post_update=post_update, windows_in_flight=windows_in_flight)
+    res, pend = [], []
+    for p in packets:
+        res.append(m.spinOnce(p))
+        pend.append(m.pending())
+    if windows_in_flight:
+        res.append(m.flush())
+        assert m.pending() == 0
+    return m, res, pend
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("formulation,k", [(backend.MOTION_IN_WORLD, 2), (backend.MOTION_IN_WORLD, 3),
+                                           (backend.LL_WORLD, 2)])
+def test_module_deferred_windows_bit_identical(gpu_available, tmp_path, formulation, k):
+    """Deferred sliding windows (windows_in_flight = k worker handles, the
+    solves overlapping later frames' construction) end with the sequential
+    module's state bit for bit: the updater's theta and graph, the CSV logs
+    of logBackendFromMap, the last solved problem, the windows' LM counts
+    and the statistics labels and sample counts. The windows ignore the
+    updater's theta (RGBDBackendModule.cc:288-300), its merges are
+    insert_or_assign in window order (:241, Formulation-impl.hpp:53-60), and
+    the later frames' constructions read the merged camera poses, so the
+    queue must keep the reference's order."""
+    cfg = stream.StreamConfig(frames=64, objects=3, static_landmarks=1200, dyn_slots=12, seed=7)
+    packets, _ = stream.generate(cfg)
+    ms, rs, _ = _module_run(packets, formulation, 0)
+    md, rd, pend = _module_run(packets, formulation, k)
+    assert max(pend) > 0, "no spin left a window outstanding"
+    # the same windows, solved with the same LM counts
+    n_win = sum(r["optimized"] for r in rs)
+    assert n_win >= 8 and sum(r["windows_merged"] for r in rd) == n_win
+    assert sum(r["iterations"] for r in rs) == sum(r["iterations"] for r in rd)
+    assert sum(r["inner_iterations"] for r in rs) == sum(r["inner_iterations"] for r in rd)
+    # theta bit for bit
+    ts, td = ms.formulation.getTheta(), md.formulation.getTheta()
+    np.testing.assert_array_equal(ts.keys, td.keys)
+    np.testing.assert_array_equal(ts.kinds, td.kinds)
+    assert ts.data.tobytes() == td.data.tobytes()
+    # the updater's graph
+    ga, gb = ms.formulation.getGraph().arrays(), md.formulation.getGraph().arrays()
+    for t in ga:
+        for a, b in zip(ga[t], gb[t]):
+            assert (a is None and b is None) or a.tobytes() == b.tobytes(), t
+    # the last solved problem (the last window)
+    pa, pb = ms.lastProblem(), md.lastProblem()
+    assert pa[1].data.tobytes() == pb[1].data.tobytes() and pa[2].tobytes() == pb[2].tobytes()
+    # CSV logs byte for byte
+    for m, d in ((ms, tmp_path / "seq"), (md, tmp_path / "def")):
+        d.mkdir()
+        m.formulation.logBackendFromMap(d)
+    for f in sorted(os.listdir(tmp_path / "seq")):
+        assert (tmp_path / "seq" / f).read_bytes() == (tmp_path / "def" / f).read_bytes(), f
+    # the reference's statistics labels, one sample per window / spin as before
+    assert ms.statisticsLabels() == md.statisticsLabels()
+    for label in ms.statisticsLabels():
+        assert len(ms.statistics(label)) == len(md.statistics(label)), label
+    # the output packet of the last frame reads the same estimates
+    last = len(packets) - 1
+    oa, ob = ms.constructOutputPacket(last), md.constructOutputPacket(last)
+    assert oa.T_world_camera.tobytes() == ob.T_world_camera.tobytes()
+    assert oa.static_landmarks[1].tobytes() == ob.static_landmarks[1].tobytes()

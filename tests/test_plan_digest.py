@@ -40,3 +40,24 @@ def test_recycled_plan_equals_fresh_plan():
     for k, x in fresh.items():
         diff = np.nonzero((x.reshape(-1, 2) != again[k].reshape(-1, 2)).any(1))[0]
         assert diff.size == 0, "%s: fields %s differ" % (k, diff.tolist())
+
+
+def test_small_plan_cap_equals_threaded_plan(tmp_path):
+    """Graphs under the small-plan threshold (T2, C1, the LLWorld T2: values
+    + factors < 20k) plan their parallel sections inline on the calling
+    thread (plan.cpp small_plan_items). The same plans built with the cap
+    off (DYNOHIP_SMALL_PLAN_ITEMS=0, the pool's threaded sections, in a
+    child process) have identical digests, field by field."""
+    path = str(tmp_path / "uncapped.npz")
+    env = dict(os.environ, DYNOHIP_SMALL_PLAN_ITEMS="0", DYNOHIP_PLAN_WORKERS="4")
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "plan_digest.py"), "save", path], env=env,
+                   check=True, timeout=600)
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import plan_digest
+    capped = plan_digest.digests()
+    threaded = np.load(path)
+    small = [k for k in capped if k.startswith(("T2", "C1"))]
+    assert small, sorted(capped)
+    for k in capped:
+        diff = np.nonzero((capped[k].reshape(-1, 2) != threaded[k].reshape(-1, 2)).any(1))[0]
+        assert diff.size == 0, "%s: fields %s differ" % (k, diff.tolist())

@@ -234,3 +234,45 @@ def test_sliding_window_check_errors():
         sw.check(k)                # triggers at 13: [10, 13]
     with pytest.raises(ValueError):
         sw.check(11)               # condition holds, start 8 < first 10
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_end_to_end(gpu_available, tmp_path):
+    """bench.py --gpus 2 launched as the driver launches it (torch.distributed
+    .run, one process per rank), here both ranks on the box's one GPU over
+    gloo: one JSON line from rank 0 with n_gpus 2, weak scaling, and value =
+    the LM iterations of both ranks' graphs (seeds 42, 43) over the slower
+    rank's wall time (max over ranks), consistent with ms_per_step and
+    lm_iterations_per_step. Unmeasured on 8 GPUs; this checks the
+    arithmetic and the launch path."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    port = 29700 + os.getpid() % 200
+    steps, warmup = 2, 1
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
+           "--gpus", "2", "--steps", str(steps), "--warmup", str(warmup), "--config", "C1", "--backend", "gloo",
+           "--no-cpu-baseline", "--no-phase-pass"]
+    r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["steps"] == steps and out["warmup"] == warmup
+    assert out["scaling"] == "weak"
+    # both ranks' iterations over the max-over-ranks time
+    total_iters = out["lm_iterations_per_step"] * steps * 2
+    assert out["value"] == pytest.approx(total_iters / (out["ms_per_step"] * steps / 1e3), rel=1e-9)
+    # per-rank iteration counts are those of the seeds' single-process solves
+    from dynosam_amd.optimizer import Solver
+    iters = 0
+    for seed in (42, 43):
+        g, v, _ = synth.generate("C1", seed=seed)
+        s = Solver(0)
+        s.set_graph(g)
+        s.set_values(v)
+        iters += s.optimize().iterations
+        s.close()
+    assert total_iters == pytest.approx(iters * steps)

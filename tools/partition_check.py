@@ -139,7 +139,12 @@ def main():
             # iterations), and then its final error lies within that spread
             counts = (sp.iterations, sp.inner_iterations)
             counts_ok = counts in ((sr.iterations, sr.inner_iterations), (sc.iterations, sc.inner_iterations))
-            acc_ok = same_acc or acc_p == [c["accepted"] for c in ctrace]
+            same_acc_ctrl = acc_p == [c["accepted"] for c in ctrace]
+            # the accept sequence of the handle whose counts the run took
+            if counts == (sr.iterations, sr.inner_iterations):
+                acc_ok = same_acc
+            else:
+                acc_ok = same_acc_ctrl
             err_ok = abs(sp.final_error - sr.final_error) <= max(1e-6 * abs(sr.final_error),
                                                                  2.0 * abs(sc.final_error - sr.final_error))
             ok_free = counts_ok and acc_ok and err_ok
@@ -148,6 +153,8 @@ def main():
                 "inner": [sp.inner_iterations, sr.inner_iterations, sc.inner_iterations],
                 "final_error": [sp.final_error, sr.final_error, sc.final_error],
                 "same_accept_sequence": same_acc,
+                "same_accept_sequence_as_count_match": acc_ok,
+                "final_error_within_spread": err_ok,
                 "values_rel_frobenius": rel(out, rv),
                 "accepted_error_rel_max": err_rel(trace, rtrace),
                 "control_values_rel_frobenius": rel(cv, rv),
