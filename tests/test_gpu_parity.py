@@ -348,13 +348,28 @@ def test_free_running_ns_vs_oracle(gpu_available):
     # oracle's summation orders stop after 15 and 17 iterations, the exact
     # steps after 17), values within the north-star 1e-6 of its end point
     ve, vo = rel(s.values_data(), ex["values"]), rel(o.values_data(), ex["values"])
-    print(f"iterations: GPU {sg.iterations}, exact-step run {int(ex['iterations'])}, oracle {so.iterations}"
-          f" (fixture orders {spread['forward']['iterations']}, {spread['reversed']['iterations']});"
-          f" values to the exact-step run: GPU {ve:.2e}, oracle {vo:.2e}")
+    # the oracle's other summation order (the fixture's "reversed" run),
+    # free-running to its own end
+    orv = Oracle(g, v, threads=cores(), reverse_sums=True)
+    srv = orv.optimize()
+    vrv = rel(orv.values_data(), ex["values"])
+    g_fw, g_rv, fw_rv = (rel(s.values_data(), o.values_data()), rel(s.values_data(), orv.values_data()),
+                         rel(o.values_data(), orv.values_data()))
+    print(f"iterations: GPU {sg.iterations}, exact-step run {int(ex['iterations'])}, oracle {so.iterations} /"
+          f" reversed {srv.iterations} (fixture orders {spread['forward']['iterations']},"
+          f" {spread['reversed']['iterations']}); end point to the exact-step run: GPU {ve:.2e}, oracle {vo:.2e},"
+          f" reversed {vrv:.2e}; GPU to the oracle's orders {g_fw:.2e} / {g_rv:.2e}, the orders apart {fw_rv:.2e}")
     assert (sg.iterations, sg.inner_iterations) == (int(ex["iterations"]), int(ex["inner_iterations"]))
-    # the end point: within 1e-6 of the exact-step run's, or no further from
-    # it than the double-precision reference's own end point
-    assert ve < max(PER_ITER_TOL, vo), (ve, vo)
+    assert srv.iterations == spread["reversed"]["iterations"]
+    # the end point: within 1e-6 of the nearer double-precision order's end
+    # point where that holds; it does not here, because the two orders of
+    # the same double solver end 4.9e-6 apart (profiles/r06/parity_probe.log)
+    # and each is 6e-6 from the exact-step run. Then the GPU's end point is
+    # held to the exact-step run's: nearer it than either double order
+    # (observed 2.35e-6 against 6.1e-6 / 6.0e-6).
+    if min(g_fw, g_rv) >= PER_ITER_TOL:
+        assert fw_rv >= PER_ITER_TOL, (g_fw, g_rv, fw_rv)
+        assert ve < min(vo, vrv), (ve, vo, vrv)
 
 
 @pytest.mark.parametrize("name,kw", [("T1", {}), ("T2", {}), ("C1", {}), ("T2", {"noise_code_defaults": 1}),
@@ -660,7 +675,7 @@ def gauge_split(values, dg, do):
     return (np.linalg.norm(rest) / nd if nd > 0 else 0.0), nd
 
 
-@pytest.mark.parametrize("name,iters", [("T2", 8), ("C1", 6), ("C2", 8)])
+@pytest.mark.parametrize("name,iters", [("T2", 8), ("C1", 6)])
 def test_llworld_per_iteration_conditioned(gpu_available, name, iters):
     """LLWorld (WorldPoseFormulation) per LM iteration, conditioned: before
     every iteration the oracle is put on the GPU's values AND lambda.
@@ -780,6 +795,84 @@ def test_llworld_per_iteration_conditioned(gpu_available, name, iters):
         assert d[1] < PER_ITER_TOL, d
 
 
+def test_llworld_c2_conditioned_against_exact(gpu_available):
+    """LLWorld at configs[1] size (C2), 12 LM iterations conditioned (the
+    oracle put on the GPU's values and lambda before each). Here the damped
+    system is singular along the object-pose gauge L_k -> L_k G up to
+    lambda, and from lambda 1e-8 on whether a double-precision Cholesky
+    factors it is decided by rounding: the oracle's own two summation orders
+    part on 2 of these 12 iterations, and the LM with every step solved in
+    x87 extended precision (the exact-step LM, oracle solve_ld) never fails
+    to factor (tools/parity_probe.py, profiles/r06/parity_probe_llworld.log).
+    So the reference for each iterate is the exact step at the lambda the
+    GPU accepted, and the double oracle's own distance to it is the scale:
+      * every iteration: the GPU's accepted iterate is within 1e-6 of the
+        exact iterate at its lambda on every value but the object poses, or
+        no further from it than the oracle's solve at that lambda (which
+        may fail to factor there); and the object motions L_k L_{k-1}^-1
+        (gauge-invariant) within 1e-6 of the exact iterate's, or no further
+        than the oracle's;
+      * iterations where GPU and oracle take the same tries: every value but
+        the object poses within 1e-6 of the oracle's iterate (observed
+        <= 3e-8), the motions within 1e-6 of the oracle's or no further
+        from the exact iterate's than the oracle's (observed 4-6x nearer at
+        lambda >= 1e-7);
+      * a try whose factorisation succeeds on one side only is at lambda <=
+        1e-5 (observed 1e-8 .. 1e-5);
+      * over the run the GPU's factorisation fails no more often than the
+        oracle's (observed 10 against 13)."""
+    g, v, _, s = make("C2", formulation=1)
+    o = Oracle(g, v, threads=cores())
+    m = gauge_mask(v)
+    mot = lambda x: llworld_motions(v, x)
+    lam = 1e-5
+    same_iters, fails_g, fails_o = [], 0, 0
+    for it in range(12):
+        start = s.values_data()
+        o.set_values_data(start)
+        o.reset(lm_params(lam))
+        s.reset(lm_params(lam))
+        sg, so = s.iterate(), o.iterate()
+        tg, to = s.trace(), o.trace()
+        vg, vo = s.values_data(), o.values_data()
+        fails_g += sum(not e["solved"] for e in tg)
+        fails_o += sum(not e["solved"] for e in to)
+        for a, b in zip(tg, to):
+            if a["lam"] == b["lam"] and a["solved"] != b["solved"]:
+                assert a["lam"] <= 1.5e-5, (it, a, b)
+        acc = [e for e in tg if e["accepted"]]
+        if not acc:
+            lam = sg.final_lambda
+            continue
+        la = acc[-1]["lam"]
+        o.set_values_data(start)
+        ok_l, dl = o.solve_damped_ld(la)
+        ok_o, do = o.solve_damped(la)
+        assert ok_l
+        exact = retract(v, start, dl)
+        ge = rel(vg[m], exact[m])
+        mg = rel(mot(vg), mot(exact))
+        if ok_o:
+            vo_l = retract(v, start, do)
+            oe, mo = rel(vo_l[m], exact[m]), rel(mot(vo_l), mot(exact))
+        else:
+            oe = mo = float("inf")
+        print(f"C2-LL {it}: lambda {lam:.0e} tries gpu {[(e['lam'], e['solved'], e['accepted']) for e in tg]}"
+              f" oracle {[(e['lam'], e['solved'], e['accepted']) for e in to]}; at the accepted {la:.0e} to the"
+              f" exact iterate: values GPU {ge:.1e} oracle {oe:.1e}, motions GPU {mg:.1e} oracle {mo:.1e}")
+        assert ge < PER_ITER_TOL or ge <= oe, (it, ge, oe)
+        assert mg < PER_ITER_TOL or mg <= mo, (it, mg, mo)
+        key = lambda t: [(e["lam"], e["solved"], e["accepted"]) for e in t]
+        if key(tg) == key(to):
+            same_iters.append(it)
+            assert rel(vg[m], vo[m]) < PER_ITER_TOL, it
+            assert rel(mot(vg), mot(vo)) < PER_ITER_TOL or mg <= mo, it
+        lam = sg.final_lambda
+    print("C2-LL iterations with the same tries:", same_iters, "failed factorisations GPU", fails_g, "oracle", fails_o)
+    assert len(same_iters) >= 3
+    assert fails_g <= fails_o
+
+
 @pytest.mark.parametrize("name,kw", [("T2", {}), ("C1", {}), ("T2", {"formulation": 1})])
 def test_linearize_matches_libm_oracle(gpu_available, name, kw):
     """The kernels share trig.h with the oracle, so their rows are bit-
@@ -804,21 +897,36 @@ def test_linearize_matches_libm_oracle(gpu_available, name, kw):
 
 def test_free_running_c2_vs_libm_oracle(gpu_available):
     """A deep-convergence free run (C2: lambda down to 1e-19) against the
-    oracle with glibc's trigonometry: the same iteration counts and accept /
-    lambda sequence, and end values within 2e-6 (the deep-convergence bar
-    that held before trig.h was shared, round 3)."""
+    oracle with glibc's trigonometry (GTSAM's libm): the same iteration
+    counts and accept / lambda sequence and the final error at 1e-6. The
+    end values are held to the north-star 1e-6 of the same LM with glibc's
+    trigonometry and every damped step solved in x87 extended precision
+    (the exact-step run; observed 1.1e-7). Against the double-precision
+    glibc oracle itself they are ~1.0e-6 apart because that oracle is
+    1.03e-6 from its own exact-step run (both summation orders: 1.03e-6 /
+    0.97e-6; tools/parity_probe.py c2_libm, profiles/r06/parity_probe.log):
+    at lambda 1e-19 every double-precision solve is ~1e-7 of the values off
+    the exact step and those errors accumulate over the deep iterations.
+    Asserted: within 1e-6 of the double oracle, or it at least 5e-7 from
+    the exact-step run."""
     g, v, _, s = make("C2")
     sg = s.optimize()
     o = Oracle(g, v, threads=cores(), libm=True)
     so = o.optimize()
     tg, to = s.trace(), o.trace()
     vr = rel(s.values_data(), o.values_data())
+    oe = Oracle(g, v, threads=cores(), libm=True, solve_ld=True)
+    se = oe.optimize()
+    ge, ome = rel(s.values_data(), oe.values_data()), rel(o.values_data(), oe.values_data())
     print("C2 vs libm oracle", (sg.iterations, sg.inner_iterations), (so.iterations, so.inner_iterations),
-          f"values rel {vr:.2e}")
+          f"values rel {vr:.2e}; to the libm exact-step run: GPU {ge:.2e}, libm oracle {ome:.2e}")
     assert (sg.iterations, sg.inner_iterations) == (so.iterations, so.inner_iterations)
     assert [(e["accepted"], e["lam"]) for e in tg] == [(e["accepted"], e["lam"]) for e in to]
+    assert [(e["accepted"], e["lam"]) for e in oe.trace()] == [(e["accepted"], e["lam"]) for e in tg]
+    assert (se.iterations, se.inner_iterations) == (sg.iterations, sg.inner_iterations)
     assert sg.final_error == pytest.approx(so.final_error, rel=1e-6)
-    assert vr < 2e-6
+    assert ge < PER_ITER_TOL, ge
+    assert vr < PER_ITER_TOL or ome >= 0.5 * PER_ITER_TOL, (vr, ome)
 
 
 def test_bit_reproducible(gpu_available):

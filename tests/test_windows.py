@@ -173,10 +173,15 @@ def test_configs3_eight_c2_windows_sharded_on_gpu(gpu_available, tmp_path):
     """configs[3]: 8 C2-shaped windows (seeds 42..49) sharded over 2 ranks
     (gloo, both on the GPU), solved by the HIP path and merged last-writer-wins
     in window order. The sharded merge equals the serial single-process merge
-    bit for bit; every window's LM matches the CPU oracle per iteration
-    (conditioned, 1e-6 relative Frobenius) and in its final error."""
+    bit for bit; every window's whole LM run matches the CPU oracle per
+    iteration, conditioned (same inner iterations; 1e-6 relative Frobenius,
+    or check_iterate's exact-step rule where the oracle itself is >= 5e-7
+    off the exact step at lambda 1e-19, as at C2), and each window's
+    free-running final error is the oracle's at 1e-6 (observed <= 1e-7,
+    profiles/r06/parity_probe.log)."""
     from dynosam_amd.optimizer import Solver
     from oracle_binding import Oracle
+    from test_gpu_parity import PER_ITER_TOL, check_iterate, cores, lm_params
 
     out = str(tmp_path / "c4.npz")
     port = 29400 + os.getpid() % 1000
@@ -195,25 +200,31 @@ def test_configs3_eight_c2_windows_sharded_on_gpu(gpu_available, tmp_path):
     off = Values(*last)._offsets()
     i = int(np.nonzero(last[0] == k_shared)[0][0])
     assert np.array_equal(merged[k_shared][1], last[2][off[i]:off[i + 1]])
-    # each window against the oracle
+    # each window's whole run against the oracle, conditioned per iteration
     for w in range(N_WINDOWS_C4):
         g, v = _c4_window(w)
         s = Solver(0)
         s.set_graph(g)
         s.set_values(v)
-        o = Oracle(g, v)
-        s.reset()
-        o.reset()
-        for it in range(3):
-            o.set_values_data(s.values_data())
+        o = Oracle(g, v, threads=cores())
+        n_it = serial[w][1][0]
+        lam, worst = 1e-5, 0.0
+        for it in range(n_it):
             start = s.values_data()
+            o.set_values_data(start)
+            o.reset(lm_params(lam))
+            s.reset(lm_params(lam))
             sg, so = s.iterate(), o.iterate()
             assert (sg.iterations, sg.inner_iterations) == (so.iterations, so.inner_iterations), (w, it)
             a, b = s.values_data(), o.values_data()
             if np.linalg.norm(b - start) > 0:
-                assert np.linalg.norm(a - b) / np.linalg.norm(b) < 1e-6, (w, it)
-        so = Oracle(g, v).optimize()
-        assert serial[w][1][2] == pytest.approx(so.final_error, rel=1e-5), w
+                worst = max(worst, check_iterate(o, start, s.trace()[-1]["lam"], a, b, v, f"window {w} it {it}"))
+            lam = sg.final_lambda
+        so = Oracle(g, v, threads=cores()).optimize()
+        print(f"window {w}: {n_it} iterations, worst conditioned distance {worst:.2e}, final error rel "
+              f"{abs(serial[w][1][2] - so.final_error) / so.final_error:.2e}")
+        assert (serial[w][1][0], serial[w][1][1]) == (so.iterations, so.inner_iterations), w
+        assert serial[w][1][2] == pytest.approx(so.final_error, rel=PER_ITER_TOL), w
 
 
 def synth_key_x(frame):
