@@ -49,34 +49,8 @@ def main():
         out[name] = {"n": int(m.sum()), "wait_us_mean": float((t[1] - t[0])[m].mean()),
                      "exec_us_mean": float((t[4] - t[1])[m].mean())}
     own = pan & (kk != ii)
-    # sub-phases: deps -> loads issued+rpart (P0) -> tiles in LDS (P1) -> factor start;
-    # factor end -> Linv in LDS (Q0) -> y (Q1) -> TRSM (Q2) -> stores (Q3) -> done
-    out["panel"]["sub_us_mean"] = {
-        "loads_diag_rhs": float((sub[0] - t[1])[pan].mean()), "tiles_lds": float((sub[1] - sub[0])[pan].mean()),
-        "pending_w0": float((t[2] - sub[1])[pan].mean()), "linv_y_sync": float((sub[2] - t[3])[own].mean()),
-        "y": float((sub[3] - sub[2])[pan].mean()), "trsm": float((sub[4] - sub[3])[own].mean()),
-        "store": float((sub[5] - sub[4])[own].mean()), "contrib_drain": float((t[4] - sub[5])[own].mean())}
-    # factorisation block steps as wave 0 passes each barrier
-    out["panel"]["factor_steps_us_mean"] = [float((bar[0] - t[2])[pan].mean())] + \
-        [float((bar[j] - bar[j - 1])[pan].mean()) for j in range(1, 4)] + [float((t[3] - bar[3])[pan].mean())]
-    # per block step, cycles on the factoring wave: pivots, U row, barrier wait
-    cyc = buf[16:32, :nt].astype(np.int64)
-    steps = []
-    for kb in range(4):
-        a, b_, c, d = cyc[4 * kb:4 * kb + 4]
-        steps.append({"pivots": float((b_ - a)[pan].mean()), "u_row": float((c - b_)[pan].mean()),
-                      "barrier": float((d - c)[pan].mean())})
-    for kb in range(1, 4):
-        steps[kb]["from_prev_barrier"] = float((cyc[4 * kb] - cyc[4 * kb - 1])[pan].mean())
-    out["panel"]["factor_step_cycles"] = steps
-    out["panel"].update({"pre_us_mean": float((t[2] - t[1])[pan].mean()),
-                         "factor_us_mean": float((t[3] - t[2])[pan].mean()),
-                         "post_us_mean": float((t[4] - t[3])[pan].mean())})
-    # worker occupancy, and the real dependency chain (Plan::fdep: the task
-    # that made the last write a task waits for)
-    busy = float((t[4] - t[1]).sum())
-    out["busy_frac_exec"] = busy / (span * (worker.max() + 1))
-    out["busy_frac_held"] = float((t[4] - t[0]).sum()) / (span * (worker.max() + 1))
+    # the real dependency chain (Plan::fdep: the task that made the last
+    # write a task waits for): each task's "ready" = its last input written
     fs = plan_export(graph, values, "fdep_start")
     fd = plan_export(graph, values, "fdep").reshape(-1, 2)
     writer, cnt = {}, {}
@@ -92,6 +66,65 @@ def main():
             w_ = writer[(int(fd[j, 0]), int(fd[j, 1]))]
             if t[4, w_] > ready[q]:
                 ready[q], dpred[q] = t[4, w_], w_
+    # sub-phases: early deps met (t1) -> operands waited for + loads issued +
+    # rpart (P0) -> tiles in LDS (P1) -> factor start; factor end -> Linv in
+    # LDS (Q0) -> y (Q1) -> TRSM (Q2) -> stores (Q3) -> done.
+    # t1 is the first class of dependencies (everything but the pending
+    # operand tiles, DESIGN §3 "Round 3"): the span t1 -> P0 includes the wait
+    # for those operands, so it is reported as such, and the hand-off proper
+    # is measured from the last input's write (the panel's `ready`)
+    from_ready = sub[0] - np.maximum(t[1], ready)
+    out["panel"]["sub_us_mean"] = {
+        "early_deps_to_loaded (incl. the operand wait)": float((sub[0] - t[1])[pan].mean()),
+        "handoff_last_input_to_loaded": float(from_ready[pan].mean()),
+        "tiles_lds": float((sub[1] - sub[0])[pan].mean()),
+        "pending_w0": float((t[2] - sub[1])[pan].mean()), "linv_y_sync": float((sub[2] - t[3])[own].mean()),
+        "y": float((sub[3] - sub[2])[pan].mean()), "trsm": float((sub[4] - sub[3])[own].mean()),
+        "store": float((sub[5] - sub[4])[own].mean()), "contrib_drain": float((t[4] - sub[5])[own].mean())}
+    # factorisation block steps as wave 0 passes each barrier: stamped by the
+    # diagonal tasks' factorisation (factor_tile_blk) only; an own panel
+    # (factor_own) leaves its entries unwritten (zero), so only tasks whose
+    # four stamps lie inside their factorisation are averaged
+    raw_bar = buf[12:16, :nt].astype(np.int64)
+    vb = pan & (raw_bar != 0).all(0)
+    vb &= (bar[0] >= t[2]) & (bar[3] <= t[3]) & (np.diff(bar, axis=0) >= 0).all(0)
+    out["panel"]["factor_steps_tasks"] = int(vb.sum())
+    out["panel"]["factor_steps_us_mean"] = ([float((bar[0] - t[2])[vb].mean())] +
+                                            [float((bar[j] - bar[j - 1])[vb].mean()) for j in range(1, 4)] +
+                                            [float((t[3] - bar[3])[vb].mean())]) if vb.any() else None
+    # per block step, cycles on the factoring wave: pivots, U row, barrier
+    # wait (s_memtime; the same diagonal tasks)
+    cyc = buf[16:32, :nt].astype(np.int64)
+    vc = pan & (cyc != 0).all(0)
+    for kb in range(4):
+        a, b_, c, d = cyc[4 * kb:4 * kb + 4]
+        vc &= (b_ >= a) & (c >= b_) & (d >= c)
+    steps = []
+    for kb in range(4):
+        a, b_, c, d = cyc[4 * kb:4 * kb + 4]
+        steps.append({"pivots": float((b_ - a)[vc].mean()), "u_row": float((c - b_)[vc].mean()),
+                      "barrier": float((d - c)[vc].mean())} if vc.any() else None)
+    out["panel"]["factor_step_cycles_tasks"] = int(vc.sum())
+    out["panel"]["factor_step_cycles"] = steps
+    out["panel"].update({"pre_us_mean": float((t[2] - t[1])[pan].mean()),
+                         "factor_us_mean": float((t[3] - t[2])[pan].mean()),
+                         "post_us_mean": float((t[4] - t[3])[pan].mean())})
+    # worker occupancy
+    busy = float((t[4] - t[1]).sum())
+    out["busy_frac_exec"] = busy / (span * (worker.max() + 1))
+    out["busy_frac_held"] = float((t[4] - t[0]).sum()) / (span * (worker.max() + 1))
+    # every reported time must be a sane span of this launch
+    def _walk(x):
+        if isinstance(x, dict):
+            for v in x.values():
+                yield from _walk(v)
+        elif isinstance(x, list):
+            for v in x:
+                yield from _walk(v)
+        elif isinstance(x, float):
+            yield x
+    bad = [x for x in _walk({k: out[k] for k in ("panel", "update")}) if not (-1.0 <= x <= 1e6)]
+    assert not bad, f"absurd task-clock fields: {bad}"
     late_pick = np.maximum(0.0, t[0] - ready)   # ready before a worker took it
     out["ready_before_pick_us"] = {"mean": float(late_pick.mean()), "max": float(late_pick.max()),
                                    "tasks_over_2us": int((late_pick > 2.0).sum())}
