@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--problems", type=int, default=4096, help="refine mode: (object, frame pair) problems per batch")
     ap.add_argument("--full-batch", action="store_true", help="stream mode: one full-batch solve at the last frame "
                                                              "instead of the sliding window (shipped flags)")
-    ap.add_argument("--windows-in-flight", type=int, default=3,
+    ap.add_argument("--windows-in-flight", type=int, default=4,
                     help="stream mode, sliding window: deferred windows on K worker handles (0: the sequential "
                          "module, each window solved inside its spin)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample (s)")

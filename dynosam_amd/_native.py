@@ -176,6 +176,7 @@ def _declare(name, lib):
             ("dynob_module_spin", [vp_, P(_abi.InputPacket), P(_abi.SpinResult)], C.c_int),
             ("dynob_module_flush", [vp_, P(_abi.SpinResult)], C.c_int),
             ("dynob_module_pending", [vp_], C.c_int),
+            ("dynob_module_window_builds", [vp_, P(C.c_int), P(C.c_int)], C.c_int),
             ("dynob_module_map", [vp_], vp_),
             ("dynob_module_formulation", [vp_], vp_),
             ("dynob_module_last_problem", [vp_, P(_abi.GraphView), P(U64), P(U8), P(D), P(D), SZ, SZ], C.c_int),

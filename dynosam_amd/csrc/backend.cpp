@@ -86,13 +86,17 @@ struct LandmarkNode {
   // frames_seen_ and measurements_ (one entry per seen frame), ordered by
   // frame id (FrameNodePtrSet / FastMap<FrameNodePtr>)
   std::map<uint64_t, std::array<double, 3>> measurements;
+  // observations made before the first one this map holds: 0 in a module's
+  // map; a window's own map (deferred windows, built from the window's
+  // frames alone) carries the count of the frames before the window here
+  size_t prior_obs = 0;
   bool is_static() const { return object_id == kBackgroundLabel; }
-  size_t num_observations() const { return measurements.size(); }
+  size_t num_observations() const { return prior_obs + measurements.size(); }
   // the observations a spin at frame `horizon` saw (frames arrive in order,
   // so a map read later holds the later frames' measurements too)
   size_t num_observations_upto(uint64_t horizon) const {
-    if (measurements.empty() || measurements.rbegin()->first <= horizon) return measurements.size();
-    return static_cast<size_t>(std::distance(measurements.begin(), measurements.upper_bound(horizon)));
+    if (measurements.empty() || measurements.rbegin()->first <= horizon) return num_observations();
+    return prior_obs + static_cast<size_t>(std::distance(measurements.begin(), measurements.upper_bound(horizon)));
   }
   bool seen_at(uint64_t f) const { return measurements.count(f) != 0; }
   const double* measurement(uint64_t f) const {
@@ -157,8 +161,15 @@ struct Map {
   FrameNode* last_fn = nullptr;
   uint64_t last_f = 0;
 
-  // Map::addOrUpdateMapStructures (Map.hpp:376-444)
-  void add(const dynob_measurement& m) {
+  // Map::addOrUpdateMapStructures (Map.hpp:376-444). `hist` (may be null)
+  // receives the landmark's observation count before this one and whether
+  // the measurement extends its history regularly: appended at its end and,
+  // for a dynamic tracklet, in the frame after its last one
+  struct AddHistory {
+    size_t before = 0;
+    bool regular = true;
+  };
+  LandmarkNode& add(const dynob_measurement& m, AddHistory* hist = nullptr) {
     const bool is_static = m.object_id == kBackgroundLabel;
     auto lit = landmarks.find(m.tracklet_id);
     if (lit == landmarks.end()) {
@@ -184,6 +195,10 @@ struct Map {
     DB_CHECK(at_end || !ln.seen_at(m.frame_id), DYNOHIP_EINVAL,
              "Unable to add new measurement to landmark node " + std::to_string(m.tracklet_id) + " at frame " +
                  std::to_string(m.frame_id) + " as a measurement already exists at this frame!");
+    if (hist) {
+      hist->before = ln.num_observations();
+      hist->regular = at_end && (is_static || ms.empty() || ms.rbegin()->first + 1u == m.frame_id);
+    }
     const std::array<double, 3> xyz = {m.landmark[0], m.landmark[1], m.landmark[2]};
     if (at_end)
       ms.emplace_hint(ms.end(), m.frame_id, xyz);
@@ -198,6 +213,7 @@ struct Map {
       fn.dynamic_landmarks.emplace_hint(fn.dynamic_landmarks.end(), m.tracklet_id);
       fn.objects_seen.insert(m.object_id);
     }
+    return ln;
   }
 
   // FrameNode::objectObservedInPrevious / objectMotionExpected
@@ -1086,162 +1102,16 @@ namespace dynob {
 // sequential module, and ends with the same theta bit for bit; only the time
 // at which each operation runs (and so each spin's output) lags.
 
-struct WindowJob {
-  uint64_t start = 0, end = 0;
-  GraphExport graph;          // the window's getGraph() / getTheta() copies
-  ValuesExport values;
-  std::vector<double> optimised;
-  dynohip_lm_summary summary{};
-  int rc = DYNOHIP_OK;
-  std::string err;
-  double ms_solve = 0.0;      // set_graph .. get_values on the worker
-  double ms_construct = 0.0;  // the window's construction on the spin's thread
-  std::mutex mu;
-  std::condition_variable cv;
-  bool done = false;
-  void wait() {
-    std::unique_lock<std::mutex> lk(mu);
-    cv.wait(lk, [&] { return done; });
-  }
-  bool ready() {
-    std::lock_guard<std::mutex> lk(mu);
-    return done;
-  }
+// One spin's input as the deferred-window mode keeps it: the frame's
+// measurements in the order the spin added them, each with its landmark's
+// observation count before it, and the frontend pose and motions
+struct FrameLog {
+  uint64_t k = 0;
+  std::vector<dynob_measurement> meas;
+  std::vector<size_t> before;
+  P3 X;
+  std::map<int32_t, P3> motions;
 };
-
-// Worker threads, each with its own solver handle (own HIP stream and device
-// buffers), taking window jobs in submission order: several windows' LM runs
-// are in flight on the device at once (one 10-frame window's kernels occupy a
-// handful of CUs).
-class WindowWorkers {
- public:
-  WindowWorkers(int n, int device, const dynohip_lm_params& lm) : device_(device), lm_(lm) {
-    for (int i = 0; i < n; ++i) threads_.emplace_back([this] { loop(); });
-  }
-  ~WindowWorkers() {
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      stop_ = true;
-    }
-    cv_.notify_all();
-    for (auto& t : threads_) t.join();
-  }
-  void submit(std::shared_ptr<WindowJob> j) {
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      q_.push_back(std::move(j));
-    }
-    cv_.notify_one();
-  }
-
- private:
-  void loop() {
-    dynohip_solver* solver = nullptr;
-    for (;;) {
-      std::shared_ptr<WindowJob> j;
-      {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
-        if (q_.empty()) break;   // stopping, nothing left
-        j = std::move(q_.front());
-        q_.pop_front();
-      }
-      run(j.get(), solver);
-      {
-        std::lock_guard<std::mutex> lk(j->mu);
-        j->done = true;
-      }
-      j->cv.notify_all();
-    }
-    if (solver) dynohip_destroy(solver);
-  }
-  void run(WindowJob* j, dynohip_solver*& solver) {
-    const auto t0 = std::chrono::steady_clock::now();
-    int rc = DYNOHIP_OK;
-    if (!solver) rc = dynohip_create(device_, &solver);
-    if (rc != DYNOHIP_OK) {
-      j->rc = rc;
-      j->err = "dynohip_create failed";
-      return;
-    }
-    dynohip_graph_view gv;
-    j->graph.view(&gv);
-    rc = dynohip_set_graph(solver, &gv);
-    if (rc == DYNOHIP_OK)
-      rc = dynohip_set_values(solver, j->values.keys.data(), j->values.kinds.data(), j->values.data.data(),
-                              j->values.keys.size());
-    if (rc == DYNOHIP_OK) rc = dynohip_optimize(solver, &lm_, &j->summary);
-    j->optimised.assign(j->values.data.size(), 0.0);
-    if (rc == DYNOHIP_OK) rc = dynohip_get_values(solver, j->optimised.data(), j->optimised.size());
-    if (rc != DYNOHIP_OK) j->err = std::string("LM solve failed: ") + dynohip_last_error(solver);
-    j->rc = rc;
-    j->ms_solve = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  }
-  std::vector<std::thread> threads_;
-  std::deque<std::shared_ptr<WindowJob>> q_;
-  std::mutex mu_;
-  std::condition_variable cv_;
-  bool stop_ = false;
-  int device_;
-  dynohip_lm_params lm_;
-};
-
-// One queued operation of the persistent updater (deferred-window mode)
-struct ModuleOp {
-  enum Kind { kBootstrap, kFrame, kMerge, kPostUpdate } kind;
-  uint64_t k = 0;                    // the spin's frame
-  std::shared_ptr<WindowJob> job;    // kMerge
-};
-
-}  // namespace dynob
-
-struct dynob_module {
-  dynob_params params;
-  dynob_module_params mp;
-  dynob_map map;
-  dynob_formulation updater;  // new_updater_
-  dynohip_sliding_window window;
-  bool bootstrapped = false;
-  dynohip_solver* solver = nullptr;
-  std::string err;
-  // deferred-window mode: the updater's pending operations in spin order,
-  // the windows being solved, and the workers (created on the first window)
-  std::deque<ModuleOp> ops;
-  size_t windows_pending = 0;
-  std::unique_ptr<WindowWorkers> workers;
-  // last solved problem
-  GraphExport last_graph;
-  ValuesExport last_values;
-  std::vector<double> last_optimised;
-  Statistics stats;
-  // Formulation::getFullyQualifiedName(): loggerPrefix() (no suffix)
-  std::string name() const {
-    return params.formulation == DYNOB_LL_WORLD ? "rgbd_LL_world_identity" : "rgbd_motion_world";
-  }
-};
-
-namespace {
-
-template <typename Fn>
-int guard(std::string& err, Fn&& fn) {
-  try {
-    fn();
-    return DYNOHIP_OK;
-  } catch (const Error& e) {
-    err = e.what();
-    return e.code;
-  } catch (const std::exception& e) {
-    err = e.what();
-    return DYNOHIP_EINVAL;
-  }
-}
-
-int64_t list_out(const std::vector<int64_t>& v, int64_t* out, size_t cap, size_t* n_out) {
-  if (n_out) *n_out = v.size();
-  if (out)
-    for (size_t i = 0; i < v.size() && i < cap; ++i) out[i] = v[i];
-  return static_cast<int64_t>(v.size());
-}
 
 // RGBDBackendModule::constructGraph (RGBDBackendModule.cc:246-296): a fresh
 // updater over [from, to]; its theta_ / factors_ are exactly the returned
@@ -1275,6 +1145,249 @@ std::unique_ptr<Formulation> construct_graph(Map* map, const dynob_params& p, ui
     u->update_static(f, new_values, new_factors, false);
   }
   return u;
+}
+
+// The map a deferred window is constructed from on its worker: the window's
+// own frames alone, each landmark carrying the count of its earlier
+// observations (LandmarkNode::prior_obs). It gives constructGraph of [start,
+// end] exactly what the module's map gives it at `end` (observation counts,
+// frame nodes, the window's measurements; the first frame a tracklet or an
+// object was seen differs only before `start`, where the construction only
+// compares it with frames of the window) as long as every landmark's
+// history grew regularly (Map::AddHistory; the module falls back to its own
+// map otherwise). The module's map meanwhile takes the next frames.
+struct WindowMap {
+  Map map;
+  explicit WindowMap(const std::vector<std::shared_ptr<const FrameLog>>& frames) {
+    for (const auto& f : frames) {
+      for (size_t i = 0; i < f->meas.size(); ++i) {
+        LandmarkNode& ln = map.add(f->meas[i]);
+        if (ln.measurements.size() == 1) ln.prior_obs = f->before[i];
+      }
+      FrameNode& fn = *map.frame(f->k);
+      fn.has_X = true;
+      fn.X_world = f->X;
+      fn.has_motions = true;
+      fn.motions_world = f->motions;
+    }
+  }
+};
+
+struct WindowJob {
+  uint64_t start = 0, end = 0;
+  // built on the worker from these frames when not empty (else by the spin)
+  std::vector<std::shared_ptr<const FrameLog>> frames;
+  dynob_params params{};
+  size_t num_vars = 0;
+  GraphExport graph;          // the window's getGraph() / getTheta() copies
+  ValuesExport values;
+  std::vector<double> optimised;
+  dynohip_lm_summary summary{};
+  int rc = DYNOHIP_OK;
+  std::string err;
+  double ms_solve = 0.0;      // set_graph .. get_values on the worker
+  double ms_construct = 0.0;  // the window's construction on the spin's thread
+  std::mutex mu;
+  std::condition_variable cv;
+  bool done = false;
+  void wait() {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return done; });
+  }
+  bool ready() {
+    std::lock_guard<std::mutex> lk(mu);
+    return done;
+  }
+};
+
+// Worker threads in two stages. Builders construct the windows that come
+// with their own frames (WindowMap; CPU work); solvers, each with its own
+// solver handle (own HIP stream and device buffers), take built windows in
+// submission order and run their LM, several windows' solves in flight on the
+// device at once (one 10-frame window's kernels occupy a handful of CUs, and
+// a solve mostly waits for them). Keeping the two apart lets a window's
+// construction overlap other windows' solves instead of idling a stream.
+class WindowWorkers {
+ public:
+  WindowWorkers(int n, int device, const dynohip_lm_params& lm, bool optimize)
+      : device_(device), lm_(lm), optimize_(optimize) {
+    const int builders = std::max(1, (n + 1) / 2);
+    for (int i = 0; i < builders; ++i) threads_.emplace_back([this] { build_loop(); });
+    if (optimize_)
+      for (int i = 0; i < n; ++i) threads_.emplace_back([this] { solve_loop(); });
+  }
+  ~WindowWorkers() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_build_.notify_all();
+    cv_solve_.notify_all();
+    for (auto& t : threads_) t.join();
+  }
+  void submit(std::shared_ptr<WindowJob> j) {
+    if (j->frames.empty()) {
+      to_solve(std::move(j));
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      qb_.push_back(std::move(j));
+    }
+    cv_build_.notify_one();
+  }
+
+ private:
+  static void finish(WindowJob* j) {
+    {
+      std::lock_guard<std::mutex> lk(j->mu);
+      j->done = true;
+    }
+    j->cv.notify_all();
+  }
+  void to_solve(std::shared_ptr<WindowJob> j) {
+    if (!optimize_ || j->rc != DYNOHIP_OK) {   // nothing to solve (graphs only, or a failed construction)
+      finish(j.get());
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      qs_.push_back(std::move(j));
+    }
+    cv_solve_.notify_one();
+  }
+  std::shared_ptr<WindowJob> take(std::deque<std::shared_ptr<WindowJob>>& q, std::condition_variable& cv) {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv.wait(lk, [&] { return stop_ || !q.empty(); });
+    if (stop_ || q.empty()) return nullptr;   // stopping: queued windows are dropped
+    std::shared_ptr<WindowJob> j = std::move(q.front());
+    q.pop_front();
+    return j;
+  }
+  void build_loop() {
+    while (std::shared_ptr<WindowJob> j = take(qb_, cv_build_)) {
+      build(j.get());
+      to_solve(std::move(j));
+    }
+  }
+  void solve_loop() {
+    dynohip_solver* solver = nullptr;
+    while (std::shared_ptr<WindowJob> j = take(qs_, cv_solve_)) {
+      solve(j.get(), solver);
+      finish(j.get());
+    }
+    if (solver) dynohip_destroy(solver);
+  }
+  static void build(WindowJob* j) {
+    const auto tc = std::chrono::steady_clock::now();
+    try {
+      WindowMap wm(j->frames);
+      std::unique_ptr<Formulation> window = construct_graph(&wm.map, j->params, j->start, j->end, true);
+      j->graph.build(window->factors);
+      j->values.build(window->theta);
+      j->num_vars = window->theta.size();
+    } catch (const Error& e) {
+      j->rc = e.code;
+      j->err = e.what();
+    } catch (const std::exception& e) {
+      j->rc = DYNOHIP_EINVAL;
+      j->err = e.what();
+    }
+    j->ms_construct = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc).count();
+  }
+  void solve(WindowJob* j, dynohip_solver*& solver) {
+    const auto t0 = std::chrono::steady_clock::now();
+    int rc = DYNOHIP_OK;
+    if (!solver) rc = dynohip_create(device_, &solver);
+    if (rc != DYNOHIP_OK) {
+      j->rc = rc;
+      j->err = "dynohip_create failed";
+      return;
+    }
+    dynohip_graph_view gv;
+    j->graph.view(&gv);
+    rc = dynohip_set_graph(solver, &gv);
+    if (rc == DYNOHIP_OK)
+      rc = dynohip_set_values(solver, j->values.keys.data(), j->values.kinds.data(), j->values.data.data(),
+                              j->values.keys.size());
+    if (rc == DYNOHIP_OK) rc = dynohip_optimize(solver, &lm_, &j->summary);
+    j->optimised.assign(j->values.data.size(), 0.0);
+    if (rc == DYNOHIP_OK) rc = dynohip_get_values(solver, j->optimised.data(), j->optimised.size());
+    if (rc != DYNOHIP_OK) j->err = std::string("LM solve failed: ") + dynohip_last_error(solver);
+    j->rc = rc;
+    j->ms_solve = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+  std::vector<std::thread> threads_;
+  std::deque<std::shared_ptr<WindowJob>> qb_, qs_;   // to build, to solve
+  std::mutex mu_;
+  std::condition_variable cv_build_, cv_solve_;
+  bool stop_ = false;
+  int device_;
+  dynohip_lm_params lm_;
+  bool optimize_;   // false: windows are constructed only (module optimize off)
+};
+
+// One queued operation of the persistent updater (deferred-window mode)
+struct ModuleOp {
+  enum Kind { kBootstrap, kFrame, kMerge, kPostUpdate } kind;
+  uint64_t k = 0;                    // the spin's frame
+  std::shared_ptr<WindowJob> job;    // kMerge
+};
+
+}  // namespace dynob
+
+struct dynob_module {
+  dynob_params params;
+  dynob_module_params mp;
+  dynob_map map;
+  dynob_formulation updater;  // new_updater_
+  dynohip_sliding_window window;
+  bool bootstrapped = false;
+  dynohip_solver* solver = nullptr;
+  std::string err;
+  // deferred-window mode: the updater's pending operations in spin order,
+  // the windows being solved, and the workers (created on the first window)
+  std::deque<ModuleOp> ops;
+  size_t windows_pending = 0;
+  // the last opt_window_size + 1 spins' inputs, and whether every landmark's
+  // history has grown regularly so far (windows then build their own maps
+  // from these on the workers)
+  std::deque<std::shared_ptr<const FrameLog>> frame_log;
+  bool log_regular = true;
+  int windows_own_map = 0, windows_module_map = 0;   // where deferred windows were constructed
+  std::unique_ptr<WindowWorkers> workers;
+  // last solved problem
+  GraphExport last_graph;
+  ValuesExport last_values;
+  std::vector<double> last_optimised;
+  Statistics stats;
+  // Formulation::getFullyQualifiedName(): loggerPrefix() (no suffix)
+  std::string name() const {
+    return params.formulation == DYNOB_LL_WORLD ? "rgbd_LL_world_identity" : "rgbd_motion_world";
+  }
+};
+
+namespace {
+
+template <typename Fn>
+int guard(std::string& err, Fn&& fn) {
+  try {
+    fn();
+    return DYNOHIP_OK;
+  } catch (const Error& e) {
+    err = e.what();
+    return e.code;
+  } catch (const std::exception& e) {
+    err = e.what();
+    return DYNOHIP_EINVAL;
+  }
+}
+
+int64_t list_out(const std::vector<int64_t>& v, int64_t* out, size_t cap, size_t* n_out) {
+  if (n_out) *n_out = v.size();
+  if (out)
+    for (size_t i = 0; i < v.size() && i < cap; ++i) out[i] = v[i];
+  return static_cast<int64_t>(v.size());
 }
 
 // the problem handed to the solver (gtsam's getGraph() / getTheta() copies,
@@ -1367,15 +1480,24 @@ void construct_frame(dynob_module* m, uint64_t k, const P3& T_k) {
 // statistics; the spin result sums the windows merged during the spin
 void merge_window(dynob_module* m, WindowJob& j, dynob_spin_result* r) {
   DB_CHECK(j.rc == DYNOHIP_OK, j.rc, j.err);
+  if (!j.frames.empty()) record_interval(m->stats, m->name() + ".sliding_window_construction", j.ms_construct);
+  m->stats.add(m->name() + ".sliding_window_optimise_num_vars_all", static_cast<double>(j.num_vars));
+  r->windows_merged += 1;
+  r->window_start = j.start;
+  r->window_end = j.end;
+  if (!m->mp.optimize) {   // graphs only: the window is the last problem, nothing is solved
+    record_interval(m->stats, m->name() + ".sliding_window_optimise", 0.0);
+    m->last_graph = std::move(j.graph);
+    m->last_values = std::move(j.values);
+    m->last_optimised = m->last_values.data;
+    return;
+  }
   const double t0 = now_ms();
   update_theta(*m->updater.f, j.values, j.optimised);
   record_interval(m->stats, m->name() + ".sliding_window_optimise", j.ms_solve + (now_ms() - t0));
   r->optimized = 1;
-  r->windows_merged += 1;
   r->iterations += static_cast<int>(j.summary.iterations);
   r->inner_iterations += static_cast<int>(j.summary.inner_iterations);
-  r->window_start = j.start;
-  r->window_end = j.end;
   r->error_before = j.summary.initial_error;
   r->error_after = j.summary.final_error;
   r->ms_optimize += j.ms_solve;
@@ -1437,9 +1559,7 @@ void drain(dynob_module* m, dynob_spin_result* r, size_t max_pending) {
   }
 }
 
-bool deferred(const dynob_module* m) {
-  return m->mp.windows_in_flight > 0 && !m->mp.use_full_batch_opt && m->mp.optimize;
-}
+bool deferred(const dynob_module* m) { return m->mp.windows_in_flight > 0 && !m->mp.use_full_batch_opt; }
 
 // windows allowed to wait for their merge before a spin blocks on the oldest
 size_t max_pending(const dynob_module* m) { return 4 * static_cast<size_t>(m->mp.windows_in_flight); }
@@ -1467,17 +1587,27 @@ void spin_deferred(dynob_module* m, uint64_t k, dynob_spin_result* r) {
     auto job = std::make_shared<WindowJob>();
     job->start = s;
     job->end = e;
-    const double tc = now_ms();
-    {
+    // the window's frames, consecutive and all logged: built on the worker
+    bool own_map = m->log_regular && !m->frame_log.empty() && m->frame_log.front()->k == s &&
+                   m->frame_log.back()->k == e && m->frame_log.size() == e - s + 1;
+    if (own_map) {
+      job->frames.assign(m->frame_log.begin(), m->frame_log.end());
+      job->params = m->params;
+      ++m->windows_own_map;
+    } else {
+      ++m->windows_module_map;
+      const double tc = now_ms();
       TimingStatsCollector timer(m->stats, name + ".sliding_window_construction");
       std::unique_ptr<Formulation> window = construct_graph(&m->map.map, m->params, s, e, true);
       job->graph.build(window->factors);
       job->values.build(window->theta);
-      m->stats.add(name + ".sliding_window_optimise_num_vars_all", static_cast<double>(window->theta.size()));
+      job->num_vars = window->theta.size();
+      timer.stop();
+      r->ms_construct += now_ms() - tc;
     }
-    job->ms_construct = now_ms() - tc;
-    r->ms_construct += job->ms_construct;
-    if (!m->workers) m->workers = std::make_unique<WindowWorkers>(m->mp.windows_in_flight, m->mp.device_id, m->mp.lm);
+    if (!m->workers)
+      m->workers = std::make_unique<WindowWorkers>(m->mp.windows_in_flight, m->mp.device_id, m->mp.lm,
+                                                   m->mp.optimize != 0);
     m->workers->submit(job);
     m->ops.push_back({ModuleOp::kMerge, k, job});
     ++m->windows_pending;
@@ -2068,8 +2198,29 @@ int dynob_module_spin(dynob_module* m, const dynob_input_packet* in, dynob_spin_
     // RGBDBackendModule::updateMap (RGBDBackendModule.cc:264-280)
     TimingStatsCollector map_timer(m->stats, "map.update_observations");
     Map& map = m->map.map;
-    for (size_t i = 0; i < in->n_static; ++i) map.add(in->static_measurements[i]);
-    for (size_t i = 0; i < in->n_dynamic; ++i) map.add(in->dynamic_measurements[i]);
+    // deferred windows: the spin's input is also logged for the windows'
+    // own maps (WindowMap), with each landmark's history
+    std::shared_ptr<FrameLog> flog;
+    if (deferred(m)) {
+      flog = std::make_shared<FrameLog>();
+      flog->k = k;
+      flog->meas.reserve(in->n_static + in->n_dynamic);
+      flog->before.reserve(in->n_static + in->n_dynamic);
+      if (!m->frame_log.empty() && m->frame_log.back()->k >= k) m->log_regular = false;
+    }
+    auto add = [&](const dynob_measurement& x) {
+      if (!flog) {
+        map.add(x);
+        return;
+      }
+      Map::AddHistory h;
+      map.add(x, &h);
+      flog->meas.push_back(x);
+      flog->before.push_back(h.before);
+      m->log_regular = m->log_regular && h.regular && x.frame_id == k;
+    };
+    for (size_t i = 0; i < in->n_static; ++i) add(in->static_measurements[i]);
+    for (size_t i = 0; i < in->n_dynamic; ++i) add(in->dynamic_measurements[i]);
     // updateSensorPoseMeasurement: CHECK_NOTNULL(frame_node) (Map.hpp:100-105)
     DB_CHECK(map.frame(k) != nullptr, DYNOHIP_ESTATE, "frame " + std::to_string(k) + " has no measurement");
     FrameNode& fn = *map.frame(k);
@@ -2080,6 +2231,13 @@ int dynob_module_spin(dynob_module* m, const dynob_input_packet* in, dynob_spin_
     for (size_t i = 0; i < in->n_motions; ++i) fn.motions_world[in->motion_object_ids[i]] = pose_from(in->motions12 + 12 * i);
     map_timer.stop();
     const P3 T_k = fn.X_world;
+    if (flog) {
+      flog->X = fn.X_world;
+      flog->motions = fn.motions_world;
+      m->frame_log.push_back(std::move(flog));
+      // a window is [k - opt_window_size, k]
+      while (m->frame_log.front()->k + static_cast<uint64_t>(m->mp.opt_window_size) < k) m->frame_log.pop_front();
+    }
     if (deferred(m)) return spin_deferred(m, k, r);
     Values nv;
     Graph nf;
@@ -2151,6 +2309,13 @@ int dynob_module_flush(dynob_module* m, dynob_spin_result* r) {
 
 int dynob_module_pending(const dynob_module* m) {
   return m ? static_cast<int>(m->ops.size()) : DYNOHIP_EINVAL;
+}
+
+int dynob_module_window_builds(const dynob_module* m, int* own_map, int* module_map) {
+  if (!m) return DYNOHIP_EINVAL;
+  if (own_map) *own_map = m->windows_own_map;
+  if (module_map) *module_map = m->windows_module_map;
+  return DYNOHIP_OK;
 }
 
 // Statistics::WriteAllSamplesToCsvFile (Statistics.cc:352-381) through

@@ -1274,10 +1274,12 @@ int dynohip_create(int device_id, dynohip_solver** out) {
   HandleRes r;
   if (!ResPool::get().take(device_id, &r)) {
     r.device = device_id;
+    // (the second stream of the level-launched factorisation is made when
+    // that path is chosen, dynohip_set_exec_options: a stream takes one of
+    // the process's few hardware queues, which several handles driven from
+    // several threads -- deferred sliding windows -- need for their own)
     bool ok = hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking) == hipSuccess &&
-              hipStreamCreateWithFlags(&r.side, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&r.ev_main, hipEventDisableTiming) == hipSuccess &&
-              hipEventCreateWithFlags(&r.ev_side, hipEventDisableTiming) == hipSuccess &&
               hipEventCreateWithFlags(&r.ev_res, hipEventDisableTiming) == hipSuccess &&
               hipHostMalloc(reinterpret_cast<void**>(&r.hres), 8 * sizeof(double), hipHostMallocDefault) == hipSuccess;
     for (auto& e : r.ev) ok = ok && hipEventCreate(&e) == hipSuccess;
@@ -1818,6 +1820,12 @@ int dynohip_set_exec_options(dynohip_solver* s, int wide_updates, int level_back
   s->sd.wide_updates = wide_updates;
   s->sd.level_backward = level_backward != 0;
   s->sd.persistent_factor = level_factor == 0;
+  if (!s->sd.persistent_factor && !s->side) {
+    (void)hipSetDevice(s->device);
+    if (hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&s->ev_side, hipEventDisableTiming) != hipSuccess)
+      return set_err(s, DYNOHIP_EHIP, "second stream");
+  }
   return DYNOHIP_OK;
 }
 

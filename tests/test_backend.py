@@ -651,3 +651,77 @@ def test_module_deferred_windows_bit_identical(gpu_available, tmp_path, formulat
     oa, ob = ms.constructOutputPacket(last), md.constructOutputPacket(last)
     assert oa.T_world_camera.tobytes() == ob.T_world_camera.tobytes()
     assert oa.static_landmarks[1].tobytes() == ob.static_landmarks[1].tobytes()
+
+
+def _window_problems(packets, formulation, windows_in_flight):
+    """every sliding window's (graph arrays, initial values) in window order,
+    graphs only (optimize off); deferred: flushed after each triggering spin"""
+    m = backend.RGBDBackendModule(backend.backend_params(formulation=formulation), use_full_batch_opt=False,
+                                  optimize=False, post_update=True, windows_in_flight=windows_in_flight)
+    out = []
+    for p in packets:
+        r = m.spinOnce(p)
+        if windows_in_flight:
+            f = m.flush()
+            hit = r["windows_merged"] + f["windows_merged"] == 1
+            if f["windows_merged"]:
+                r = f
+        else:
+            hit = r["window_end"] > r["window_start"]
+        if hit:
+            g, v, opt = m.lastProblem()
+            out.append(((r["window_start"], r["window_end"]), g.arrays(), v, opt))
+    return m, out
+
+
+@pytest.mark.parametrize("formulation", [backend.MOTION_IN_WORLD, backend.LL_WORLD])
+@pytest.mark.parametrize("name", ["late_objects", "edges", "long"])
+def test_deferred_window_construction_equals_module_map(name, formulation):
+    """Deferred windows construct each window on a worker from the window's
+    own frames (WindowMap: the logged measurements, each landmark carrying
+    its earlier observation count), not from the module's map. Every
+    window's graph (every factor, in order) and initial values are the
+    sequential module's bit for bit, and the updater ends identical; host
+    only (optimize off: graphs are built, nothing is solved)."""
+    cfg = STREAMS.get(name) or stream.StreamConfig(frames=70, objects=3, static_landmarks=600, dyn_slots=8, seed=9)
+    packets, _ = stream.generate(cfg)
+    ms, ws = _window_problems(packets, formulation, 0)
+    md, wd = _window_problems(packets, formulation, 2)
+    assert len(ws) == len(wd) >= 2
+    own, fallback = md.windowBuilds()
+    print(name, formulation, "windows built from their own frames", own, "from the module's map", fallback)
+    assert own + fallback == len(wd) and own >= 1
+    for (ra, ga, va, oa), (rb, gb, vb, ob) in zip(ws, wd):
+        assert ra == rb
+        for t in ga:
+            for a, b in zip(ga[t], gb[t]):
+                assert (a is None and b is None) or a.tobytes() == b.tobytes(), (ra, t)
+        np.testing.assert_array_equal(va.keys, vb.keys)
+        assert va.data.tobytes() == vb.data.tobytes() and oa.tobytes() == ob.tobytes()
+    ta, tb = ms.formulation.getTheta(), md.formulation.getTheta()
+    np.testing.assert_array_equal(ta.keys, tb.keys)
+    assert ta.data.tobytes() == tb.data.tobytes()
+    for label in ms.statisticsLabels():
+        assert len(ms.statistics(label)) == len(md.statistics(label)), label
+
+
+def test_deferred_window_construction_fallback_on_irregular_history():
+    """A packet carrying a measurement of an earlier frame makes the
+    landmark histories irregular: later deferred windows are constructed by
+    the spin from the module's map instead (the windows' own maps would no
+    longer see what the module's map shows), with the same graphs."""
+    packets, _ = stream.generate(stream.StreamConfig(frames=50, objects=2, static_landmarks=400, dyn_slots=6,
+                                                     seed=4))
+    p = packets[30]
+    extra = backend.make_measurements([10 ** 6], [0], [p.frame_id - 1], [[1.0, 2.0, 9.0]])
+    p.static_measurements = np.concatenate([np.asarray(p.static_measurements), extra])
+    ms, ws = _window_problems(packets, backend.MOTION_IN_WORLD, 0)
+    md, wd = _window_problems(packets, backend.MOTION_IN_WORLD, 3)
+    own, fallback = md.windowBuilds()
+    assert own >= 1 and fallback >= 1 and own + fallback == len(wd) == len(ws)
+    for (ra, ga, va, oa), (rb, gb, vb, ob) in zip(ws, wd):
+        assert ra == rb
+        for t in ga:
+            for a, b in zip(ga[t], gb[t]):
+                assert (a is None and b is None) or a.tobytes() == b.tobytes(), (ra, t)
+        assert va.data.tobytes() == vb.data.tobytes()
