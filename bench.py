@@ -42,7 +42,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector/matrix dense peak (spec)
-PROFILE_ROUND = "r05"       # profiles/<round>/ holding this round's rocprof summaries
+PROFILE_ROUND = "r06"       # profiles/<round>/ holding this round's rocprof summaries
 
 
 def parse():

@@ -100,6 +100,8 @@ struct LandmarkNode {
   }
   bool seen_at(uint64_t f) const { return measurements.count(f) != 0; }
   const double* measurement(uint64_t f) const {
+    // (a construction reads the frame it is at: usually the latest entry)
+    if (!measurements.empty() && measurements.rbegin()->first == f) return measurements.rbegin()->second.data();
     auto it = measurements.find(f);
     DB_CHECK(it != measurements.end(), DYNOHIP_ESTATE,
              "Missing measurement in landmark node with id " + std::to_string(tracklet_id) + " at frame " +
@@ -648,12 +650,13 @@ struct Formulation {
     P3 T_world_camera_frontend;
     DB_CHECK(map->initial_sensor_pose(k, &T_world_camera_frontend), DYNOHIP_ESTATE, "no frontend pose");
     std::vector<std::pair<uint64_t, Value>> added;
+    const uint64_t x_k = camera_pose_key(k);
     for (int64_t t : fk->static_landmarks) {
       const LandmarkNode& ln = map->landmarks.at(t);
       DB_CHECK(ln.is_static(), DYNOHIP_EINVAL, "Static estimate requested but landmark is dynamic!");
       const uint64_t point_key = static_key(t);
       if (is_other_values_in_map.count(point_key)) {
-        internal.add(kPoseToPoint, {camera_pose_key(k), point_key}, ln.measurement(k), noise.static_point);
+        internal.add(kPoseToPoint, {x_k, point_key}, ln.measurement(k), noise.static_point);
       } else {
         if (static_cast<int64_t>(observations(ln)) < params.min_static_observations) continue;
         // seen frames, ascending, up to k (only k itself without backtracking)
