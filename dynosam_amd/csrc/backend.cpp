@@ -77,6 +77,79 @@ uint64_t dynamic_key(uint64_t frame, int64_t trk) {
 uint64_t motion_key(int obj, uint64_t frame) { return dynohip_object_motion_key(obj, frame); }
 uint64_t object_pose_key(int obj, uint64_t frame) { return dynohip_object_pose_key(obj, frame); }
 
+// Ordered id sets and frame-keyed maps of the Map nodes as sorted vectors:
+// the same order and membership as the std::set / std::map they replace
+// (FastMapNodeSet's id order), but entries arrive almost always in order
+// (frames in sequence, a frame's ids mostly ascending), so an insert is an
+// append, a lookup a binary search in contiguous memory, and a node's
+// destruction one free instead of a tree walk.
+template <typename T>
+class FlatSet {
+ public:
+  using const_iterator = typename std::vector<T>::const_iterator;
+  const_iterator begin() const { return v_.begin(); }
+  const_iterator end() const { return v_.end(); }
+  size_t size() const { return v_.size(); }
+  bool empty() const { return v_.empty(); }
+  size_t count(const T& x) const { return std::binary_search(v_.begin(), v_.end(), x) ? 1 : 0; }
+  void insert(const T& x) {
+    if (v_.empty() || v_.back() < x) {
+      v_.push_back(x);
+      return;
+    }
+    auto it = std::lower_bound(v_.begin(), v_.end(), x);
+    if (it == v_.end() || *it != x) v_.insert(it, x);
+  }
+  template <typename Hint>
+  void emplace_hint(Hint, const T& x) { insert(x); }
+
+ private:
+  std::vector<T> v_;
+};
+
+template <typename K, typename V>
+class FlatMap {
+ public:
+  using value_type = std::pair<K, V>;
+  using iterator = typename std::vector<value_type>::iterator;
+  using const_iterator = typename std::vector<value_type>::const_iterator;
+  using const_reverse_iterator = typename std::vector<value_type>::const_reverse_iterator;
+  const_iterator begin() const { return v_.begin(); }
+  const_iterator end() const { return v_.end(); }
+  const_reverse_iterator rbegin() const { return v_.rbegin(); }
+  size_t size() const { return v_.size(); }
+  bool empty() const { return v_.empty(); }
+  const_iterator lower_bound(const K& k) const {
+    return std::lower_bound(v_.begin(), v_.end(), k, [](const value_type& e, const K& x) { return e.first < x; });
+  }
+  const_iterator upper_bound(const K& k) const {
+    return std::upper_bound(v_.begin(), v_.end(), k, [](const K& x, const value_type& e) { return x < e.first; });
+  }
+  const_iterator find(const K& k) const {
+    auto it = lower_bound(k);
+    return it != v_.end() && it->first == k ? it : v_.end();
+  }
+  size_t count(const K& k) const { return find(k) != v_.end() ? 1 : 0; }
+  // insert (k, x) unless k is present, as std::map::emplace_hint
+  template <typename Hint>
+  void emplace_hint(Hint, const K& k, const V& x) {
+    if (v_.empty() || v_.back().first < k) {
+      v_.emplace_back(k, x);
+      return;
+    }
+    auto it = std::lower_bound(v_.begin(), v_.end(), k, [](const value_type& e, const K& y) { return e.first < y; });
+    if (it == v_.end() || it->first != k) v_.emplace(it, k, x);
+  }
+  V& operator[](const K& k) {
+    auto it = std::lower_bound(v_.begin(), v_.end(), k, [](const value_type& e, const K& y) { return e.first < y; });
+    if (it == v_.end() || it->first != k) it = v_.emplace(it, k, V{});
+    return it->second;
+  }
+
+ private:
+  std::vector<value_type> v_;
+};
+
 // ---------------------------------------------------------------------------
 // Map (Map.hpp:112-444, MapNodes-inl.hpp:37-262)
 // ---------------------------------------------------------------------------
@@ -85,7 +158,7 @@ struct LandmarkNode {
   int32_t object_id = 0;
   // frames_seen_ and measurements_ (one entry per seen frame), ordered by
   // frame id (FrameNodePtrSet / FastMap<FrameNodePtr>)
-  std::map<uint64_t, std::array<double, 3>> measurements;
+  FlatMap<uint64_t, std::array<double, 3>> measurements;
   // observations made before the first one this map holds: 0 in a module's
   // map; a window's own map (deferred windows, built from the window's
   // frames alone) carries the count of the frames before the window here
@@ -112,8 +185,8 @@ struct LandmarkNode {
 
 struct FrameNode {
   uint64_t frame_id = 0;
-  std::set<int64_t> dynamic_landmarks, static_landmarks;  // by tracklet id
-  std::set<int32_t> objects_seen;
+  FlatSet<int64_t> dynamic_landmarks, static_landmarks;  // by tracklet id
+  FlatSet<int32_t> objects_seen;
   bool has_X = false;
   P3 X_world;
   bool has_motions = false;
@@ -123,7 +196,7 @@ struct FrameNode {
 
 struct ObjectNode {
   int32_t object_id = 0;
-  std::set<int64_t> dynamic_landmarks;
+  FlatSet<int64_t> dynamic_landmarks;
 };
 
 struct Map {
@@ -298,6 +371,16 @@ void values_insert(Values& vals, uint64_t key, const Value& v) {
 void values_insert(Values& vals, const Values& other) {
   for (const auto& kv : other) values_insert(vals, kv.first, kv.second);
 }
+
+// The new_values lists of the formulation's updates (the reference fills one
+// per call, Formulation-impl.hpp:83-584): every caller here discards them --
+// the module's spin, constructGraph (whose fresh theta_ holds the same
+// values) and the C-ABI updates -- and a key they would reject as a
+// duplicate is rejected by the theta insert made with it, or cannot arise
+// (is_other_values_in_map), so they are sinks
+struct NewValues {};
+inline void values_insert(NewValues&, uint64_t, const Value&) {}
+inline void values_insert(NewValues&, const Values&) {}
 // both maps ascend, so each key is tried next to the previous one first (O(1)
 // when the keys are adjacent in vals, as in a window's own theta)
 void values_insert_or_assign(Values& vals, const Values& other) {
@@ -456,6 +539,11 @@ struct Formulation {
   dynob_params params;
   NoiseModels noise;
   Values theta;
+  // theta has taken values from outside this formulation's own updates
+  // (updateTheta: a solve's merge). Until then a static landmark is in theta
+  // exactly when it is in is_other_values_in_map (both are set together), so
+  // a landmark not yet added needs no theta lookup
+  bool theta_external = false;
   Graph factors;
   // membership only (never iterated), hashed
   std::unordered_set<uint64_t> is_other_values_in_map;       // Formulation.hpp:448
@@ -608,7 +696,7 @@ struct Formulation {
   // same value into both. So theta takes just the values the call added: a
   // window's construction no longer re-assigns its growing new_values at
   // every frame.)
-  void set_initial_pose(uint64_t f, const P3& T, Values& new_values) {
+  void set_initial_pose(uint64_t f, const P3& T, NewValues& new_values) {
     const Value v = pose_value(T);
     values_insert(new_values, camera_pose_key(f), v);
     theta.insert_or_assign(camera_pose_key(f), v);
@@ -623,7 +711,7 @@ struct Formulation {
     factors.append(internal);
   }
   // Formulation::addOdometry (Formulation-impl.hpp:128-161)
-  void add_odometry(uint64_t f, const P3& T_world_camera, Values& new_values, Graph& new_factors) {
+  void add_odometry(uint64_t f, const P3& T_world_camera, NewValues& new_values, Graph& new_factors) {
     const Value v = pose_value(T_world_camera);
     values_insert(new_values, camera_pose_key(f), v);
     theta.insert_or_assign(camera_pose_key(f), v);
@@ -642,7 +730,7 @@ struct Formulation {
   }
 
   // Formulation::updateStaticObservations (Formulation-impl.hpp:203-305)
-  void update_static(uint64_t k, Values& new_values, Graph& new_factors, bool do_backtrack) {
+  void update_static(uint64_t k, NewValues& new_values, Graph& new_factors, bool do_backtrack) {
     FactorSink sink(factors, new_factors);
     Graph& internal = sink.out();
     const FrameNode* fk = map->frame(k);
@@ -664,7 +752,8 @@ struct Formulation {
              it != ln.measurements.end() && it->first <= k; ++it)
           internal.add(kPoseToPoint, {camera_pose_key(it->first), point_key}, it->second.data(), noise.static_point);
         double lmk_world[3];
-        if (!static_landmark(t, lmk_world)) transform_from(T_world_camera_frontend, ln.measurement(k), lmk_world);
+        if (!(theta_external && static_landmark(t, lmk_world)))
+          transform_from(T_world_camera_frontend, ln.measurement(k), lmk_world);
         const Value v = point_value(lmk_world);
         values_insert(new_values, point_key, v);
         added.emplace_back(point_key, v);
@@ -689,7 +778,7 @@ struct Formulation {
   // (the caller's theta and new_values both take the point's values; they go
   // into each directly, where the reference collects them in a local Values
   // first: same contents, same exception on a key already in theta)
-  void dynamic_point_update(const PointContext& c, UpdateResult& result, Values& new_values, Graph& nf) {
+  void dynamic_point_update(const PointContext& c, UpdateResult& result, NewValues& new_values, Graph& nf) {
     auto put = [&](uint64_t key, const Value& v) {
       values_insert(theta, key, v);
       values_insert(new_values, key, v);
@@ -796,7 +885,7 @@ struct Formulation {
   }
 
   // Formulation::updateDynamicObservations (Formulation-impl.hpp:307-584)
-  void update_dynamic(uint64_t k, Values& new_values, Graph& new_factors, bool do_backtrack) {
+  void update_dynamic(uint64_t k, NewValues& new_values, Graph& new_factors, bool do_backtrack) {
     constexpr size_t kMinNumberPoints = 3u;
     FactorSink sink(factors, new_factors);
     Graph& internal = sink.out();
@@ -1125,7 +1214,7 @@ std::unique_ptr<Formulation> construct_graph(Map* map, const dynob_params& p, ui
   DB_CHECK(from >= map->first_frame_id() && to <= map->last_frame_id(), DYNOHIP_ESTATE,
            "constructGraph: window outside the map");
   auto u = std::make_unique<Formulation>(map, p);
-  Values new_values;
+  NewValues new_values;
   Graph new_factors;
   new_factors.discard = true;   // u->factors is the window's graph
   // room for the window's factors up front (a PoseToPoint per static
@@ -1135,6 +1224,7 @@ std::unique_ptr<Formulation> construct_graph(Map* map, const dynob_params& p, ui
   for (uint64_t f = from; f <= to; ++f)
     if (const FrameNode* fn = map->frame(f)) est += fn->static_landmarks.size() + 3 * fn->dynamic_landmarks.size() + 4;
   u->factors.factors.reserve(est);
+  u->is_other_values_in_map.reserve(est);
   for (uint64_t f = from; f <= to; ++f) {
     P3 T;
     DB_CHECK(map->initial_sensor_pose(f, &T), DYNOHIP_ESTATE, "no frontend pose for frame " + std::to_string(f));
@@ -1416,6 +1506,7 @@ void update_theta(Formulation& up, const ValuesExport& vals, const std::vector<d
     opt[vals.keys[i]] = v;
   }
   values_insert_or_assign(up.theta, opt);
+  up.theta_external = true;
 }
 
 // LM on the exported problem (export_problem first), then updateTheta
@@ -1464,7 +1555,7 @@ void record_interval(Statistics& st, const std::string& tag, double ms) {
 // (RGBDBackendModule.cc:154-199): odometry, static and dynamic observations
 void construct_frame(dynob_module* m, uint64_t k, const P3& T_k) {
   Formulation& up = *m->updater.f;
-  Values nv;
+  NewValues nv;
   Graph nf;
   nf.discard = true;   // the spin's new factors are only kept in the updater's factors_
   up.add_odometry(k, T_k, nv, nf);
@@ -1521,7 +1612,7 @@ void run_op(dynob_module* m, ModuleOp& op, dynob_spin_result* r) {
   const FrameNode* fn = m->map.map.frame(op.k);
   switch (op.kind) {
     case ModuleOp::kBootstrap: {
-      Values nv;
+      NewValues nv;
       Graph nf;
       nf.discard = true;
       up.set_initial_pose(op.k, fn->X_world, nv);
@@ -1782,7 +1873,7 @@ const char* dynob_formulation_last_error(const dynob_formulation* f) { return f 
 int dynob_set_initial_pose(dynob_formulation* f, uint64_t frame_id, const double* pose12) {
   if (!f || !pose12) return DYNOHIP_EINVAL;
   return guard(f->f->err, [&] {
-    Values nv;
+    NewValues nv;
     f->f->set_initial_pose(frame_id, pose_from(pose12), nv);
   });
 }
@@ -1796,7 +1887,7 @@ int dynob_set_initial_pose_prior(dynob_formulation* f, uint64_t frame_id, const 
 int dynob_add_odometry(dynob_formulation* f, uint64_t frame_id, const double* pose12) {
   if (!f || !pose12) return DYNOHIP_EINVAL;
   return guard(f->f->err, [&] {
-    Values nv;
+    NewValues nv;
     Graph nf;
     f->f->add_odometry(frame_id, pose_from(pose12), nv, nf);
   });
@@ -1804,7 +1895,7 @@ int dynob_add_odometry(dynob_formulation* f, uint64_t frame_id, const double* po
 int dynob_update_static_observations(dynob_formulation* f, uint64_t frame_id, int do_backtrack) {
   if (!f) return DYNOHIP_EINVAL;
   return guard(f->f->err, [&] {
-    Values nv;
+    NewValues nv;
     Graph nf;
     f->f->update_static(frame_id, nv, nf, do_backtrack != 0);
   });
@@ -1812,7 +1903,7 @@ int dynob_update_static_observations(dynob_formulation* f, uint64_t frame_id, in
 int dynob_update_dynamic_observations(dynob_formulation* f, uint64_t frame_id, int do_backtrack) {
   if (!f) return DYNOHIP_EINVAL;
   return guard(f->f->err, [&] {
-    Values nv;
+    NewValues nv;
     Graph nf;
     f->f->update_dynamic(frame_id, nv, nf, do_backtrack != 0);
   });
@@ -1834,6 +1925,7 @@ int dynob_update_theta(dynob_formulation* f, const uint64_t* keys, const uint8_t
       v[keys[i]] = x;
     }
     values_insert_or_assign(f->f->theta, v);
+    f->f->theta_external = true;
   });
 }
 
@@ -2242,7 +2334,7 @@ int dynob_module_spin(dynob_module* m, const dynob_input_packet* in, dynob_spin_
       while (m->frame_log.front()->k + static_cast<uint64_t>(m->mp.opt_window_size) < k) m->frame_log.pop_front();
     }
     if (deferred(m)) return spin_deferred(m, k, r);
-    Values nv;
+    NewValues nv;
     Graph nf;
     nf.discard = true;   // the spin's new factors are only kept in the updater's factors_
     if (!m->bootstrapped) {
