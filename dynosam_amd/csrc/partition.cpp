@@ -126,7 +126,10 @@ int build_partitioned_plan(const dynohip_graph_view& g, const uint64_t* keys, co
     return o;
   };
   // a separator node's factors and chains go to its group's leader
-  auto to_rank = [&](int32_t o) { return o >= 0 ? o : o == kOwnNone ? 0 : nodes[sep_node(o)].r0; };
+  // (a conflict maps to rank 0 here; the caller reports it as an error)
+  auto to_rank = [&](int32_t o) {
+    return o >= 0 ? o : (o == kOwnNone || o == kOwnConflict) ? 0 : nodes[sep_node(o)].r0;
+  };
   std::vector<int32_t> comp_of(G.n_pt);
   parallel_for(G.n_comp, [&](int64_t c0, int64_t c1) {
     for (int64_t c = c0; c < c1; ++c)
@@ -327,6 +330,7 @@ extern "C" int dynohip_plan_export(const dynohip_graph_view* g, const uint64_t* 
     vec(tmp);
   } else if (nm == "tile_pos") vec(P.tile_pos);
   else if (nm == "tile_owner") vec(P.tile_owner);
+  else if (nm == "pose_key") raw(P.pose_key.data(), P.pose_key.size() * sizeof(uint64_t));   // reduced pose order
   else if (nm == "row_start") vec(P.row_start);
   else if (nm == "row_col") vec(P.row_col);
   else if (nm == "row_slot") vec(P.row_slot);

@@ -275,6 +275,78 @@ def test_partitioned_replay_uneven_density():
     assert tiles[0] + tiles[1] < tiles[2] + tiles[3], tiles
 
 
+def _with_between(graph, ka, kb):
+    """the graph plus one Between<Pose3> factor on (ka, kb)"""
+    from dynosam_amd.graph import NonlinearFactorGraph
+    arr = dict(graph.arrays())
+    keys, meas, sig, hub = arr["between"]
+    m12 = np.concatenate([np.eye(3).reshape(-1), np.zeros(3)])
+    arr["between"] = (np.vstack([keys, np.array([[ka, kb]], dtype=np.uint64)]), np.vstack([meas, m12[None]]),
+                      np.vstack([sig, np.full((1, sig.shape[1]), 0.1)]), np.concatenate([hub, [0.0]]))
+    return NonlinearFactorGraph.from_arrays(arr)
+
+
+def test_separator_to_separator_factor_four_ranks():
+    """At 4 ranks a left subtree's reach is clipped at its end, so tiles of
+    its depth-2 separator can neighbour the top separator's. A factor whose
+    poses lie only in those two separators (here a Between on a pose pair
+    the graph already couples, so the dissection is unchanged) goes to the
+    leader of the deeper node (partition.cpp merge_owner), every factor is
+    owned once, and the partitioned plan still solves the system exactly
+    (the numpy replay). Before round 6 such a factor made the plan fail."""
+    kw = dict(frames=60, objects=2, static_landmarks=2000, dyn_slots=8)
+    graph, values, _ = synth.generate(None, **kw)
+    own = plan_export(graph, values, "tile_owner", 4, 0)
+    nodes = sep_nodes(export_all(graph, values, 4, 0))
+    glob = plan_schedule(graph, values)
+    order = plan_export(graph, values, "pose_key", 4, 0).view(np.uint64)
+    tiles = lambda p: range(6 * p // T, (6 * p + 5) // T + 1)
+    pair = None
+    for a, b in zip(glob["red_a"], glob["red_b"]):
+        codes = {int(own[t]) for t in tiles(a)} | {int(own[t]) for t in tiles(b)}
+        if all(c < 0 for c in codes) and {int(nodes[-1 - c][2]) for c in codes} == {1, 2}:
+            pair = (int(a), int(b))
+            break
+    assert pair is not None, "no pose pair couples a depth-2 separator with the top one"
+    g2 = _with_between(graph, int(order[pair[0]]), int(order[pair[1]]))
+    assert np.array_equal(plan_export(g2, values, "tile_owner", 4, 0), own)
+    infos = [plan_export(g2, values, "info", 4, r) for r in range(4)]
+    assert sum(int(i[5]) for i in infos) == int(infos[0][6]) == g2.size()
+    # replay the partitioned solve of the crafted graph
+    plans = [export_all(g2, values, 4, r) for r in range(4)]
+    rng = np.random.default_rng(3)
+    g2s = plan_schedule(g2, values)
+    M = random_spd(g2s["n_pose"], g2s["n_tiles"], g2s["red_a"], g2s["red_b"], rng)
+    rhs = rng.standard_normal(M.shape[0])
+    Ms, rs = split(M, rhs, own, 4, rng)
+    states = [RankState(plans[r], Ms[r], rs[r]) for r in range(4)]
+    for st in states:
+        st.forward(st.p["ftask"], st.p["flevel"])
+        st.sep_rhs(st.p["rhs0_tile"], st.p["rhs0_start"], st.p["rhs0_slot"], True)
+    nph = len(plans[0]["phase"])
+    for ph in range(nph):
+        px = plans[0]["phase"][ph]
+        for b0, e0 in px["xslot"].reshape(-1, 2):
+            tot = sum(st.slots[b0:e0] for st in states)
+            for st in states:
+                st.slots[b0:e0] = tot
+        for b0, e0 in px["xtile"].reshape(-1, 2):
+            tot = sum(st.r[b0:e0] for st in states)
+            for st in states:
+                st.r[b0:e0] = tot
+        for st in states:
+            leader = int(st.p["phases"][2 * ph + 1])
+            F = st.p["phase"][ph]
+            st.forward(F["ftask"], F["flevel"])
+            st.sep_rhs(F["rhs_tile"], F["rhs_start"], F["rhs_slot"], bool(leader))
+    ref = np.linalg.solve(M, rhs).reshape(-1, T)
+    for r, st in enumerate(states):
+        st.backward()
+        path = {sep_code(int(st.p["phases"][2 * ph])) for ph in range(nph)}
+        mine = [t for t in range(st.NT) if own[t] == r or own[t] in path]
+        assert np.allclose(st.x[mine], ref[mine], rtol=1e-9, atol=1e-10), r
+
+
 def test_partition_ownership():
     graph, values, _ = synth.generate("C2")
     nranks = 4
