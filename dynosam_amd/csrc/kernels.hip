@@ -613,9 +613,6 @@ struct SumDev {
   double* extra_out = nullptr;
 };
 
-__device__ __forceinline__ double ld_sc1(const double* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 __device__ __forceinline__ void st_sc1(double* p, double v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1804,7 +1801,7 @@ __device__ void lone_schur_block(const LoneSchurDev& d, int gb, double* __restri
   for (int q = tid; q < kLoneBlk; q += kBlock) hdr[q] = d.blk[static_cast<int64_t>(gb) * kLoneBlk + q];
   __syncthreads();
   LCLK(1);
-  const int m = hdr[0], npt = hdr[1], m18 = 18 * m, np = m * (m + 1) / 2, ntask = 6 * np + 6 * m;
+  const int m = hdr[0], npt = hdr[1], m18 = 18 * m, np = m * (m + 1) / 2;
   const int32_t* spt = hdr + kLoneHdrPt;
   const int32_t* se0 = hdr + kLoneHdrE0;
   const int32_t* srec = hdr + kLoneHdrRec;
