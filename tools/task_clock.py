@@ -128,6 +128,21 @@ def main():
     late_pick = np.maximum(0.0, t[0] - ready)   # ready before a worker took it
     out["ready_before_pick_us"] = {"mean": float(late_pick.mean()), "max": float(late_pick.max()),
                                    "tasks_over_2us": int((late_pick > 2.0).sum())}
+    # per panel, when its pending operands were written: the diagonal one
+    # (pd, L(k,c)) and the own pair's first one (qa, L(i,c)); -1 if none
+    pairs = plan_export(graph, values, "pairs").reshape(-1, 2)
+
+    def operand_end(q, sl):
+        for j in range(fs[q], fs[q + 1]):
+            if int(fd[j, 0]) == sl:
+                return float(t[4, writer[(sl, int(fd[j, 1]))]])
+        return -1.0
+
+    def operands(q):
+        pd = int(pairs[ft[q, 5], 0]) if ft[q, 6] - ft[q, 5] == 1 else -1
+        qa = int(pairs[ft[q, 7], 0]) if kk[q] != ii[q] and ft[q, 8] - ft[q, 7] == 1 else -1
+        return {"pd_end": operand_end(q, pd) if pd >= 0 else -1.0,
+                "qa_end": operand_end(q, qa) if qa >= 0 else -1.0}
     dchain = []
     cur = int(np.argmax(t[4]))
     while cur >= 0:
@@ -142,7 +157,8 @@ def main():
                          # pending diagonal block, factorisation, TRSM + stores
                          **({"to_loaded": float(sub[0, q] - ready[q]), "to_lds": float(sub[1, q] - sub[0, q]),
                              "pend": float(t[2, q] - sub[1, q]), "fac": float(t[3, q] - t[2, q]),
-                             "post": float(t[4, q] - t[3, q])} if kind[q] == 0 else {})} for q in dchain]
+                             "post": float(t[4, q] - t[3, q]), **operands(q)} if kind[q] == 0 else {})}
+                         for q in dchain]
     # chain ending last
     chain = []
     cur = int(np.argmax(t[4]))
