@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "../../include/dynobackend.h"
+#include "prepared.hpp"
 #include "se3.hpp"
 
 namespace dynob {
@@ -1278,6 +1279,10 @@ struct WindowJob {
   dynohip_lm_summary summary{};
   int rc = DYNOHIP_OK;
   std::string err;
+  // the window's solver plan, built on the builder thread after the
+  // construction (null: the solver handle plans)
+  std::unique_ptr<dynohip::PreparedPlan, void (*)(dynohip::PreparedPlan*)> plan{nullptr, dynohip::free_prepared_plan};
+  double ms_plan = 0.0;       // that planning (part of the window's optimise time, as on the handle)
   double ms_solve = 0.0;      // set_graph .. get_values on the worker
   double ms_construct = 0.0;  // the window's construction on the spin's thread
   std::mutex mu;
@@ -1294,7 +1299,8 @@ struct WindowJob {
 };
 
 // Worker threads in two stages. Builders construct the windows that come
-// with their own frames (WindowMap; CPU work); solvers, each with its own
+// with their own frames (WindowMap; CPU work) and plan their solves
+// (prepared.hpp: the planner's host work off the solver threads); solvers, each with its own
 // solver handle (own HIP stream and device buffers), take built windows in
 // submission order and run their LM, several windows' solves in flight on the
 // device at once (one 10-frame window's kernels occupy a handful of CUs, and
@@ -1304,7 +1310,8 @@ class WindowWorkers {
  public:
   WindowWorkers(int n, int device, const dynohip_lm_params& lm, bool optimize)
       : device_(device), lm_(lm), optimize_(optimize) {
-    const int builders = std::max(1, (n + 1) / 2);
+    // (builders also plan each window's solve when the module optimises)
+    const int builders = std::max(1, optimize ? n : (n + 1) / 2);
     for (int i = 0; i < builders; ++i) threads_.emplace_back([this] { build_loop(); });
     if (optimize_)
       for (int i = 0; i < n; ++i) threads_.emplace_back([this] { solve_loop(); });
@@ -1359,7 +1366,7 @@ class WindowWorkers {
   }
   void build_loop() {
     while (std::shared_ptr<WindowJob> j = take(qb_, cv_build_)) {
-      build(j.get());
+      build(j.get(), optimize_);
       to_solve(std::move(j));
     }
   }
@@ -1371,7 +1378,9 @@ class WindowWorkers {
     }
     if (solver) dynohip_destroy(solver);
   }
-  static void build(WindowJob* j) {
+  // the window's graph, then (plan: the module optimises) its solver plan,
+  // so that the solver threads only upload it and run the LM
+  static void build(WindowJob* j, bool plan) {
     const auto tc = std::chrono::steady_clock::now();
     try {
       WindowMap wm(j->frames);
@@ -1386,7 +1395,18 @@ class WindowWorkers {
       j->rc = DYNOHIP_EINVAL;
       j->err = e.what();
     }
-    j->ms_construct = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc).count();
+    const auto tp = std::chrono::steady_clock::now();
+    j->ms_construct = std::chrono::duration<double, std::milli>(tp - tc).count();
+    if (plan && j->rc == DYNOHIP_OK) {
+      // (a failed plan leaves it to the handle, which reports the error)
+      dynohip_graph_view gv;
+      j->graph.view(&gv);
+      int prc = DYNOHIP_OK;
+      std::string perr;
+      j->plan.reset(dynohip::prepare_plan(gv, j->values.keys.data(), j->values.kinds.data(), j->values.keys.size(),
+                                          prc, perr));
+      j->ms_plan = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp).count();
+    }
   }
   void solve(WindowJob* j, dynohip_solver*& solver) {
     const auto t0 = std::chrono::steady_clock::now();
@@ -1401,14 +1421,15 @@ class WindowWorkers {
     j->graph.view(&gv);
     rc = dynohip_set_graph(solver, &gv);
     if (rc == DYNOHIP_OK)
-      rc = dynohip_set_values(solver, j->values.keys.data(), j->values.kinds.data(), j->values.data.data(),
-                              j->values.keys.size());
+      rc = dynohip::set_values_prepared(solver, j->plan.get(), j->values.keys.data(), j->values.kinds.data(),
+                                        j->values.data.data(), j->values.keys.size());
+    j->plan.reset();   // (now the handle's previous plan)
     if (rc == DYNOHIP_OK) rc = dynohip_optimize(solver, &lm_, &j->summary);
     j->optimised.assign(j->values.data.size(), 0.0);
     if (rc == DYNOHIP_OK) rc = dynohip_get_values(solver, j->optimised.data(), j->optimised.size());
     if (rc != DYNOHIP_OK) j->err = std::string("LM solve failed: ") + dynohip_last_error(solver);
     j->rc = rc;
-    j->ms_solve = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    j->ms_solve = j->ms_plan + std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   }
   std::vector<std::thread> threads_;
   std::deque<std::shared_ptr<WindowJob>> qb_, qs_;   // to build, to solve

@@ -25,6 +25,7 @@
 #include "../../include/dynohip.h"
 #include "kernels.hpp"
 #include "plan.hpp"
+#include "prepared.hpp"
 #include "plan_pool.hpp"
 
 using namespace dynohip;
@@ -1474,14 +1475,65 @@ int refresh_records(dynohip_solver* s) {
   return DYNOHIP_OK;
 }
 
-int dynohip_set_values(dynohip_solver* s, const uint64_t* keys, const uint8_t* kind, const double* data, size_t n) {
+}  // extern "C"
+
+namespace dynohip {
+struct PreparedPlan {
+  Plan plan;
+};
+PreparedPlan* prepare_plan(const dynohip_graph_view& g, const uint64_t* keys, const uint8_t* kind, size_t n, int& rc,
+                           std::string& err) {
+  auto* p = new PreparedPlan;
+  try {
+    rc = build_plan(g, keys, kind, n, p->plan, err, 1, 0, true, false, nullptr);
+  } catch (const std::exception& ex) {
+    rc = DYNOHIP_EINVAL;
+    err = std::string("planner: ") + ex.what();
+  }
+  if (rc == DYNOHIP_OK) return p;
+  delete p;
+  return nullptr;
+}
+void free_prepared_plan(PreparedPlan* p) { delete p; }
+}  // namespace dynohip
+
+namespace {
+int set_values_impl(dynohip_solver* s, const uint64_t* keys, const uint8_t* kind, const double* data, size_t n,
+                    Plan* pre);
+}
+
+namespace dynohip {
+int set_values_prepared(dynohip_solver* s, PreparedPlan* p, const uint64_t* keys, const uint8_t* kind,
+                        const double* data, size_t n) {
+  return set_values_impl(s, keys, kind, data, n, p ? &p->plan : nullptr);
+}
+}  // namespace dynohip
+
+namespace {
+// pre: a plan built by prepare_plan for this handle's graph and these keys
+// (taken instead of planning here; the handle's previous plan goes to *pre)
+int set_values_impl(dynohip_solver* s, const uint64_t* keys, const uint8_t* kind, const double* data, size_t n,
+                    Plan* pre) {
   if (!s || (n && (!keys || !kind || !data))) return DYNOHIP_EINVAL;
   if (!s->has_graph) return set_err(s, DYNOHIP_ESTATE, "set_graph first");
   (void)hipSetDevice(s->device);
   s->error_fresh = false;
   const bool same = s->has_plan && s->value_keys.size() == n &&
                     std::equal(s->value_keys.begin(), s->value_keys.end(), keys);
-  if (!same) {
+  if (!same && pre && s->nranks == 1) {
+    // the prepared plan: only its upload is left
+    HIPCHK(s, hipStreamSynchronize(s->stream));   // (as below: nothing may still run on the buffers)
+    s->has_plan = false;
+    std::swap(s->plan, *pre);
+    int rc = upload_plan(s, false);
+    if (rc) return rc;
+    s->value_keys.assign(keys, keys + n);
+    s->value_kind.assign(kind, kind + n);
+    s->has_plan = true;
+    s->records_stale = false;
+    ++s->plan_gen;
+    s->base_stats_valid = false;
+  } else if (!same) {
     const auto tb0 = std::chrono::steady_clock::now();
     // re-planning may grow device buffers, whose old blocks then go to the
     // process-wide pool: nothing of this handle may still run on them (the
@@ -1573,6 +1625,12 @@ int dynohip_set_values(dynohip_solver* s, const uint64_t* keys, const uint8_t* k
                  std::chrono::duration<double, std::milli>(tv1 - tv0).count(),
                  std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tv1).count());
   return rc;
+}
+}  // namespace
+
+extern "C" {
+int dynohip_set_values(dynohip_solver* s, const uint64_t* keys, const uint8_t* kind, const double* data, size_t n) {
+  return set_values_impl(s, keys, kind, data, n, nullptr);
 }
 
 int dynohip_get_values(dynohip_solver* s, double* out, size_t n_doubles) {
