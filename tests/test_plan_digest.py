@@ -61,3 +61,30 @@ def test_small_plan_cap_equals_threaded_plan(tmp_path):
     for k in capped:
         diff = np.nonzero((capped[k].reshape(-1, 2) != threaded[k].reshape(-1, 2)).any(1))[0]
         assert diff.size == 0, "%s: fields %s differ" % (k, diff.tolist())
+
+
+def test_value_key_index_errors_on_a_large_graph():
+    """plan.cpp KeyIndex over a C2-sized value list (30k values):
+    a duplicated value key or a bad value kind at the start, the middle or
+    the end is reported (DYNOHIP_EINVAL), and the same graph without the
+    defect plans."""
+    from dynosam_amd import synth
+    from dynosam_amd.graph import Values
+    from dynosam_amd.optimizer import DynohipError, plan_export
+    g, v, _ = synth.generate("C2")
+    assert plan_export(g, v, "info")[0] > 0
+    for where in (1, len(v) // 2, len(v) - 1):
+        keys = v.keys.copy()
+        keys[where] = keys[where - 1]   # a duplicate (the earlier copy keeps its index)
+        try:
+            plan_export(g, Values(keys, v.kinds, v.data), "info")
+            raise AssertionError("duplicate value key accepted")
+        except DynohipError as e:
+            assert e.code == -1   # DYNOHIP_EINVAL
+        kinds = v.kinds.copy()
+        kinds[where] = 7
+        try:
+            plan_export(g, Values(v.keys, kinds, v.data), "info")
+            raise AssertionError("bad value kind accepted")
+        except DynohipError as e:
+            assert e.code == -1
