@@ -23,6 +23,7 @@ namespace dynohip {
 namespace {
 
 constexpr int kBlock = 256;
+static_assert(kBlock == kRedBlock, "the planner's reduced-gather block table assumes this block size");
 typedef double v4d __attribute__((ext_vector_type(4)));
 
 inline int nblocks(int64_t n, int b = kBlock) { return static_cast<int>((n + b - 1) / b); }
@@ -1204,14 +1205,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(DYNOHIP_
   }
   if (hb < r.nb_grad + r.nb_band) hb -= r.nb_grad;
   if (hb < r.nb_band) {
-    // dispatch position d runs class cls[d]: targets order[ooff[c], + ncls[c])
-    int d = 0;
+    int c, blk;
+    if (r.blocks) {
+      // the plan's block table (Plan::red_blocks): column bands, each XCD a
+      // contiguous part of it
+      const int e = r.blocks[xcd_block(hb, r.nb_band)];
+      c = e & 7;
+      blk = e >> 3;
+    } else {
+      // dispatch position d runs class cls[d]: targets order[ooff[c], + ncls[c])
+      int d = 0;
 #pragma unroll
-    for (int k = 1; k < ReducedGatherDev::kClasses; ++k)
-      if (hb >= r.bstart[k]) d = k;
-    const int c = r.cls[d];
-    const int nbc = r.bstart[d + 1] - r.bstart[d];
-    const int blk = xcd_block(hb - r.bstart[d], nbc);
+      for (int k = 1; k < ReducedGatherDev::kClasses; ++k)
+        if (hb >= r.bstart[k]) d = k;
+      c = r.cls[d];
+      const int nbc = r.bstart[d + 1] - r.bstart[d];
+      blk = xcd_block(hb - r.bstart[d], nbc);
+    }
     const int32_t* ord = r.order + r.ooff[c];
 #define DH_GB(G) gather_band<G>(r.band, ord, r.ncls[c], r.tA, r.tB, r.tslot, blk, arena, b, lambda, r.damp)
     switch (c) {
@@ -2451,7 +2461,7 @@ void launch_gather_point(const GatherDev (&g)[4], double* const (&dst)[4], const
 void launch_gather_reduced(const GatherDev& band, const int32_t* order, const int32_t* ncls, const int32_t* tA,
                            const int32_t* tB, const uint32_t* tslot, const GatherDev& grad,
                            double* gred, const double* arena, const TileDev& b, double lambda, hipStream_t s,
-                           const uint8_t* damp) {
+                           const uint8_t* damp, const int32_t* blocks, int n_blocks) {
   ReducedGatherDev r;
   r.damp = damp;
   r.band = band;
@@ -2481,6 +2491,10 @@ void launch_gather_reduced(const GatherDev& band, const int32_t* order, const in
   r.grad = grad;
   r.gred = gred;
   r.nb_band = r.bstart[ReducedGatherDev::kClasses];
+  if (blocks) {   // the plan's column-ordered block table (no per-class padding)
+    r.blocks = blocks;
+    r.nb_band = n_blocks;
+  }
   r.nb_grad = (nblocks(static_cast<int64_t>(grad.n) * 64) + 7) / 8 * 8;
   const int nb = r.nb_band + r.nb_grad + nblocks(std::max(0, b.NT * kTile - b.n_red));
   if (nb == 0) return;

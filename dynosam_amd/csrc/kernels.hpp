@@ -59,6 +59,8 @@ struct ReducedGatherDev {
   double* gred = nullptr;
   int nb_band = 0, nb_grad = 0;
   const uint8_t* damp = nullptr;  // partitioned: per reduced row, 1 = this rank adds lambda (null: every row)
+  // Plan::red_blocks (null: each class's blocks in turn, bstart/cls)
+  const int32_t* blocks = nullptr;
 };
 
 // buffers zeroed by the blocks past the chains in k_chain_factor, and
@@ -181,7 +183,7 @@ void launch_gather_point(const GatherDev (&g)[4], double* const (&dst)[4], const
 void launch_gather_reduced(const GatherDev& band, const int32_t* order, const int32_t* ncls, const int32_t* tA, const int32_t* tB, const uint32_t* tslot,
                            const GatherDev& grad,
                            double* gred, const double* arena, const TileDev& b, double lambda, hipStream_t s,
-                           const uint8_t* damp = nullptr);
+                           const uint8_t* damp = nullptr, const int32_t* blocks = nullptr, int n_blocks = 0);
 // partitioned: r[rows of separator tile] -= sum of this rank's contributions
 // L(s,c) y_c (c interior), which are then zeroed; CSR over separator tiles
 // Plan upload: one host-to-device copy of a staged block, then this kernel

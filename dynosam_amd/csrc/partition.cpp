@@ -375,6 +375,7 @@ extern "C" int dynohip_plan_export(const dynohip_graph_view* g, const uint64_t* 
   else if (nm == "bent") vec(P.bent);
   else if (nm == "red_a") vec(P.red_A);
   else if (nm == "red_order") vec(P.red_order);
+  else if (nm == "red_blocks") vec(P.red_blocks);
   else if (nm.size() > 6 && nm.compare(nm.size() - 6, 6, "_start") == 0) {  // gather lists, e.g. "gRed_start"
     const std::string gl = nm.substr(0, nm.size() - 6);
     const GatherList* G = gl == "gD" ? &P.gD : gl == "gE" ? &P.gE : gl == "gGp" ? &P.gGp : gl == "gW" ? &P.gW
@@ -442,7 +443,7 @@ extern "C" int dynohip_plan_export(const dynohip_graph_view* g, const uint64_t* 
       v(P.types[t].idx); v(P.types[t].meas); v(P.types[t].isig); v(P.types[t].hk);
     }
     for (const GatherList* G : {&P.gD, &P.gE, &P.gGp, &P.gW, &P.gRed, &P.gGred}) { v(G->start); v(G->ent); }
-    v(P.red_A); v(P.red_B); v(P.red_slot); v(P.red_order);
+    v(P.red_A); v(P.red_B); v(P.red_slot); v(P.red_order); v(P.red_blocks);
     v(P.lgroup); v(P.lone_pose); v(P.lone_blk); v(P.lin_list0);
     v(P.band_D); v(P.tile_pos); v(P.row_start); v(P.row_col); v(P.row_slot);
     v(P.ftask); v(P.pairs); v(P.flevel); v(P.fpanels); v(P.fdep_start); v(P.fdep); v(P.fqueue);

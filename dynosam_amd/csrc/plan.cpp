@@ -213,12 +213,37 @@ void compute_red_slots(Plan& P) {
   for (int c = 0; c < Plan::kRedClasses; ++c) P.red_ncls[c] = 0;
   if (P.gRed.start.size() != static_cast<size_t>(nt) + 1) {   // no band gather (structure-only plans)
     P.red_order.clear();
+    P.red_blocks.clear();
     return;
   }
   for (int64_t t = 0; t < nt; ++t) ++P.red_ncls[cls(t)];
   for (int c = 0; c < Plan::kRedClasses; ++c) pos[c + 1] = pos[c] + P.red_ncls[c];
   P.red_order.resize(static_cast<size_t>(nt));
   for (int64_t t = 0; t < nt; ++t) P.red_order[pos[cls(t)]++] = static_cast<int32_t>(t);
+  // The band blocks by column. Every class spans every column (a column's
+  // targets near the diagonal have the most entries, the far ones the
+  // fewest), so class after class each pass streamed the chains' W and Y
+  // blocks again (NS: 2.4x the deduplicated operand bytes from HBM). In
+  // column order the classes' blocks of one column band run together, on
+  // one XCD (xcd_block), and share those operands in its L2.
+  struct Blk {
+    int32_t col, cls, k;
+  };
+  std::vector<Blk> blks;
+  int32_t off = 0;
+  for (int c = 0; c < Plan::kRedClasses; ++c) {
+    const int lanes = c < Plan::kRedClasses - 1 ? 8 << c : 128;
+    const int per = kRedBlock / lanes;   // targets per block
+    for (int32_t k = 0; k * per < P.red_ncls[c]; ++k)
+      blks.push_back(Blk{P.red_B[P.red_order[off + k * per]], c, k});
+    off += P.red_ncls[c];
+  }
+  // (larger classes first within a column: their targets hold the longest entry chains)
+  std::stable_sort(blks.begin(), blks.end(), [](const Blk& a, const Blk& b) {
+    return a.col < b.col || (a.col == b.col && a.cls > b.cls);
+  });
+  P.red_blocks.resize(blks.size());
+  for (size_t i = 0; i < blks.size(); ++i) P.red_blocks[i] = (blks[i].k << 3) | blks[i].cls;
 }
 
 void plan_recycle(Plan& P) {
@@ -243,6 +268,7 @@ void plan_recycle(Plan& P) {
     k((f.*m).ent, (P.*m).ent);
   }
   k(f.red_A, P.red_A); k(f.red_B, P.red_B); k(f.red_slot, P.red_slot); k(f.red_order, P.red_order);
+  k(f.red_blocks, P.red_blocks);
   k(f.lgroup, P.lgroup); k(f.lone_pose, P.lone_pose); k(f.lone_blk, P.lone_blk); k(f.lin_list0, P.lin_list0);
   k(f.band_D, P.band_D); k(f.tile_pos, P.tile_pos); k(f.row_start, P.row_start); k(f.row_col, P.row_col);
   k(f.row_slot, P.row_slot); k(f.ftask, P.ftask); k(f.pairs, P.pairs); k(f.flevel, P.flevel);

@@ -44,6 +44,7 @@ constexpr int kSlotKind[kNTypes][4] = {{0, 1, -1, -1}, {1, 1, 0, -1}, {0, 0, -1,
 constexpr int kColStart[kNTypes][4] = {{0, 6, 0, 0}, {0, 3, 6, 0}, {0, 6, 0, 0},
                                        {0, 0, 0, 0}, {0, 3, 6, 12}, {0, 6, 12, 0}};
 constexpr int kTile = 64;
+constexpr int kRedBlock = 256;   // threads of a k_gather_reduced workgroup (kernels.hip kBlock)
 
 // sum_e sign * A_e^T B_e, A_e: k x R, B_e: k x C (row-major blocks);
 // sign kAddBlock: A_e is the R x R identity (a = Plan::off_I6), and the
@@ -226,6 +227,12 @@ struct Plan {
   static constexpr int kRedClasses = 5;
   std::vector<int32_t> red_order;
   int32_t red_ncls[kRedClasses] = {};
+  // k_gather_reduced's band blocks in column order: entry (k << 3) | c is
+  // block k of class c (its targets red_order[class offset + k * per-block
+  // targets ...]), blocks sorted by the column (red_B) of their first
+  // target, so every class's targets of a column band run at the same time
+  // and on the same XCD (plan.cpp compute_red_slots)
+  std::vector<int32_t> red_blocks;
   // lone-point groups (k_lone_schur); their points' factor pairs and
   // component pairs are not in gRed / gGred
   std::vector<LoneGroup> lgroup;

@@ -437,6 +437,8 @@ struct dynohip_solver {
   DevBuf<int32_t> redA, redB;
   DevBuf<uint32_t> redslot;
   DevBuf<int32_t> redorder;   // Plan::red_order (targets by entry count)
+  DevBuf<int32_t> redblocks;  // Plan::red_blocks (the band blocks in column order)
+  bool red_blocks_env = true; // DYNOHIP_RED_BLOCKS=0: each class's blocks in turn (A/B)
   DevBuf<int32_t> comp_start, comp_nb_start, nb_comp, nbedge_start, nbedge_pt, pt_edge_start, edge_pose, edge_pt;
   DevBuf<int64_t> comp_y_base;
   DevBuf<uint32_t> nbedge_w;
@@ -607,6 +609,7 @@ int upload_plan(dynohip_solver* s, bool types_done = false) {
       return set_err(s, DYNOHIP_ESTRUCT, "internal: reduced-gather target classes do not cover the targets");
   }
   HIPCHK(s, up.add(s->redorder, P.red_order));
+  HIPCHK(s, up.add(s->redblocks, P.red_blocks));
   HIPCHK(s, up.add(s->comp_start, P.comp_start));
   HIPCHK(s, up.add(s->comp_nb_start, P.comp_nb_start));
   HIPCHK(s, up.add(s->nb_comp, P.nb_comp));
@@ -912,7 +915,9 @@ int enqueue_try(dynohip_solver* s, double lambda) {
   if (timed) (void)hipEventRecord(s->ev[3], st);
   launch_gather_reduced(s->gRed.dev(P.gRed.ntargets()), s->redorder.p, P.red_ncls, s->redA.p, s->redB.p, s->redslot.p,
                         s->gGred.dev(P.gGred.ntargets()),
-                        s->gred.p, A, s->bd, lambda, st, s->nranks > 1 ? s->damp.p : nullptr);
+                        s->gred.p, A, s->bd, lambda, st, s->nranks > 1 ? s->damp.p : nullptr,
+                        s->red_blocks_env && !P.red_blocks.empty() ? s->redblocks.p : nullptr,
+                        static_cast<int>(P.red_blocks.size()));
   if (timed) (void)hipEventRecord(s->ev[4], st);
   double* y = s->xy.p;
   double* x = s->xy.p + nrp;
@@ -1304,6 +1309,7 @@ int dynohip_create(int device_id, dynohip_solver** out) {
   if (const char* e = std::getenv("DYNOHIP_BACK_POLL")) s->sd.back_poll = std::atoi(e) != 0;
   if (const char* e = std::getenv("DYNOHIP_CHAIN_LONE")) s->chain_lone = std::atoi(e) != 0;
   if (const char* e = std::getenv("DYNOHIP_SMALL_SOLVE")) s->small_solve = std::atoi(e) != 0;
+  if (const char* e = std::getenv("DYNOHIP_RED_BLOCKS")) s->red_blocks_env = std::atoi(e) != 0;
   s->stream = r.stream;
   s->side = r.side;
   s->ev_main = r.ev_main;

@@ -1261,6 +1261,27 @@ def test_mixed_lone_points_conditioned(gpu_available):
         assert rel(s.values_data(), o.values_data()) < PER_ITER_TOL, it
 
 
+@pytest.mark.parametrize("name", ["C2", "NS"])
+def test_reduced_gather_block_order_is_bit_identical(gpu_available, monkeypatch, name):
+    """k_gather_reduced's band blocks in column order (Plan::red_blocks)
+    against each entry-count class's blocks in turn (DYNOHIP_RED_BLOCKS=0):
+    every target is summed by the same lanes in the same order, only the
+    workgroup that does it moves, so the LM run is bit-identical."""
+    g, v, _ = synth.generate(name)
+    out = []
+    for on in ("0", "1"):
+        monkeypatch.setenv("DYNOHIP_RED_BLOCKS", on)
+        s = Solver(0)
+        s.set_graph(g)
+        s.set_values(v)
+        sm = s.optimize()
+        out.append((sm.iterations, sm.inner_iterations, sm.final_error, s.values_data()))
+        s.close()
+    (ia, na, ea, va), (ib, nb, eb, vb) = out
+    assert (ia, na, ea) == (ib, nb, eb)
+    assert np.array_equal(va, vb)
+
+
 def test_queue_order_is_bit_identical(gpu_available, monkeypatch):
     """The dataflow factorisation's queue order (list-scheduled by default,
     DYNOHIP_QUEUE_ORDER=level for the schedule's level order) changes only
