@@ -957,12 +957,18 @@ __device__ __forceinline__ void lone_point_block(const PointGatherDev& pg, int g
   }
 }
 
+// The D, g_p and W targets of the same points read the same factor records
+// (J_p, then J_p with b, then J_p with J_x): each list's range starts at a
+// multiple of 8 blocks and is remapped with xcd_block, so the blocks of one
+// point range land on one XCD in every list and share the records in its L2
+// (they ran on different XCDs, each fetching them).
 __global__ __launch_bounds__(kBlock) void k_gather_point(PointGatherDev p, const double* __restrict__ arena) {
   const int b = blockIdx.x;
-  if (b < p.bstart[1]) gather_thread<3, 3>(p.g[0], b, arena, p.dst[0]);
-  else if (b < p.bstart[2]) gather_thread<3, 3>(p.g[1], b - p.bstart[1], arena, p.dst[1]);
-  else if (b < p.bstart[3]) gather_thread<3, 1>(p.g[2], b - p.bstart[2], arena, p.dst[2]);
-  else if (b < p.bstart[4]) gather_thread<3, 6>(p.g[3], b - p.bstart[3], arena, p.dst[3]);
+  auto at = [&](int k) { return xcd_block(b - p.bstart[k], p.bstart[k + 1] - p.bstart[k]); };
+  if (b < p.bstart[1]) gather_thread<3, 3>(p.g[0], at(0), arena, p.dst[0]);
+  else if (b < p.bstart[2]) gather_thread<3, 3>(p.g[1], at(1), arena, p.dst[1]);
+  else if (b < p.bstart[3]) gather_thread<3, 1>(p.g[2], at(2), arena, p.dst[2]);
+  else if (b < p.bstart[4]) gather_thread<3, 6>(p.g[3], at(3), arena, p.dst[3]);
   else lone_point_block(p, b - p.bstart[4], arena);
 }
 
@@ -2449,7 +2455,7 @@ void launch_gather_point(const GatherDev (&g)[4], double* const (&dst)[4], const
   for (int k = 0; k < 4; ++k) {
     p.g[k] = g[k];
     p.dst[k] = dst[k];
-    p.bstart[k + 1] = p.bstart[k] + nblocks(g[k].n);
+    p.bstart[k + 1] = p.bstart[k] + (nblocks(g[k].n) + 7) / 8 * 8;   // (XCD-aligned ranges, k_gather_point)
   }
   p.n_lone = n_lone;
   p.lone_blk = lone_blk;
