@@ -409,11 +409,12 @@ def test_free_running_optimize(gpu_available, name, kw):
         assert ome >= 0.5 * PER_ITER_TOL, (vr, ge, ome)
 
 
-@pytest.mark.parametrize("name,kw", [("T2", {}), ("C1", {}), ("T2", {"robust": 0})])
-@pytest.mark.parametrize("seed", [1, 2, 3, 7])
+@pytest.mark.parametrize("name,kw,seed", [(n, k, sd) for n, k in (("T2", {}), ("C1", {}), ("T2", {"robust": 0}))
+                                          for sd in (1, 2, 3, 7)] + [("C2", {}, 1), ("C2", {}, 2)])
 def test_free_running_seed_sweep(gpu_available, name, kw, seed):
     """The free-running LM of test_free_running_optimize on other synthetic
-    draws (seeds other than the configs' 42, with and without Huber): the
+    draws (seeds other than the configs' 42, with and without Huber; C2,
+    the bench workload, on two of them): the
     same iteration and inner-iteration counts, accept / lambda sequence and
     final error as the oracle, and the end values within the per-iterate bar
     of the oracle's (or, where the oracle itself is that far off, of the
