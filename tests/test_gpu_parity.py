@@ -150,10 +150,11 @@ def test_per_iteration_parity_conditioned(gpu_available, name, kw, iters):
     the Pose3 logmap's sin / tan / acos come from the shared trig.h), so
     what differs is the linear solve's summation order.
     Also on two other draws (C1 seed 3, C2 seed 1). Not C2 with Gaussian
-    noise: at lambda 1e-8 its damped system is conditioned so that a
-    double-precision solve's step moves the next error by ~13 % between
-    summation orders (test_free_running_c2_gaussian_follows_exact_step
-    compares that run with the exact-step one instead)."""
+    noise: at lambda 1e-8 its damped system is conditioned so that the
+    GPU's and the oracle's double-precision steps from the same values
+    leave errors 13 % apart (and the oracle's two summation orders differ
+    too; test_free_running_c2_gaussian_follows_exact_step compares that
+    run with the exact-step one instead)."""
     g, v, _, s = make(name, **kw)
     o = Oracle(g, v, threads=cores())
     s.reset()
