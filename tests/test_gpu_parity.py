@@ -737,8 +737,8 @@ def gauge_split(values, dg, do):
     return (np.linalg.norm(rest) / nd if nd > 0 else 0.0), nd
 
 
-@pytest.mark.parametrize("name,iters", [("T2", 8), ("C1", 6)])
-def test_llworld_per_iteration_conditioned(gpu_available, name, iters):
+@pytest.mark.parametrize("name,iters,kw", [("T2", 8, {}), ("C1", 6, {}), ("T2", 8, {"seed": 3}), ("C1", 6, {"seed": 7})])
+def test_llworld_per_iteration_conditioned(gpu_available, name, iters, kw):
     """LLWorld (WorldPoseFormulation) per LM iteration, conditioned: before
     every iteration the oracle is put on the GPU's values AND lambda.
     L_k -> L_k G changes no factor but the smoothing ones (their twist is
@@ -763,7 +763,7 @@ def test_llworld_per_iteration_conditioned(gpu_available, name, iters):
     1/eps, each side is measured from the exact step (x87 extended
     precision) and the GPU held within 4x the oracle's own distance; object
     motions 1e-5 or more apart likewise (C2's weakly pinned gauge)."""
-    g, v, _, s = make(name, formulation=1)
+    g, v, _, s = make(name, formulation=1, **kw)
     o = Oracle(g, v)
     p = Solver(0)   # probe handle for the steps of a divergent try
     p.set_graph(g)
